@@ -1,0 +1,74 @@
+"""Pin the CPU oracle (oracle/) against golden vectors produced by the REFERENCE's own Python
+(tests/golden/make_golden.py imports model_definition.py, nano_ctc.py, text_merge.py, gguf quants)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import ctc, encoder as en, q8, qwen3, synth
+
+# experience/03 ONNX_Export_Optimization_Experience.md:68-73: fp32 max-abs ~1e-5..1e-4, cosine >= 0.999999
+ENC_ATOL = 1e-4
+ENC_COS = 0.999999
+
+
+def _cos(a, b):
+    return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+
+
+@pytest.mark.parametrize("tag,cfgname", [("tiny_3s", "ENC_TINY"), ("tiny_pad2s", "ENC_TINY"), ("full_10s", "ENC_FULL")])
+def test_encoder_matches_reference(tag, cfgname):
+    cfg = getattr(synth, cfgname)
+    g = np.load(os.path.join(GOLDEN, f"encoder_{tag}.npz"))
+    W = synth.make_weights(synth.encoder_tensors(cfg))
+    taps = {}
+    r = en.encode(g["audio"], W, cfg, valid=int(g["valid"]), taps=taps)
+    # log-mel LFR features: relative tolerance (log amplifies the f32 DFT rounding of near-silent bins)
+    assert np.abs(taps["lfr"] - g["lfr"]).max() <= 1e-4 * np.abs(g["lfr"]).max()
+    e = r["enc"][: g["enc"].shape[0]]
+    assert np.abs(e - g["enc"]).max() <= ENC_ATOL and _cos(e, g["enc"]) >= ENC_COS
+    assert r["counts"]["target_len"] == int(g["target_len"])
+    assert np.abs(r["audio_embd"] - g["adaptor"]).max() <= ENC_ATOL
+    tv = int(g["t_lfr_valid"])
+    ids = en.ctc_logits(r["enc"][:tv], W, cfg).argmax(-1)
+    nontie = g["ctc_margin"] > 1e-3
+    assert ((ids != g["ctc_ids"]) & nontie).sum() == 0
+
+
+def test_ctc_align_merge_match_reference():
+    G = json.load(open(os.path.join(GOLDEN, "ctc_align_merge.json"), encoding="utf-8"))
+    id2 = {int(k): v for k, v in G["id2token"].items()}
+    for c in G["decode"]:
+        t, res = ctc.decode_ctc(c["ids"], id2)
+        assert t == c["text"] and [[a, b] for a, b in res] == c["tokens"]
+    for c in G["align"]:
+        assert ctc.align_timestamps([tuple(x) for x in c["ctc"]], c["llm"]) == c["aligned"]
+    for c in G["merge"]:
+        t, s = ctc.merge_results(c["results"], c["offsets"], c["overlap"])
+        assert t == c["text"] and s == c["segments"]
+
+
+def test_q8_0_bit_exact_vs_vendored_gguf():
+    g = np.load(os.path.join(GOLDEN, "q8_0.npz"))
+    d, q = q8.quantize_q8_0(g["x"])
+    assert (q8.pack_q8_0(d, q) == g["q8_bytes"]).all()
+    assert (q8.dequant_f32(d, q) == g["deq"]).all()
+    d, q = q8.quantize_q8_0(g["emb"])
+    assert (q8.dequant_numpy_f16(d, q) == g["emb_table"]).all()  # llama.py:778-784 fp16 rounding
+
+
+def test_qwen3_oracle_anchored_on_hf():
+    """Decoder restatement vs HF Qwen3 on the same q8_0-dequantised weights. The oracle quantises
+    activations to q8_0 (ggml integer dot), HF does not -> tolerance: per-row cosine >= 0.999,
+    argmax agreement >= 90 %, and the greedy continuation identical."""
+    h = np.load(os.path.join(GOLDEN, "qwen3_tiny_hf.npz"))
+    cfg = synth.LLM_TINY
+    m = qwen3.Qwen3Q8(synth.make_weights(synth.llm_tensors(cfg)), cfg, n_ctx=64)
+    lg = m.forward(h["prompt"], 0, all_logits=True)
+    ref = h["logits"]
+    cos = (lg * ref).sum(-1) / np.linalg.norm(lg, axis=-1) / np.linalg.norm(ref, axis=-1)
+    assert cos.min() >= 0.999
+    assert (lg.argmax(-1) == ref.argmax(-1)).mean() >= 0.9
+    assert m.greedy(h["prompt"], 6) == list(h["greedy"])
