@@ -1,0 +1,212 @@
+// Encoder-side memory-bound kernels: frontend (F1, F4), LayerNorm (E1 + E5 mask sweep),
+// FSMN depthwise memory (E4), and the wavefront CTC greedy collapse (C2).
+#include "common.h"
+#include "kernels.h"
+
+namespace fa {
+
+// ---------------- F1: mean over valid samples (model_definition.py:277-278), partial sums per block
+constexpr int MEAN_PARTS = 64;
+
+__global__ void k_mean_partial(const float* __restrict__ pcm, int64_t stride, const int64_t* __restrict__ n_samples,
+                               float* __restrict__ partial) {
+  const int b = blockIdx.y, p = blockIdx.x;
+  const int64_t n = n_samples[b];
+  const int64_t chunk = (n + MEAN_PARTS - 1) / MEAN_PARTS;
+  const int64_t lo = p * chunk, hi = min(n, lo + chunk);
+  const float* x = pcm + b * stride;
+  float acc = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += x[i];
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[b * MEAN_PARTS + p] = red[0] + red[1] + red[2] + red[3];
+}
+
+// pre-emphasis into the 200/200 zero-padded STFT input xp[b][0 .. xp_stride) (model_definition.py:279-282, 255)
+__global__ void k_preemph_pad(const float* __restrict__ pcm, int64_t stride, const int64_t* __restrict__ n_samples,
+                              const float* __restrict__ partial, float* __restrict__ xp, int64_t xp_stride) {
+  const int b = blockIdx.y;
+  __shared__ float s_mean;
+  if (threadIdx.x < 64) {
+    float v = threadIdx.x < MEAN_PARTS ? partial[b * MEAN_PARTS + threadIdx.x] : 0.f;
+    v = wave_sum(v);
+    if (threadIdx.x == 0) s_mean = v / (float)n_samples[b];
+  }
+  __syncthreads();
+  const float mean = s_mean;
+  const int64_t n = n_samples[b];
+  const float* x = pcm + b * stride;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < xp_stride; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = i - 200;
+    float v = 0.f;
+    if (t >= 0 && t < n) {
+      float a = x[t] - mean;
+      v = t == 0 ? a : a - 0.97f * (x[t - 1] - mean);
+    }
+    xp[b * xp_stride + i] = v;
+  }
+}
+
+void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,
+                      float* xp, int64_t xp_stride, hipStream_t s) {
+  hipLaunchKernelGGL(k_mean_partial, dim3(MEAN_PARTS, batch), dim3(256), 0, s, pcm, stride, d_n_samples, partial);
+  hipLaunchKernelGGL(k_preemph_pad, dim3(cdiv(xp_stride, 256 * 8), batch), dim3(256), 0, s, pcm, stride, d_n_samples,
+                     partial, xp, xp_stride);
+}
+
+// ---------------- F4: LFR (m=7, n=6) with replicate padding, mask, x*sqrt(512) + PE (model_definition.py:290-311, 206)
+// x[b, i, j*80 + c] = mel[b, clamp(6i + j - 3, 0, t_mel_valid-1), c] for i < t_lfr_valid else 0; then *22.627417 + pe[i].
+__global__ void k_lfr_pe(const float* __restrict__ mel, int mel_stride, const int* __restrict__ t_mel_valid,
+                         const int* __restrict__ t_lfr_valid, const float* __restrict__ pe, float* __restrict__ x,
+                         int t_stride, int n_mels, int lfr_m, int lfr_n) {
+  const int b = blockIdx.y;
+  const int d_in = n_mels * lfr_m;
+  const int64_t total = (int64_t)t_stride * d_in;
+  const int tmv = t_mel_valid[b], tlv = t_lfr_valid[b];
+  const float sq = 22.627416997969522f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int i = (int)(e / d_in), jc = (int)(e - (int64_t)i * d_in);
+    int j = jc / n_mels, c = jc - j * n_mels;
+    float v = 0.f;
+    if (i < tlv) {
+      int p = i * lfr_n + j - (lfr_m - 1) / 2;
+      p = p < 0 ? 0 : (p > tmv - 1 ? tmv - 1 : p);
+      v = mel[((int64_t)b * mel_stride + p) * n_mels + c];
+    }
+    x[((int64_t)b * t_stride + i) * d_in + jc] = v * sq + pe[(int64_t)i * d_in + jc];
+  }
+}
+
+void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, const int* t_lfr_valid, const float* pe,
+                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s) {
+  int64_t total = (int64_t)t_stride * n_mels * lfr_m;
+  hipLaunchKernelGGL(k_lfr_pe, dim3(std::min(cdiv(total, 256), 4096), batch), dim3(256), 0, s, mel, mel_stride,
+                     t_mel_valid, t_lfr_valid, pe, x, t_stride, n_mels, lfr_m, lfr_n);
+}
+
+// ---------------- E1: LayerNorm, one wave per row, optional row-mask sweep (model_definition.py:209-213)
+template <int PER>
+__global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
+                            const float* __restrict__ w, const float* __restrict__ bb, int rows, int D, float eps,
+                            const int* __restrict__ lens, int t_stride) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    v[i] = c < D ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    float dv = c < D ? v[i] - mean : 0.f;
+    q += dv * dv;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+  float mk = 1.0f;
+  if (lens) {
+    int b = row / t_stride, t = row - b * t_stride;
+    mk = t < lens[b] ? 1.0f : 0.0f;
+  }
+  float* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + i * 64;
+    if (c < D) yr[c] = ((v[i] - mean) * rstd * w[c] + bb[c]) * mk;
+  }
+}
+
+void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
+               float eps, const int* lens, int t_stride, hipStream_t s) {
+  dim3 grid(cdiv(rows, 4));
+  if (D <= 512) hipLaunchKernelGGL(k_layernorm<8>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
+  else if (D <= 640) hipLaunchKernelGGL(k_layernorm<10>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
+  else if (D <= 1024) hipLaunchKernelGGL(k_layernorm<16>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
+  else FA_REQUIRE(false, "layernorm: D > 1024");
+}
+
+// ---------------- E4: FSMN memory = depthwise conv_k(v*m) (zero pad (k-1)/2) + v*m (model_definition.py:60-66)
+__global__ void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w, float* __restrict__ out,
+                       int64_t ldo, int rows, int C, int ksize, const int* __restrict__ lens, int t_stride) {
+  const int64_t total = (int64_t)rows * C;
+  const int lp = (ksize - 1) / 2;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int row = (int)(e / C), c = (int)(e - (int64_t)row * C);
+    int b = row / t_stride, t = row - b * t_stride;
+    int len = lens ? lens[b] : t_stride;
+    float acc = 0.f;
+    for (int j = 0; j < ksize; ++j) {
+      int tt = t + j - lp;
+      float xv = (tt >= 0 && tt < len && tt < t_stride) ? v[((int64_t)b * t_stride + tt) * ldv + c] : 0.f;
+      acc += w[c * ksize + j] * xv;
+    }
+    float self = t < len ? v[(int64_t)row * ldv + c] : 0.f;
+    out[(int64_t)row * ldo + c] = acc + self;
+  }
+}
+
+void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
+          const int* lens, int t_stride, hipStream_t s) {
+  int64_t total = (int64_t)rows * C;
+  hipLaunchKernelGGL(k_fsmn, dim3(std::min(cdiv(total, 256), 8192)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
+                     ksize, lens, t_stride);
+}
+
+// ---------------- C2: CTC greedy collapse (nano_ctc.py:65-104): keep frame i iff id != blank and
+// (i == 0 or id != id[i-1]); block-wide ballot + prefix sum compaction, one block per clip.
+__global__ void k_ctc_collapse(const int* __restrict__ ids, int64_t ids_stride, const int* __restrict__ lens, int blank,
+                               int* __restrict__ out_ids, int* __restrict__ out_frames, int64_t out_stride,
+                               int* __restrict__ n_out) {
+  const int b = blockIdx.x;
+  const int n = lens[b];
+  const int* x = ids + (int64_t)b * ids_stride;
+  __shared__ int wave_cnt[16];
+  __shared__ int base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c0 = 0; c0 < n; c0 += blockDim.x) {
+    int i = c0 + threadIdx.x;
+    bool keep = false;
+    int id = 0;
+    if (i < n) {
+      id = x[i];
+      keep = id != blank && (i == 0 || x[i - 1] != id);
+    }
+    unsigned long long bal = __ballot(keep);
+    int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[wave] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wave_cnt[w];
+    if (keep) {
+      out_ids[(int64_t)b * out_stride + off + pre] = id;
+      out_frames[(int64_t)b * out_stride + off + pre] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int w = 0; w < nw; ++w) tot += wave_cnt[w];
+      base += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) n_out[b] = base;
+}
+
+void ctc_collapse(const int* ids, int64_t ids_stride, const int* lens, int batch, int blank, int* out_ids,
+                  int* out_frames, int64_t out_stride, int* n_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_ctc_collapse, dim3(batch), dim3(1024), 0, s, ids, ids_stride, lens, blank, out_ids, out_frames,
+                     out_stride, n_out);
+}
+
+}  // namespace fa

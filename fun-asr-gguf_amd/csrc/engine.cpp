@@ -1,0 +1,1125 @@
+// libfunasr_hip: C-ABI engine for the Fun-ASR hot path on MI355X (see include/funasr_hip.h).
+//
+// Owns, per GPU: all weights (encoder f32, decoder q8_0 in engine layout), activation arenas sized
+// for max_batch x max_samples, the fp16 KV cache [layer][seq][n_ctx][kv*128], one HIP stream.
+// Encoder math follows model_definition.py (SenseVoiceEncoderSmall / CorrectTransformerAdaptor /
+// CTC head); decoder math follows llama.cpp's qwen3 graph with ggml q8_0 numerics (oracle/qwen3.py).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/funasr_hip.h"
+#include "common.h"
+#include "gguf.h"
+#include "kernels.h"
+
+namespace fa {
+
+static thread_local std::string g_err;
+static void (*g_log_cb)(int32_t, const char*, void*) = nullptr;
+static void* g_log_ud = nullptr;
+
+void set_error(const std::string& m) {
+  g_err = m;
+  log(2, m);
+}
+void log(int level, const std::string& m) {
+  if (g_log_cb) g_log_cb(level, m.c_str(), g_log_ud);
+}
+
+static uint32_t fnv1a32(const std::string& s) {
+  uint32_t h = 0x811C9DC5u;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 0x01000193u;
+  }
+  return h;
+}
+static uint32_t lowbias32_h(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------------
+struct Slot {
+  int kind = 0;  // 0 f32 encoder/norm tensor, 1 q8_0 decoder matrix rows
+  float* f = nullptr;
+  int8_t* q = nullptr;
+  __half* d = nullptr;
+  int64_t n = 0;      // elements
+  int64_t rows = 0, cols = 0;
+  float scale = 0.f, offset = 0.f;  // synthetic spec
+  bool set = false;
+};
+
+struct EncBlockW {
+  const float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *qkv_w, *qkv_b, *out_w, *out_b, *fsmn_w, *w1, *b1, *w2, *b2;
+  int d_in;
+};
+struct AdBlockW {
+  const float *ln1_w, *ln1_b, *ln2_w, *ln2_b, *qkv_w, *qkv_b, *o_w, *o_b, *w1, *b1, *w2, *b2;
+};
+struct AdaptorW {
+  const float *l1_w, *l1_b, *l2_w, *l2_b;
+  std::vector<AdBlockW> blocks;
+};
+struct Q8Mat {
+  int8_t* q = nullptr;
+  __half* d = nullptr;
+};
+struct LlmLayerW {
+  Q8Mat qkv, o, gate, up, down;
+  float *attn_norm, *ffn_norm, *q_norm, *k_norm;
+};
+
+struct Engine {
+  int device = 0;
+  fa_encoder_config ec{};
+  fa_llm_config lc{};
+  int max_batch = 1;
+  int64_t max_samples = 0;
+  hipStream_t stream = nullptr;
+  std::vector<void*> allocs;
+  std::unordered_map<std::string, Slot> slots;
+  std::vector<std::string> spec_order;
+
+  // encoder weights
+  std::vector<EncBlockW> enc_blocks;  // encoders0 + encoders + tp_encoders
+  const float *after_w, *after_b, *tp_w, *tp_b;
+  AdaptorW adaptor, ctc_dec;
+  const float *ctc_w, *ctc_b;
+  // frontend constants
+  float *basis = nullptr, *fbank = nullptr, *pe = nullptr;
+  // encoder arenas
+  int tm_max = 0, tl_max = 0, R = 0;
+  int64_t xp_stride_max = 0;
+  float *d_pcm = nullptr, *xp = nullptr, *mean_part = nullptr, *power = nullptr, *mel = nullptr;
+  float *xa = nullptr, *hbuf = nullptr, *qkv = nullptr, *att = nullptr, *mem = nullptr, *ffn = nullptr;
+  float *enc = nullptr, *ad = nullptr, *cbuf = nullptr, *ctc_pval = nullptr;
+  int *ctc_pidx = nullptr, *ctc_ids = nullptr;
+  int64_t* d_nsamp = nullptr;
+  int *d_tmel = nullptr, *d_tlfr = nullptr, *d_tgt = nullptr, *d_ctclen = nullptr;
+  int *d_col_ids = nullptr, *d_col_frames = nullptr, *d_col_n = nullptr;
+  int debug_flags = 0;
+  float* tap_lfr = nullptr;
+  // last encode geometry
+  int last_batch = 0, last_tstride = 0;
+  std::vector<int> h_tlfr, h_tgt, h_ctclen;
+
+  // decoder
+  std::vector<LlmLayerW> layers;
+  Q8Mat tok_embd;
+  float* out_norm = nullptr;
+  float *rcos = nullptr, *rsin = nullptr;
+  __half *kcache = nullptr, *vcache = nullptr;
+  int64_t seq_stride = 0, layer_stride = 0;
+  int m_max = 0, n_part = 0;
+  float *lx = nullptr, *lqkv = nullptr, *lq = nullptr, *latt = nullptr, *lact = nullptr, *logits = nullptr;
+  int8_t* lxq = nullptr;
+  float* lxd = nullptr;
+  float* pval = nullptr;
+  int* pidx = nullptr;
+  int *d_tok_seq = nullptr, *d_tok_pos = nullptr, *d_step = nullptr, *d_tok_cur = nullptr, *d_tok_hist = nullptr,
+      *d_ids = nullptr;
+  int hist_max = 0;
+  std::vector<int> n_past, last_tok, logits_row;
+
+  // profiling
+  bool prof = false;
+  struct ProfCls {
+    double ms = 0, bytes = 0, flops = 0;
+    int64_t launches = 0;
+  } pcls[4];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  struct Pending {
+    int cls;
+    hipEvent_t a, b;
+    double bytes, flops;
+  };
+  std::vector<Pending> pending;
+  size_t ev_next = 0;
+
+  template <class T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    FA_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    allocs.push_back(p);
+    return (T*)p;
+  }
+  ~Engine() {
+    if (stream) hipStreamSynchronize(stream);
+    for (auto& e : ev_pool) {
+      hipEventDestroy(e.first);
+      hipEventDestroy(e.second);
+    }
+    for (void* p : allocs) hipFree(p);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  // ---- profiling helpers: bracket launches of class `cls` with events on the engine stream
+  void prof_begin(int cls, hipEvent_t* a) {
+    if (!prof) return;
+    if (ev_next >= ev_pool.size()) {
+      hipEvent_t x, y;
+      FA_HIP(hipEventCreate(&x));
+      FA_HIP(hipEventCreate(&y));
+      ev_pool.push_back({x, y});
+    }
+    *a = ev_pool[ev_next].first;
+    FA_HIP(hipEventRecord(*a, stream));
+    (void)cls;
+  }
+  void prof_end(int cls, double bytes, double flops) {
+    if (!prof) return;
+    hipEvent_t a = ev_pool[ev_next].first, b = ev_pool[ev_next].second;
+    FA_HIP(hipEventRecord(b, stream));
+    pending.push_back({cls, a, b, bytes, flops});
+    ev_next++;
+  }
+  void prof_collect() {
+    if (pending.empty()) return;
+    FA_HIP(hipStreamSynchronize(stream));
+    for (auto& p : pending) {
+      float ms = 0;
+      FA_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+      pcls[p.cls].ms += ms;
+      pcls[p.cls].bytes += p.bytes;
+      pcls[p.cls].flops += p.flops;
+      pcls[p.cls].launches++;
+    }
+    pending.clear();
+    ev_next = 0;
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  void add_f32(const std::string& name, int64_t n, float scale, float offset, float* dst) {
+    Slot s;
+    s.kind = 0;
+    s.f = dst;
+    s.n = n;
+    s.scale = scale;
+    s.offset = offset;
+    slots[name] = s;
+    spec_order.push_back(name);
+  }
+  float* f32_tensor(const std::string& name, int64_t n, float scale, float offset) {
+    float* p = alloc<float>(n);
+    add_f32(name, n, scale, offset, p);
+    return p;
+  }
+  void add_q8(const std::string& name, int64_t rows, int64_t cols, float scale, int8_t* q, __half* d) {
+    Slot s;
+    s.kind = 1;
+    s.q = q;
+    s.d = d;
+    s.rows = rows;
+    s.cols = cols;
+    s.n = rows * cols;
+    s.scale = scale;
+    slots[name] = s;
+    spec_order.push_back(name);
+  }
+
+  static float lin_scale(int n_in) { return (float)std::sqrt(3.0 / n_in); }
+
+  void lin(const std::string& p, int n_in, int n_out, float* w, float* b) {
+    add_f32(p + ".weight", (int64_t)n_in * n_out, lin_scale(n_in), 0.f, w);
+    if (b) add_f32(p + ".bias", n_out, 0.02f, 0.f, b);
+  }
+
+  EncBlockW sanm_block(const std::string& p, int d_in) {
+    const int d = ec.d_model, f = ec.d_ffn, k = ec.fsmn_k;
+    EncBlockW w{};
+    w.d_in = d_in;
+    w.ln1_w = f32_tensor(p + ".norm1.weight", d_in, 0.1f, 1.0f);
+    w.ln1_b = f32_tensor(p + ".norm1.bias", d_in, 0.02f, 0.f);
+    w.ln2_w = f32_tensor(p + ".norm2.weight", d, 0.1f, 1.0f);
+    w.ln2_b = f32_tensor(p + ".norm2.bias", d, 0.02f, 0.f);
+    float* qw = alloc<float>((size_t)3 * d * d_in);
+    float* qb = alloc<float>(3 * d);
+    lin(p + ".self_attn.linear_q_k_v", d_in, 3 * d, qw, qb);
+    w.qkv_w = qw;
+    w.qkv_b = qb;
+    float* ow = alloc<float>((size_t)d * d);
+    float* ob = alloc<float>(d);
+    lin(p + ".self_attn.linear_out", d, d, ow, ob);
+    w.out_w = ow;
+    w.out_b = ob;
+    w.fsmn_w = f32_tensor(p + ".self_attn.fsmn_block.weight", (int64_t)d * k, (float)(std::sqrt(3.0 / k) * 0.5), 0.f);
+    float* w1 = alloc<float>((size_t)f * d);
+    float* b1 = alloc<float>(f);
+    lin(p + ".feed_forward.w_1", d, f, w1, b1);
+    float* w2 = alloc<float>((size_t)d * f);
+    float* b2 = alloc<float>(d);
+    lin(p + ".feed_forward.w_2", f, d, w2, b2);
+    w.w1 = w1;
+    w.b1 = b1;
+    w.w2 = w2;
+    w.b2 = b2;
+    return w;
+  }
+
+  AdaptorW adaptor_w(const std::string& p, int d_enc, int d_out, int d_ffn, int n_blocks) {
+    AdaptorW a;
+    float* l1w = alloc<float>((size_t)d_ffn * d_enc);
+    float* l1b = alloc<float>(d_ffn);
+    lin(p + ".linear1", d_enc, d_ffn, l1w, l1b);
+    float* l2w = alloc<float>((size_t)d_out * d_ffn);
+    float* l2b = alloc<float>(d_out);
+    lin(p + ".linear2", d_ffn, d_out, l2w, l2b);
+    a.l1_w = l1w;
+    a.l1_b = l1b;
+    a.l2_w = l2w;
+    a.l2_b = l2b;
+    for (int b = 0; b < n_blocks; ++b) {
+      std::string q = p + ".blocks." + std::to_string(b);
+      AdBlockW w{};
+      // linear_q/k/v are stored concatenated [3*d_out][d_out] so one GEMM produces q|k|v
+      float* qkvw = alloc<float>((size_t)3 * d_out * d_out);
+      float* qkvb = alloc<float>(3 * d_out);
+      const char* nm[3] = {"linear_q", "linear_k", "linear_v"};
+      for (int i = 0; i < 3; ++i)
+        lin(q + ".self_attn." + nm[i], d_out, d_out, qkvw + (size_t)i * d_out * d_out, qkvb + i * d_out);
+      w.qkv_w = qkvw;
+      w.qkv_b = qkvb;
+      float* ow = alloc<float>((size_t)d_out * d_out);
+      float* ob = alloc<float>(d_out);
+      lin(q + ".self_attn.linear_out", d_out, d_out, ow, ob);
+      w.o_w = ow;
+      w.o_b = ob;
+      float* w1 = alloc<float>((size_t)(d_out / 4) * d_out);
+      float* b1 = alloc<float>(d_out / 4);
+      lin(q + ".feed_forward.w_1", d_out, d_out / 4, w1, b1);
+      float* w2 = alloc<float>((size_t)d_out * (d_out / 4));
+      float* b2 = alloc<float>(d_out);
+      lin(q + ".feed_forward.w_2", d_out / 4, d_out, w2, b2);
+      w.w1 = w1;
+      w.b1 = b1;
+      w.w2 = w2;
+      w.b2 = b2;
+      w.ln1_w = f32_tensor(q + ".norm1.weight", d_out, 0.1f, 1.0f);
+      w.ln1_b = f32_tensor(q + ".norm1.bias", d_out, 0.02f, 0.f);
+      w.ln2_w = f32_tensor(q + ".norm2.weight", d_out, 0.1f, 1.0f);
+      w.ln2_b = f32_tensor(q + ".norm2.bias", d_out, 0.02f, 0.f);
+      a.blocks.push_back(w);
+    }
+    return a;
+  }
+
+  void build_encoder() {
+    const int d = ec.d_model;
+    enc_blocks.push_back(sanm_block("audio_encoder.encoders0.0", ec.d_in));
+    for (int i = 0; i < ec.n_blocks - 1; ++i) enc_blocks.push_back(sanm_block("audio_encoder.encoders." + std::to_string(i), d));
+    for (int i = 0; i < ec.n_tp_blocks; ++i)
+      enc_blocks.push_back(sanm_block("audio_encoder.tp_encoders." + std::to_string(i), d));
+    after_w = f32_tensor("audio_encoder.after_norm.weight", d, 0.1f, 1.0f);
+    after_b = f32_tensor("audio_encoder.after_norm.bias", d, 0.02f, 0.f);
+    tp_w = f32_tensor("audio_encoder.tp_norm.weight", d, 0.1f, 1.0f);
+    tp_b = f32_tensor("audio_encoder.tp_norm.bias", d, 0.02f, 0.f);
+    adaptor = adaptor_w("audio_adaptor", d, ec.d_llm, ec.adaptor_ffn, ec.adaptor_blocks);
+    ctc_dec = adaptor_w("ctc_decoder", d, d, ec.ctc_ffn, ec.ctc_blocks);
+    float* cw = alloc<float>((size_t)ec.ctc_vocab * d);
+    float* cb = alloc<float>(ec.ctc_vocab);
+    lin("ctc_proj.ctc_lo", d, ec.ctc_vocab, cw, cb);
+    ctc_w = cw;
+    ctc_b = cb;
+  }
+
+  Q8Mat q8mat(int64_t rows, int64_t cols) {
+    Q8Mat m;
+    m.q = alloc<int8_t>((size_t)rows * cols);
+    m.d = alloc<__half>((size_t)rows * cols / 32);
+    return m;
+  }
+
+  void build_llm() {
+    const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
+    tok_embd = q8mat(lc.n_vocab, E);
+    add_q8("token_embd.weight", lc.n_vocab, E, 0.05f, tok_embd.q, tok_embd.d);
+    for (int l = 0; l < lc.n_layer; ++l) {
+      std::string b = "blk." + std::to_string(l) + ".";
+      LlmLayerW w{};
+      w.attn_norm = f32_tensor(b + "attn_norm.weight", E, 0.1f, 1.0f);
+      w.qkv = q8mat((int64_t)(H + 2 * KV) * D, E);
+      add_q8(b + "attn_q.weight", (int64_t)H * D, E, lin_scale(E), w.qkv.q, w.qkv.d);
+      add_q8(b + "attn_k.weight", (int64_t)KV * D, E, lin_scale(E), w.qkv.q + (size_t)H * D * E,
+             w.qkv.d + (size_t)H * D * E / 32);
+      add_q8(b + "attn_v.weight", (int64_t)KV * D, E, lin_scale(E), w.qkv.q + (size_t)(H + KV) * D * E,
+             w.qkv.d + (size_t)(H + KV) * D * E / 32);
+      w.q_norm = f32_tensor(b + "attn_q_norm.weight", D, 0.1f, 1.0f);
+      w.k_norm = f32_tensor(b + "attn_k_norm.weight", D, 0.1f, 1.0f);
+      w.o = q8mat(E, (int64_t)H * D);
+      add_q8(b + "attn_output.weight", E, (int64_t)H * D, lin_scale(H * D), w.o.q, w.o.d);
+      w.ffn_norm = f32_tensor(b + "ffn_norm.weight", E, 0.1f, 1.0f);
+      w.gate = q8mat(F, E);
+      add_q8(b + "ffn_gate.weight", F, E, lin_scale(E), w.gate.q, w.gate.d);
+      w.up = q8mat(F, E);
+      add_q8(b + "ffn_up.weight", F, E, lin_scale(E), w.up.q, w.up.d);
+      w.down = q8mat(E, F);
+      add_q8(b + "ffn_down.weight", E, F, lin_scale(F), w.down.q, w.down.d);
+      layers.push_back(w);
+    }
+    out_norm = f32_tensor("output_norm.weight", E, 0.1f, 1.0f);
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // host constants (STFT basis, mel fbank, PE, RoPE) — same float32 formulas as oracle/frontend.py
+  static std::vector<float> linspace_f32(float start, float end, int steps) {
+    std::vector<float> o(steps);
+    float step = (end - start) / (float)(steps - 1);
+    int half = steps / 2;
+    for (int i = 0; i < steps; ++i) o[i] = i < half ? start + step * (float)i : end - step * (float)(steps - i - 1);
+    return o;
+  }
+
+  void build_constants() {
+    const double PI = 3.14159265358979323846;
+    // STFT basis, rows interleaved (cos_f, -sin_f) [402][400]
+    std::vector<float> basis_h(402 * 400), win(400);
+    const float wstep = (float)(2.0 * PI / 400.0);
+    for (int n = 0; n < 400; ++n) win[n] = (float)std::cos((double)((float)n * wstep)) * -0.46f + 0.54f;
+    const float twopi = (float)(2.0 * PI);
+    for (int f = 0; f < 201; ++f)
+      for (int t = 0; t < 400; ++t) {
+        float om = ((twopi * (float)f) * (float)t) / 400.0f;
+        basis_h[(2 * f) * 400 + t] = (float)std::cos((double)om) * win[t];
+        basis_h[(2 * f + 1) * 400 + t] = -(float)std::sin((double)om) * win[t];
+      }
+    basis = alloc<float>(basis_h.size());
+    FA_HIP(hipMemcpy(basis, basis_h.data(), basis_h.size() * 4, hipMemcpyHostToDevice));
+    // HTK mel filterbank [80][204] (torchaudio melscale_fbanks(201, 20, 8000, 80, 16000, None, 'htk'))
+    std::vector<float> allf = linspace_f32(0.f, 8000.f, 201);
+    double mmin = 2595.0 * std::log10(1.0 + 20.0 / 700.0), mmax = 2595.0 * std::log10(1.0 + 8000.0 / 700.0);
+    std::vector<float> mp = linspace_f32((float)mmin, (float)mmax, 82), fp(82);
+    for (int i = 0; i < 82; ++i) fp[i] = 700.0f * ((float)std::pow(10.0, (double)(mp[i] / 2595.0f)) - 1.0f);
+    std::vector<float> fb(80 * 204, 0.f);
+    for (int j = 0; j < 201; ++j)
+      for (int i = 0; i < 80; ++i) {
+        float fd0 = fp[i + 1] - fp[i], fd1 = fp[i + 2] - fp[i + 1];
+        float down = (-1.0f * (fp[i] - allf[j])) / fd0;
+        float up = (fp[i + 2] - allf[j]) / fd1;
+        fb[i * 204 + j] = std::max(0.0f, std::min(down, up));
+      }
+    fbank = alloc<float>(fb.size());
+    FA_HIP(hipMemcpy(fbank, fb.data(), fb.size() * 4, hipMemcpyHostToDevice));
+    // sinusoidal PE [tl_max][d_in], positions 1..T (model_definition.py:13-28)
+    const int depth = ec.d_in, half = depth / 2;
+    std::vector<float> pe_h((size_t)tl_max * depth);
+    float inc = (float)std::log(10000.0f) / (float)(depth / 2.0 - 1.0);
+    std::vector<float> inv(half);
+    for (int i = 0; i < half; ++i) inv[i] = (float)std::exp((double)((float)i * -inc));
+    for (int t = 0; t < tl_max; ++t)
+      for (int i = 0; i < half; ++i) {
+        float st = (float)(t + 1) * inv[i];
+        pe_h[(size_t)t * depth + i] = (float)std::sin((double)st);
+        pe_h[(size_t)t * depth + half + i] = (float)std::cos((double)st);
+      }
+    pe = alloc<float>(pe_h.size());
+    FA_HIP(hipMemcpy(pe, pe_h.data(), pe_h.size() * 4, hipMemcpyHostToDevice));
+    // RoPE cos/sin [n_ctx][head_dim/2], ggml iterative f32 theta
+    const int hd = lc.head_dim / 2;
+    std::vector<float> c((size_t)lc.n_ctx * hd), sn((size_t)lc.n_ctx * hd);
+    const float ts = std::pow(lc.rope_theta, -2.0f / (float)lc.head_dim);
+    for (int p = 0; p < lc.n_ctx; ++p) {
+      float th = (float)p;
+      for (int i = 0; i < hd; ++i) {
+        c[(size_t)p * hd + i] = (float)std::cos((double)th);
+        sn[(size_t)p * hd + i] = (float)std::sin((double)th);
+        th = th * ts;
+      }
+    }
+    rcos = alloc<float>(c.size());
+    rsin = alloc<float>(sn.size());
+    FA_HIP(hipMemcpy(rcos, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+    FA_HIP(hipMemcpy(rsin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+  }
+
+  static int t_lfr_of(int64_t n) { return (int)(((n / 160 + 1) + 5) / 6); }
+
+  void build_arenas() {
+    const int64_t n_eff = std::max<int64_t>(max_samples, 16000);
+    tm_max = (int)(n_eff / 160 + 1);
+    tl_max = t_lfr_of(n_eff);
+    R = max_batch * tl_max;
+    xp_stride_max = ((int64_t)160 * (tm_max - 1) + 400 + 3) / 4 * 4;
+    const int d = ec.d_model;
+    d_pcm = alloc<float>((size_t)max_batch * n_eff);
+    xp = alloc<float>((size_t)max_batch * xp_stride_max);
+    mean_part = alloc<float>((size_t)max_batch * 64);
+    power = alloc<float>((size_t)max_batch * tm_max * 204);
+    mel = alloc<float>((size_t)max_batch * tm_max * ec.n_mels);
+    const int wmax = std::max({ec.d_in, ec.d_llm, d});
+    xa = alloc<float>((size_t)R * wmax);
+    hbuf = alloc<float>((size_t)R * wmax);
+    qkv = alloc<float>((size_t)R * 3 * std::max(d, ec.d_llm));
+    att = alloc<float>((size_t)R * std::max(d, ec.d_llm));
+    mem = alloc<float>((size_t)R * d);
+    ffn = alloc<float>((size_t)R * std::max({ec.d_ffn, ec.adaptor_ffn, ec.ctc_ffn}));
+    enc = alloc<float>((size_t)R * d);
+    ad = alloc<float>((size_t)R * ec.d_llm);
+    cbuf = alloc<float>((size_t)R * d);
+    const int nt = cdiv(ec.ctc_vocab, 64);
+    ctc_pval = alloc<float>((size_t)R * nt);
+    ctc_pidx = alloc<int>((size_t)R * nt);
+    ctc_ids = alloc<int>(R);
+    d_nsamp = alloc<int64_t>(max_batch);
+    d_tmel = alloc<int>(max_batch);
+    d_tlfr = alloc<int>(max_batch);
+    d_tgt = alloc<int>(max_batch);
+    d_ctclen = alloc<int>(max_batch);
+    d_col_ids = alloc<int>(R);
+    d_col_frames = alloc<int>(R);
+    d_col_n = alloc<int>(max_batch);
+    // decoder
+    const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim;
+    m_max = std::max(lc.n_ctx, lc.max_seqs);
+    seq_stride = (int64_t)lc.n_ctx * KV * D;
+    layer_stride = seq_stride * lc.max_seqs;
+    kcache = alloc<__half>((size_t)layer_stride * lc.n_layer);
+    vcache = alloc<__half>((size_t)layer_stride * lc.n_layer);
+    lx = alloc<float>((size_t)m_max * E);
+    lqkv = alloc<float>((size_t)m_max * (H + 2 * KV) * D);
+    lq = alloc<float>((size_t)m_max * H * D);
+    latt = alloc<float>((size_t)m_max * H * D);
+    lact = alloc<float>((size_t)m_max * lc.n_ff);
+    const int kmax = std::max({E, H * D, lc.n_ff});
+    lxq = alloc<int8_t>((size_t)m_max * kmax);
+    lxd = alloc<float>((size_t)m_max * kmax / 32);
+    logits = alloc<float>((size_t)lc.max_seqs * lc.n_vocab);
+    const int rpw = gemv_rows_per_wave(lc.n_vocab);
+    n_part = cdiv(lc.n_vocab, 4 * rpw) * 4;
+    pval = alloc<float>((size_t)lc.max_seqs * n_part);
+    pidx = alloc<int>((size_t)lc.max_seqs * n_part);
+    d_tok_seq = alloc<int>(m_max);
+    d_tok_pos = alloc<int>(m_max);
+    d_step = alloc<int>(m_max);
+    d_tok_cur = alloc<int>(lc.max_seqs);
+    hist_max = 4096;
+    d_tok_hist = alloc<int>((size_t)lc.max_seqs * hist_max);
+    d_ids = alloc<int>(m_max);
+    n_past.assign(lc.max_seqs, 0);
+    last_tok.assign(lc.max_seqs, -1);
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  void synthetic(uint32_t seed) {
+    float* tmp = nullptr;
+    int64_t tmp_n = 0;
+    for (const std::string& name : spec_order) {
+      Slot& s = slots[name];
+      const uint32_t key = lowbias32_h(fnv1a32(name) ^ (uint32_t)(seed * 0x9E3779B9u));
+      if (s.kind == 0) {
+        launch_synth_fill(s.f, s.n, key, s.scale, s.offset, stream);
+      } else {
+        if (tmp_n < s.n) {
+          if (tmp) {
+            FA_HIP(hipStreamSynchronize(stream));
+            FA_HIP(hipFree(tmp));
+          }
+          FA_HIP(hipMalloc(&tmp, s.n * 4));
+          tmp_n = s.n;
+        }
+        launch_synth_fill(tmp, s.n, key, s.scale, s.offset, stream);
+        launch_quant_q8_0(tmp, s.n, s.q, s.d, stream);
+      }
+      s.set = true;
+    }
+    FA_HIP(hipStreamSynchronize(stream));
+    if (tmp) FA_HIP(hipFree(tmp));
+  }
+
+  Slot& slot(const char* name) {
+    auto it = slots.find(name);
+    if (it == slots.end()) {
+      set_error(std::string("unknown tensor ") + name);
+      throw arg_failure();
+    }
+    return it->second;
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // encoder forward (batch, device pcm)
+  void enc_lin(const float* A, int64_t lda, const float* W, const float* b, float* C, int64_t ldc, int M, int N, int K,
+               int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0) {
+    hipEvent_t ev;
+    prof_begin(1, &ev);
+    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream);
+    prof_end(1, 0, 2.0 * M * N * K);
+  }
+
+  void sanm(const EncBlockW& w, int rows, int ts, const int* lens, bool first) {
+    const int d = ec.d_model;
+    const float* xin = first ? hbuf : xa;  // block0 input = PE'd LFR features (hbuf holds them)
+    float* x = xa;
+    // LN1
+    layernorm(first ? xin : x, w.d_in, att, w.d_in, w.ln1_w, w.ln1_b, rows, w.d_in, 1e-5f, nullptr, ts, stream);
+    enc_lin(att, w.d_in, w.qkv_w, w.qkv_b, qkv, 3 * d, rows, 3 * d, w.d_in);
+    fsmn(qkv + 2 * d, 3 * d, w.fsmn_w, mem, d, rows, d, ec.fsmn_k, lens, ts, stream);
+    {
+      hipEvent_t ev;
+      prof_begin(2, &ev);
+      attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.n_heads, d / ec.n_heads, lens,
+               stream);
+      prof_end(2, 0, 4.0 * rows * (double)ts * d);
+    }
+    if (first) {
+      enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, nullptr, 0, mem, d);
+      return;
+    }
+    enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, x, d, mem, d);
+    layernorm(x, d, hbuf, d, w.ln2_w, w.ln2_b, rows, d, 1e-5f, nullptr, ts, stream);
+    enc_lin(hbuf, d, w.w1, w.b1, ffn, ec.d_ffn, rows, ec.d_ffn, d, 1);
+    enc_lin(ffn, ec.d_ffn, w.w2, w.b2, x, d, rows, d, ec.d_ffn, 0, x, d);
+  }
+
+  // CorrectTransformerAdaptor: out [rows][d_out] in `out`; uses hbuf/qkv/att/ffn as scratch
+  void run_adaptor(const AdaptorW& a, const float* in, int d_enc, int d_out, int d_ffn, int n_heads, float* out,
+                   int rows, int ts, const int* lens) {
+    enc_lin(in, d_enc, a.l1_w, a.l1_b, ffn, d_ffn, rows, d_ffn, d_enc, 1);
+    enc_lin(ffn, d_ffn, a.l2_w, a.l2_b, out, d_out, rows, d_out, d_ffn);
+    for (const AdBlockW& b : a.blocks) {
+      layernorm(out, d_out, hbuf, d_out, b.ln1_w, b.ln1_b, rows, d_out, 1e-12f, nullptr, ts, stream);
+      enc_lin(hbuf, d_out, b.qkv_w, b.qkv_b, qkv, 3 * d_out, rows, 3 * d_out, d_out);
+      {
+        hipEvent_t ev;
+        prof_begin(2, &ev);
+        attn_f32(qkv, qkv + d_out, qkv + 2 * d_out, 3 * d_out, 3 * d_out, 3 * d_out, att, d_out, rows / ts, ts, n_heads,
+                 d_out / n_heads, lens, stream);
+        prof_end(2, 0, 4.0 * rows * (double)ts * d_out);
+      }
+      enc_lin(att, d_out, b.o_w, b.o_b, out, d_out, rows, d_out, d_out, 0, out, d_out);
+      layernorm(out, d_out, hbuf, d_out, b.ln2_w, b.ln2_b, rows, d_out, 1e-12f, nullptr, ts, stream);
+      enc_lin(hbuf, d_out, b.w1, b.b1, ffn, d_out / 4, rows, d_out / 4, d_out, 1);
+      enc_lin(ffn, d_out / 4, b.w2, b.b2, out, d_out, rows, d_out, d_out / 4, 0, out, d_out);
+    }
+  }
+
+  void encode_device(const float* pcm, const int64_t* n_samples, int batch, int64_t stride) {
+    FA_REQUIRE(batch >= 1 && batch <= max_batch, "batch out of range");
+    std::vector<int> tmel(batch), ctcl(batch);
+    h_tlfr.assign(batch, 0);
+    h_tgt.assign(batch, 0);
+    h_ctclen.assign(batch, 0);
+    int tm_stride = 1, ts = 1;
+    for (int b = 0; b < batch; ++b) {
+      const int64_t n = n_samples[b];
+      FA_REQUIRE(n >= 1 && n <= max_samples, "n_samples out of range");
+      FA_REQUIRE(n <= stride, "n_samples > stride");
+      tmel[b] = (int)(n / 160 + 1);
+      h_tlfr[b] = (tmel[b] + 5) / 6;
+      const int o1 = 1 + (h_tlfr[b] - 3 + 2) / 2;
+      h_tgt[b] = (1 + (o1 - 3 + 2) / 2 - 1) / 2 + 1;
+      // CPU-EP policy (nano_onnx.py:90-99): clips < 1 s are zero-padded to 1 s; the unmasked CTC head
+      // then runs over the padded length (model_definition.py:336)
+      h_ctclen[b] = t_lfr_of(std::max<int64_t>(n, 16000));
+      tm_stride = std::max(tm_stride, tmel[b]);
+      ts = std::max(ts, h_ctclen[b]);
+    }
+    const int64_t xps = ((int64_t)160 * (tm_stride - 1) + 400 + 3) / 4 * 4;
+    const int rows = batch * ts;
+    last_batch = batch;
+    last_tstride = ts;
+    FA_HIP(hipMemcpyAsync(d_nsamp, n_samples, batch * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tmel, tmel.data(), batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tlfr, h_tlfr.data(), batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tgt, h_tgt.data(), batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_ctclen, h_ctclen.data(), batch * 4, hipMemcpyHostToDevice, stream));
+    // F1-F4
+    frontend_preemph(pcm, stride, d_nsamp, batch, mean_part, xp, xps, stream);
+    {
+      hipEvent_t ev;
+      prof_begin(1, &ev);
+      gemm_stft_power(xp, xps, tm_stride, batch * tm_stride, basis, power, 204, stream);
+      prof_end(1, 0, 2.0 * batch * tm_stride * 402.0 * 400.0);
+    }
+    gemm_mel_log(power, 204, fbank, 204, mel, batch * tm_stride, ec.n_mels, 201, stream);
+    frontend_lfr(mel, tm_stride, d_tmel, d_tlfr, pe, hbuf, batch, ts, ec.n_mels, ec.lfr_m, ec.lfr_n, stream);
+    if (debug_flags & 1) {
+      if (!tap_lfr) tap_lfr = alloc<float>((size_t)tl_max * ec.d_in);
+      // LFR features before the x*sqrt(512)+PE embed are not materialised; the tap holds the embedded rows
+      FA_HIP(hipMemcpyAsync(tap_lfr, hbuf, (size_t)ts * ec.d_in * 4, hipMemcpyDeviceToDevice, stream));
+    }
+    // SenseVoiceEncoderSmall (embed is folded into frontend_lfr: x*sqrt(512) + PE)
+    const int d = ec.d_model;
+    for (size_t i = 0; i < enc_blocks.size(); ++i) {
+      if ((int)i == ec.n_blocks) {
+        layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream);
+      }
+      sanm(enc_blocks[i], rows, ts, d_tlfr, i == 0);
+    }
+    if ((int)enc_blocks.size() == ec.n_blocks) layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream);
+    layernorm(xa, d, enc, d, tp_w, tp_b, rows, d, 1e-5f, d_tlfr, ts, stream);
+    // adaptor (key mask = valid frames) -> ad [rows][d_llm]
+    run_adaptor(adaptor, enc, d, ec.d_llm, ec.adaptor_ffn, ec.adaptor_heads, ad, rows, ts, d_tlfr);
+    // CTC head (reference: unmasked over the clip's own frames -> key length = ctc_len)
+    run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, rows, ts, d_ctclen);
+    {
+      hipEvent_t ev;
+      prof_begin(1, &ev);
+      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, rows, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream);
+      prof_end(1, 0, 2.0 * rows * (double)ec.ctc_vocab * d);
+    }
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // decoder forward over M token rows (embeddings already in lx). Logits for rows listed in
+  // `logit_rows` (indices into the M rows), one per sequence slot in the same order.
+  void llm_forward(int M, const std::vector<int>& logit_rows) {
+    const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
+    const int QKV = (H + 2 * KV) * D;
+    const bool small = M <= 4;
+    for (int l = 0; l < lc.n_layer; ++l) {
+      const LlmLayerW& w = layers[l];
+      __half* kc = kcache + (size_t)l * layer_stride;
+      __half* vc = vcache + (size_t)l * layer_stride;
+      GemvArgs a{};
+      a.M = M;
+      a.eps = lc.rms_eps;
+      // q|k|v = W . rms_norm(x)*attn_norm
+      a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
+      a.out = lqkv; a.ldo = QKV;
+      if (small) { a.x = lx; a.ldx = E; a.norm_w = w.attn_norm; }
+      else { prep_q8(lx, E, w.attn_norm, lc.rms_eps, M, E, lxq, lxd, stream); a.xq = lxq; a.xd = lxd; }
+      gemv(a, E, 0);
+      qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
+                    seq_stride, stream);
+      {
+        hipEvent_t ev;
+        prof_begin(3, &ev);
+        attn_decode(lq, kc, vc, latt, M, H, KV, d_tok_seq, d_tok_pos, seq_stride, stream);
+        prof_end(3, 0, 0);
+      }
+      // x += Wo . attn
+      GemvArgs o{};
+      o.M = M; o.eps = lc.rms_eps; o.wq = w.o.q; o.wd = w.o.d; o.O = E; o.rpw = gemv_rows_per_wave(E);
+      o.out = lx; o.ldo = E; o.res = lx; o.ldr = E;
+      if (small) { o.x = latt; o.ldx = H * D; }
+      else { prep_q8(latt, H * D, nullptr, 0.f, M, H * D, lxq, lxd, stream); o.xq = lxq; o.xd = lxd; }
+      gemv(o, H * D, 1);
+      // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
+      GemvArgs g{};
+      g.M = M; g.eps = lc.rms_eps; g.wq = w.gate.q; g.wd = w.gate.d; g.wq2 = w.up.q; g.wd2 = w.up.d; g.O = F;
+      g.rpw = gemv_rows_per_wave(F); g.out = lact; g.ldo = F;
+      if (small) { g.x = lx; g.ldx = E; g.norm_w = w.ffn_norm; }
+      else { prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream); g.xq = lxq; g.xd = lxd; }
+      gemv(g, E, 2);
+      // x += Wdown . act
+      GemvArgs dn{};
+      dn.M = M; dn.eps = lc.rms_eps; dn.wq = w.down.q; dn.wd = w.down.d; dn.O = E; dn.rpw = gemv_rows_per_wave(E);
+      dn.out = lx; dn.ldo = E; dn.res = lx; dn.ldr = E;
+      if (small) { dn.x = lact; dn.ldx = F; }
+      else { prep_q8(lact, F, nullptr, 0.f, M, F, lxq, lxd, stream); dn.xq = lxq; dn.xd = lxd; }
+      gemv(dn, F, 1);
+    }
+    // lm_head (tied token_embd) on the requested rows, fused argmax partials
+    for (size_t i = 0; i < logit_rows.size(); ++i) {
+      GemvArgs h{};
+      h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
+      h.rpw = gemv_rows_per_wave(lc.n_vocab);
+      h.x = lx + (size_t)logit_rows[i] * E; h.ldx = E; h.norm_w = out_norm;
+      h.out = logits + (size_t)i * lc.n_vocab; h.ldo = lc.n_vocab;
+      h.pval = pval + (size_t)i * n_part; h.pidx = pidx + (size_t)i * n_part; h.n_part = n_part;
+      gemv(h, E, 3);
+    }
+  }
+
+  void gemv(const GemvArgs& a, int K, int epi) {
+    hipEvent_t ev;
+    prof_begin(0, &ev);
+    gemv_q8(a, K, epi, stream);
+    const double wbytes = (double)a.O * K * (epi == 2 ? 2.0 : 1.0) * 34.0 / 32.0;
+    prof_end(0, wbytes, 2.0 * a.M * a.O * K * (epi == 2 ? 2.0 : 1.0));
+  }
+
+  void sample(int M, const fa_sampling* s, const int* step_ctr, int* tok_out, int* hist) {
+    const float temp = s ? s->temperature : 0.f;
+    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part, M, temp, s ? s->top_k : 1, s ? s->top_p : 1.f,
+                  s ? s->seed : 0u, step_ctr, tok_out, hist, hist_max, stream);
+  }
+};
+
+}  // namespace fa
+
+using fa::Engine;
+
+struct fa_engine {
+  Engine* e;
+};
+
+#define FA_API_BEGIN try {
+#define FA_API_END                 \
+  }                                \
+  catch (fa::hip_failure&) {       \
+    return FA_ERR_HIP;             \
+  }                                \
+  catch (fa::arg_failure&) {       \
+    return FA_ERR_ARG;             \
+  }                                \
+  catch (std::exception & ex) {    \
+    fa::set_error(ex.what());      \
+    return FA_ERR_STATE;           \
+  }                                \
+  return FA_OK;
+
+extern "C" {
+
+const char* fa_last_error(void) { return fa::g_err.c_str(); }
+
+int fa_set_log_callback(void (*cb)(int32_t, const char*, void*), void* user) {
+  fa::g_log_cb = cb;
+  fa::g_log_ud = user;
+  return FA_OK;
+}
+
+int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_config* llm, int32_t max_batch,
+                     int64_t max_samples, fa_engine** out) {
+  if (!enc || !llm || !out || max_batch < 1 || max_samples < 1) {
+    fa::set_error("fa_engine_create: bad arguments");
+    return FA_ERR_ARG;
+  }
+  Engine* e = new Engine();
+  try {
+    e->device = device;
+    e->ec = *enc;
+    e->lc = *llm;
+    e->max_batch = max_batch;
+    e->max_samples = max_samples;
+    FA_REQUIRE(enc->d_model % 64 == 0 && enc->d_model / enc->n_heads <= 128, "d_model/heads");
+    FA_REQUIRE(llm->head_dim == 128 && llm->n_head == 2 * llm->n_head_kv, "decoder head layout");
+    FA_REQUIRE(llm->n_embd % 1024 == 0 && llm->n_ff % 1024 == 0, "decoder widths must be multiples of 1024");
+    FA_HIP(hipSetDevice(device));
+    FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    e->build_arenas();
+    e->build_constants();
+    e->build_encoder();
+    e->build_llm();
+    FA_HIP(hipDeviceSynchronize());
+  } catch (...) {
+    delete e;
+    return FA_ERR_HIP;
+  }
+  *out = new fa_engine{e};
+  return FA_OK;
+}
+
+int fa_engine_destroy(fa_engine* h) {
+  if (!h) return FA_OK;
+  delete h->e;
+  delete h;
+  return FA_OK;
+}
+
+int fa_weights_synthetic(fa_engine* h, uint32_t seed) {
+  FA_API_BEGIN
+  h->e->synthetic(seed);
+  FA_API_END
+}
+
+int fa_set_tensor_f32(fa_engine* h, const char* name, const float* host, int64_t n) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  fa::Slot& s = e->slot(name);
+  FA_REQUIRE(n == s.n, std::string("size mismatch for ") + name);
+  if (s.kind == 0) {
+    FA_HIP(hipMemcpyAsync(s.f, host, n * 4, hipMemcpyHostToDevice, e->stream));
+  } else {
+    float* tmp = nullptr;
+    FA_HIP(hipMalloc(&tmp, n * 4));
+    FA_HIP(hipMemcpyAsync(tmp, host, n * 4, hipMemcpyHostToDevice, e->stream));
+    fa::launch_quant_q8_0(tmp, n, s.q, s.d, e->stream);
+    FA_HIP(hipStreamSynchronize(e->stream));
+    FA_HIP(hipFree(tmp));
+  }
+  FA_HIP(hipStreamSynchronize(e->stream));
+  s.set = true;
+  FA_API_END
+}
+
+int fa_set_tensor_q8_0(fa_engine* h, const char* name, const uint8_t* blocks, int64_t n_bytes) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  fa::Slot& s = e->slot(name);
+  FA_REQUIRE(s.kind == 1, std::string("not a q8_0 tensor: ") + name);
+  FA_REQUIRE(n_bytes == s.n / 32 * 34, std::string("q8_0 size mismatch for ") + name);
+  uint8_t* tmp = nullptr;
+  FA_HIP(hipMalloc(&tmp, n_bytes));
+  FA_HIP(hipMemcpyAsync(tmp, blocks, n_bytes, hipMemcpyHostToDevice, e->stream));
+  fa::launch_unpack_q8_0(tmp, s.n / 32, s.q, s.d, e->stream);
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_HIP(hipFree(tmp));
+  s.set = true;
+  FA_API_END
+}
+
+int fa_get_tensor_q8_0(fa_engine* h, const char* name, uint8_t* out, int64_t n_bytes) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  fa::Slot& s = e->slot(name);
+  FA_REQUIRE(s.kind == 1 && n_bytes == s.n / 32 * 34, "fa_get_tensor_q8_0: size/kind");
+  uint8_t* tmp = nullptr;
+  FA_HIP(hipMalloc(&tmp, n_bytes));
+  fa::launch_pack_q8_0(s.q, s.d, s.n / 32, tmp, e->stream);
+  FA_HIP(hipMemcpyAsync(out, tmp, n_bytes, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_HIP(hipFree(tmp));
+  FA_API_END
+}
+
+int fa_load_gguf(fa_engine* h, const char* path) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  fa::GGUFFile g;
+  FA_REQUIRE(g.open(path), std::string("cannot read GGUF: ") + fa::gguf_error());
+  for (const auto& t : g.tensors) {
+    auto it = e->slots.find(t.name);
+    if (it == e->slots.end()) {
+      fa::log(3, "gguf: ignoring tensor " + t.name);
+      continue;
+    }
+    fa::Slot& s = it->second;
+    FA_REQUIRE(t.n_elements == s.n, "gguf: element count mismatch for " + t.name);
+    const uint8_t* data = g.data(t);
+    if (t.type == fa::GGML_Q8_0) {
+      FA_REQUIRE(fa_set_tensor_q8_0(h, t.name.c_str(), data, t.n_bytes) == FA_OK, "gguf q8_0 upload");
+    } else if (t.type == fa::GGML_F32) {
+      FA_REQUIRE(fa_set_tensor_f32(h, t.name.c_str(), (const float*)data, t.n_elements) == FA_OK, "gguf f32 upload");
+    } else if (t.type == fa::GGML_F16) {
+      std::vector<float> tmp(t.n_elements);
+      const uint16_t* hp = (const uint16_t*)data;
+      for (int64_t i = 0; i < t.n_elements; ++i) tmp[i] = fa::half_to_float_host(hp[i]);
+      FA_REQUIRE(fa_set_tensor_f32(h, t.name.c_str(), tmp.data(), t.n_elements) == FA_OK, "gguf f16 upload");
+    } else {
+      FA_REQUIRE(false, "gguf: unsupported tensor type for " + t.name);
+    }
+  }
+  FA_API_END
+}
+
+int fa_encode_device(fa_engine* h, const float* d_pcm, const int64_t* n_samples, int32_t batch, int64_t stride) {
+  FA_API_BEGIN
+  h->e->encode_device(d_pcm, n_samples, batch, stride);
+  FA_API_END
+}
+
+int fa_encode_fetch(fa_engine* h, float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out, int64_t ids_stride,
+                    int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  const int B = e->last_batch, ts = e->last_tstride, d = e->ec.d_model, L = e->ec.d_llm;
+  FA_REQUIRE(B > 0, "no encode to fetch");
+  for (int b = 0; b < B; ++b) {
+    if (audio_embd_out) {
+      FA_REQUIRE(tgt_stride >= e->h_tgt[b], "tgt_stride too small");
+      FA_HIP(hipMemcpyAsync(audio_embd_out + (size_t)b * tgt_stride * L, e->ad + (size_t)b * ts * L,
+                            (size_t)e->h_tgt[b] * L * 4, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (ctc_ids_out) {
+      FA_REQUIRE(ids_stride >= e->h_ctclen[b], "ids_stride too small");
+      FA_HIP(hipMemcpyAsync(ctc_ids_out + (size_t)b * ids_stride, e->ctc_ids + (size_t)b * ts,
+                            (size_t)e->h_ctclen[b] * 4, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (enc_out) {
+      FA_REQUIRE(ids_stride >= e->h_ctclen[b], "ids_stride too small");
+      FA_HIP(hipMemcpyAsync(enc_out + (size_t)b * ids_stride * d, e->enc + (size_t)b * ts * d,
+                            (size_t)e->h_ctclen[b] * d * 4, hipMemcpyDeviceToHost, e->stream));
+    }
+    if (t_lfr_out) t_lfr_out[b] = e->h_ctclen[b];
+    if (target_len_out) target_len_out[b] = e->h_tgt[b];
+  }
+  FA_HIP(hipStreamSynchronize(e->stream));
+  e->prof_collect();
+  FA_API_END
+}
+
+int fa_encode(fa_engine* h, const float* pcm, const int64_t* n_samples, int32_t batch, int64_t stride,
+              float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out, int64_t ids_stride, int32_t* t_lfr_out,
+              int32_t* target_len_out, float* enc_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(pcm && n_samples && batch >= 1 && batch <= e->max_batch && stride >= 1, "fa_encode args");
+  FA_REQUIRE(stride <= std::max<int64_t>(e->max_samples, 16000), "stride > max_samples");
+  FA_HIP(hipMemcpyAsync(e->d_pcm, pcm, (size_t)batch * stride * 4, hipMemcpyHostToDevice, e->stream));
+  e->encode_device(e->d_pcm, n_samples, batch, stride);
+  int r = fa_encode_fetch(h, audio_embd_out, tgt_stride, ctc_ids_out, ids_stride, t_lfr_out, target_len_out, enc_out);
+  if (r != FA_OK) return r;
+  FA_API_END
+}
+
+int fa_ctc_collapse(fa_engine* h, int32_t blank_id, int32_t* ids_out, int32_t* frames_out, int64_t out_stride,
+                    int32_t* n_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  const int B = e->last_batch, ts = e->last_tstride;
+  FA_REQUIRE(B > 0, "no encode");
+  fa::ctc_collapse(e->ctc_ids, ts, e->d_ctclen, B, blank_id, e->d_col_ids, e->d_col_frames, ts, e->d_col_n, e->stream);
+  std::vector<int> n(B);
+  FA_HIP(hipMemcpyAsync(n.data(), e->d_col_n, B * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  for (int b = 0; b < B; ++b) {
+    FA_REQUIRE(out_stride >= n[b], "collapse out_stride too small");
+    if (n[b]) {
+      FA_HIP(hipMemcpyAsync(ids_out + (size_t)b * out_stride, e->d_col_ids + (size_t)b * ts, n[b] * 4,
+                            hipMemcpyDeviceToHost, e->stream));
+      FA_HIP(hipMemcpyAsync(frames_out + (size_t)b * out_stride, e->d_col_frames + (size_t)b * ts, n[b] * 4,
+                            hipMemcpyDeviceToHost, e->stream));
+    }
+    n_out[b] = n[b];
+  }
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_set_debug(fa_engine* h, int32_t flags) {
+  FA_API_BEGIN
+  h->e->debug_flags = flags;
+  FA_API_END
+}
+
+int fa_encode_tap(fa_engine* h, int32_t which, float* out, int64_t n) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(which == 0 && (e->debug_flags & 1) && e->tap_lfr, "tap 0 needs fa_set_debug(e, 1) before fa_encode");
+  const int64_t have = (int64_t)e->last_tstride * e->ec.d_in;
+  FA_REQUIRE(n <= have, "tap size");
+  FA_HIP(hipMemcpy(out, e->tap_lfr, n * 4, hipMemcpyDeviceToHost));
+  FA_API_END
+}
+
+int fa_embd_rows(fa_engine* h, const int32_t* ids, int32_t n, int32_t fp16_round, float* out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(n >= 1 && n <= e->m_max, "fa_embd_rows: n");
+  for (int i = 0; i < n; ++i) FA_REQUIRE(ids[i] >= 0 && ids[i] < e->lc.n_vocab, "token id out of range");
+  FA_HIP(hipMemcpyAsync(e->d_ids, ids, n * 4, hipMemcpyHostToDevice, e->stream));
+  fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_ids, n, e->lc.n_embd, fp16_round, e->lx, e->stream);
+  FA_HIP(hipMemcpyAsync(out, e->lx, (size_t)n * e->lc.n_embd * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_llm_reset(fa_engine* h, int32_t seq) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
+  e->n_past[seq] = 0;
+  e->last_tok[seq] = -1;
+  FA_API_END
+}
+
+int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_tokens, const fa_sampling* s,
+                   int32_t* tok_out, float* logits_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
+  FA_REQUIRE(n_tokens >= 1 && e->n_past[seq] + n_tokens <= e->lc.n_ctx, "prefill exceeds n_ctx");
+  const int E = e->lc.n_embd;
+  FA_HIP(hipMemcpyAsync(e->lx, embd, (size_t)n_tokens * E * 4, hipMemcpyHostToDevice, e->stream));
+  std::vector<int> sq(n_tokens, seq), ps(n_tokens);
+  for (int i = 0; i < n_tokens; ++i) ps[i] = e->n_past[seq] + i;
+  FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
+  e->llm_forward(n_tokens, {n_tokens - 1});
+  e->sample(1, s, nullptr, e->d_tok_cur, nullptr);
+  int tok = 0;
+  FA_HIP(hipMemcpyAsync(&tok, e->d_tok_cur, 4, hipMemcpyDeviceToHost, e->stream));
+  if (logits_out)
+    FA_HIP(hipMemcpyAsync(logits_out, e->logits, (size_t)e->lc.n_vocab * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  e->prof_collect();
+  e->n_past[seq] += n_tokens;
+  e->last_tok[seq] = tok;
+  if (tok_out) *tok_out = tok;
+  FA_API_END
+}
+
+int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
+                    int32_t* tokens_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs && n_steps >= 1 && n_steps <= e->hist_max, "generate args");
+  std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0), rows(n_seqs);
+  for (int i = 0; i < n_seqs; ++i) {
+    const int q = seqs[i];
+    FA_REQUIRE(q >= 0 && q < e->lc.max_seqs, "seq out of range");
+    FA_REQUIRE(e->last_tok[q] >= 0, "sequence has no sampled token (prefill first)");
+    FA_REQUIRE(e->n_past[q] + n_steps <= e->lc.n_ctx, "generate exceeds n_ctx");
+    sq[i] = q;
+    ps[i] = e->n_past[q];
+    cur[i] = e->last_tok[q];
+    rows[i] = i;
+  }
+  FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(e->d_tok_cur, cur.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(e->d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
+  for (int st = 0; st < n_steps; ++st) {
+    fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_tok_cur, n_seqs, e->lc.n_embd, 0, e->lx, e->stream);
+    e->llm_forward(n_seqs, rows);
+    e->sample(n_seqs, s, e->d_step, e->d_tok_cur, e->d_tok_hist);
+    fa::advance_positions(e->d_tok_pos, e->d_step, n_seqs, e->stream);
+  }
+  std::vector<int> hist((size_t)n_seqs * e->hist_max);
+  FA_HIP(hipMemcpyAsync(hist.data(), e->d_tok_hist, hist.size() * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  e->prof_collect();
+  for (int i = 0; i < n_seqs; ++i) {
+    for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hist[(size_t)i * e->hist_max + st];
+    e->n_past[seqs[i]] += n_steps;
+    e->last_tok[seqs[i]] = hist[(size_t)i * e->hist_max + n_steps - 1];
+  }
+  FA_API_END
+}
+
+int fa_llm_logits(fa_engine* h, int32_t row, float* out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(row >= 0 && row < e->lc.max_seqs, "row");
+  FA_HIP(hipMemcpy(out, e->logits + (size_t)row * e->lc.n_vocab, (size_t)e->lc.n_vocab * 4, hipMemcpyDeviceToHost));
+  FA_API_END
+}
+
+int fa_llm_n_past(fa_engine* h, int32_t seq, int32_t* out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq");
+  *out = e->n_past[seq];
+  FA_API_END
+}
+
+int fa_profile_enable(fa_engine* h, int32_t on) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  e->prof_collect();
+  e->prof = on != 0;
+  for (auto& c : e->pcls) c = Engine::ProfCls{};
+  FA_API_END
+}
+
+int fa_profile_read(fa_engine* h, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(cls >= 0 && cls < 4, "class");
+  e->prof_collect();
+  if (ms) *ms = e->pcls[cls].ms;
+  if (launches) *launches = e->pcls[cls].launches;
+  if (bytes) *bytes = e->pcls[cls].bytes;
+  if (flops) *flops = e->pcls[cls].flops;
+  FA_API_END
+}
+
+int fa_synchronize(fa_engine* h) {
+  FA_API_BEGIN
+  FA_HIP(hipStreamSynchronize(h->e->stream));
+  FA_API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,287 @@
+// FP32 GEMM on CDNA4 matrix cores: C[M,N] = epilogue(A[M,K] . W[N,K]^T)  (nn.Linear layout).
+//
+// v_mfma_f32_32x32x2_f32 (exact f32 fma chain, 157 TF/s dense peak on MI355X): lane l holds
+// A[i=l&31][k=l>>5], B[k=l>>5][j=l&31]; accumulator reg r -> row (r&3)+8(r>>2)+4(l>>5), col l&31.
+// Block tile 64x64x32, 4 waves (2x2 of 32x32), LDS k-major [BK][BM+1] double-buffered: global loads are
+// 8 rows x 128 B per wave instruction, LDS writes/reads are bank-conflict free with the +1 pad.
+// Used for every encoder/adaptor/CTC projection, the STFT-as-DFT-GEMM (F2) with a
+// power epilogue (F3), the mel projection with a log epilogue, and the CTC projection with a fused
+// row-argmax epilogue (C1) so the [T, 60515] logits never reach HBM.
+#include "common.h"
+#include "kernels.h"
+
+namespace fa {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 64, BN = 64, BK = 32, LDP = BM + 1;
+
+struct ALoadPlain {
+  const float* A;
+  int64_t lda;
+  __device__ __forceinline__ float4 load4(int row, int k, int M, int K) const {
+    if (row >= M) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* p = A + (int64_t)row * lda + k;
+    if (k + 3 < K) return *reinterpret_cast<const float4*>(p);
+    float4 r;
+    r.x = k < K ? p[0] : 0.f;
+    r.y = k + 1 < K ? p[1] : 0.f;
+    r.z = k + 2 < K ? p[2] : 0.f;
+    r.w = k + 3 < K ? p[3] : 0.f;
+    return r;
+  }
+};
+
+// STFT framing (model_definition.py:255 F.pad + conv1d stride 160): row = clip*t_stride + t reads
+// xp[clip][160 t + k] from the 200/200 zero-padded, pre-emphasised signal.
+struct ALoadFrames {
+  const float* xp;
+  int64_t xp_stride;
+  int t_stride, hop;
+  __device__ __forceinline__ float4 load4(int row, int k, int M, int K) const {
+    if (row >= M || k >= K) return make_float4(0.f, 0.f, 0.f, 0.f);  // K % 4 == 0
+    int b = row / t_stride, t = row - b * t_stride;
+    return *reinterpret_cast<const float4*>(xp + (int64_t)b * xp_stride + (int64_t)t * hop + k);
+  }
+};
+
+template <class AL>
+__device__ __forceinline__ void load_tiles(const AL& al, const float* __restrict__ W, int64_t ldw, int m0, int n0,
+                                           int k0, int M, int N, int K, float4 (&ra)[2], float4 (&rb)[2]) {
+  int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int idx = t + i * 256;           // 0..511 -> (row 0..63, k4 0..7)
+    int r = idx >> 3, k4 = idx & 7;
+    int k = k0 + 4 * k4;
+    ra[i] = al.load4(m0 + r, k, M, K);
+    int n = n0 + r;
+    if (n < N) {
+      const float* p = W + (int64_t)n * ldw + k;
+      if (k + 3 < K) {
+        rb[i] = *reinterpret_cast<const float4*>(p);
+      } else {
+        rb[i].x = k < K ? p[0] : 0.f;
+        rb[i].y = k + 1 < K ? p[1] : 0.f;
+        rb[i].z = k + 2 < K ? p[2] : 0.f;
+        rb[i].w = k + 3 < K ? p[3] : 0.f;
+      }
+    } else {
+      rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (&ra)[2], const float4 (&rb)[2]) {
+  int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    int idx = t + i * 256;
+    int r = idx >> 3, k = 4 * (idx & 7);
+    As[(k + 0) * LDP + r] = ra[i].x;
+    As[(k + 1) * LDP + r] = ra[i].y;
+    As[(k + 2) * LDP + r] = ra[i].z;
+    As[(k + 3) * LDP + r] = ra[i].w;
+    Bs[(k + 0) * LDP + r] = rb[i].x;
+    Bs[(k + 1) * LDP + r] = rb[i].y;
+    Bs[(k + 2) * LDP + r] = rb[i].z;
+    Bs[(k + 3) * LDP + r] = rb[i].w;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Epilogues. `apply` receives the wave's 32x32 accumulator at (row0, col0).
+struct EpiLinear {
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  const float* add1;  // residual (added last)
+  int64_t ld1;
+  const float* add2;  // e.g. FSMN memory (added before the residual, model_definition.py:90,109)
+  int64_t ld2;
+  int relu;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    int lane = threadIdx.x & 63;
+    int col = col0 + (lane & 31);
+    if (col >= N) return;
+    float b = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) {
+        float v = acc[r] + b;
+        if (relu) v = fmaxf(v, 0.f);
+        if (add2) v = v + add2[(int64_t)row * ld2 + col];
+        if (add1) v = add1[(int64_t)row * ld1 + col] + v;
+        C[(int64_t)row * ldc + col] = v;
+      }
+    }
+  }
+};
+
+// STFT: W rows interleave (cos_f, -sin_f); power[row][f] = re^2 + im^2 (model_definition.py:287).
+struct EpiPower {
+  float* P;
+  int64_t ldp;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    int lane = threadIdx.x & 63;
+    int col = col0 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = acc[r];
+      float o = __shfl_xor(v, 1, 64);
+      int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (!(lane & 1) && row < M && col < N) P[(int64_t)row * ldp + (col >> 1)] = v * v + o * o;
+    }
+  }
+};
+
+// mel = log(fbank . power + 1e-7)
+struct EpiLog {
+  float* C;
+  int64_t ldc;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    int lane = threadIdx.x & 63;
+    int col = col0 + (lane & 31);
+    if (col >= N) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < M) C[(int64_t)row * ldc + col] = logf(acc[r] + 1e-7f);
+    }
+  }
+};
+
+// CTC projection + bias + row argmax over this block's 64 columns -> partial (value, index).
+struct EpiArgmax {
+  const float* bias;
+  float* pval;   // [M][n_tiles]
+  int* pidx;
+  int n_tiles;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int col = col0 + (lane & 31);
+    float b = col < N ? bias[col] : 0.f;
+    float* sv = lds;                              // [64 rows][2]
+    int* si = reinterpret_cast<int*>(lds + 128);  // [64][2]
+    int wr = wave >> 1, wc = wave & 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = col < N ? acc[r] + b : -INFINITY;
+      int i = col < N ? col : 0x7fffffff;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) {
+        float v2 = __shfl_xor(v, o, 32);
+        int i2 = __shfl_xor(i, o, 32);
+        argmax_combine(v, i, v2, i2);
+      }
+      if ((lane & 31) == 0) {
+        int lr = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        sv[lr * 2 + wc] = v;
+        si[lr * 2 + wc] = i;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      int lr = threadIdx.x;
+      int row = (row0 - (row0 % 64)) + lr;  // block row base
+      float v = sv[lr * 2];
+      int i = si[lr * 2];
+      argmax_combine(v, i, sv[lr * 2 + 1], si[lr * 2 + 1]);
+      int tile = col0 / 64;
+      if (row < M) {
+        pval[(int64_t)row * n_tiles + tile] = v;
+        pidx[(int64_t)row * n_tiles + tile] = i;
+      }
+    }
+  }
+};
+
+template <class AL, class EPI>
+__global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
+                                                  EPI epi) {
+  __shared__ float smem[2 * 2 * BK * LDP];
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc = {};
+  float4 ra[2], rb[2];
+  load_tiles(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
+  store_tiles(smem, smem + BK * LDP, ra, rb);
+  __syncthreads();
+  const int nk = (K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
+    const float* a = smem + cur * 2 * BK * LDP + wr * 32 + r;
+    const float* b = smem + cur * 2 * BK * LDP + BK * LDP + wc * 32 + r;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float av = a[(2 * kk + h) * LDP];
+      float bv = b[(2 * kk + h) * LDP];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      store_tiles(smem + (cur ^ 1) * 2 * BK * LDP, smem + (cur ^ 1) * 2 * BK * LDP + BK * LDP, ra, rb);
+    }
+    __syncthreads();
+  }
+  epi.apply(acc, m0 + wr * 32, n0 + wc * 32, M, N, smem);
+}
+
+template <class AL, class EPI>
+static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
+  dim3 grid(cdiv(N, BN), cdiv(M, BM));
+  hipLaunchKernelGGL((k_gemm_f32<AL, EPI>), grid, dim3(256), 0, s, al, W, ldw, M, N, K, epi);
+}
+
+void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
+                 int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
+                 hipStream_t s) {
+  ALoadPlain al{A, lda};
+  EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu};
+  run_gemm(al, W, ldw, M, N, K, epi, s);
+}
+
+void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
+                     int64_t ldp, hipStream_t s) {
+  ALoadFrames al{xp, xp_stride, t_stride, 160};
+  EpiPower epi{power, ldp};
+  run_gemm(al, basis, 400, M, 402, 400, epi, s);
+}
+
+void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
+                  int n_freq, hipStream_t s) {
+  ALoadPlain al{power, ldp};
+  EpiLog epi{mel, n_mels};
+  run_gemm(al, fbank, ldf, M, n_mels, n_freq, epi, s);
+}
+
+__global__ void k_argmax_final(const float* __restrict__ pval, const int* __restrict__ pidx, int M, int n_tiles,
+                               int* __restrict__ out) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  float v = -INFINITY;
+  int i = 0x7fffffff;
+  for (int t = lane; t < n_tiles; t += 64) argmax_combine(v, i, pval[(int64_t)row * n_tiles + t], pidx[(int64_t)row * n_tiles + t]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    float v2 = __shfl_xor(v, o, 64);
+    int i2 = __shfl_xor(i, o, 64);
+    argmax_combine(v, i, v2, i2);
+  }
+  if (lane == 0) out[row] = i;
+}
+
+void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
+                     int* pidx, int* out, hipStream_t s) {
+  int n_tiles = cdiv(N, BN);
+  ALoadPlain al{A, lda};
+  EpiArgmax epi{bias, pval, pidx, n_tiles};
+  run_gemm(al, W, K, M, N, K, epi, s);
+  hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
+}
+
+}  // namespace fa

@@ -1,0 +1,69 @@
+// Host-callable launchers of the HIP kernels (all enqueue on stream `s`, no synchronisation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace fa {
+
+// synth.hip
+void launch_synth_fill(float* out, int64_t n, uint32_t key, float scale, float offset, hipStream_t s);
+void launch_quant_q8_0(const float* x, int64_t n, int8_t* qs, __half* d, hipStream_t s);
+void launch_unpack_q8_0(const uint8_t* blocks, int64_t n_blocks, int8_t* qs, __half* d, hipStream_t s);
+void launch_pack_q8_0(const int8_t* qs, const __half* d, int64_t n_blocks, uint8_t* blocks, hipStream_t s);
+void launch_h2f(const __half* a, float* b, int64_t n, hipStream_t s);
+
+// gemm_f32.hip
+void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
+                 int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
+                 hipStream_t s);
+void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
+                     int64_t ldp, hipStream_t s);
+void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
+                  int n_freq, hipStream_t s);
+void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
+                     int* pidx, int* out, hipStream_t s);
+
+// attn_f32.hip
+void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
+              int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens, hipStream_t s);
+
+// enc_misc.hip
+void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,
+                      float* xp, int64_t xp_stride, hipStream_t s);
+void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, const int* t_lfr_valid, const float* pe,
+                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s);
+void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
+               float eps, const int* lens, int t_stride, hipStream_t s);
+void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
+          const int* lens, int t_stride, hipStream_t s);
+void ctc_collapse(const int* ids, int64_t ids_stride, const int* lens, int batch, int blank, int* out_ids,
+                  int* out_frames, int64_t out_stride, int* n_out, hipStream_t s);
+
+// llm.hip
+struct GemvArgs {
+  const int8_t* wq; const __half* wd;      // [O][K], [O][K/32]
+  const int8_t* wq2; const __half* wd2;    // up matrix for SwiGLU
+  const float* x; int64_t ldx; const float* norm_w; float eps;  // FUSED input
+  const int8_t* xq; const float* xd;       // pre-quantised input
+  float* out; int64_t ldo;                 // [M][O]
+  const float* res; int64_t ldr;
+  float* pval; int* pidx; int n_part;      // argmax partials [M][n_part]
+  int M, O, rpw;
+};
+void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
+void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
+int gemv_rows_per_wave(int O);
+void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
+                   const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
+                   int64_t seq_stride, hipStream_t s);
+void attn_decode(const float* q, const __half* kc, const __half* vc, float* out, int M, int H, int KV,
+                 const int* tok_seq, const int* tok_pos, int64_t seq_stride, hipStream_t s);
+void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
+                hipStream_t s);
+void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
+                   float temperature, int top_k, float top_p, uint32_t seed, const int* step_ctr, int* tok_out,
+                   int* tok_hist, int hist_stride, hipStream_t s);
+void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s);
+
+}  // namespace fa

@@ -1,0 +1,532 @@
+// Qwen3 decoder kernels with ggml q8_0 x q8_0 numerics (oracle/qwen3.py):
+//   activations are RMS-normalised (optional) and quantised per 32-block with the ggml reference
+//   quantiser, weight rows are q8_0 (engine layout: int8 qs[O][K] + fp16 d[O][K/32]), each block's
+//   integer dot is exact (v_dot4_i32_i8), scaled by f32(dw)*f32(dx) and summed in f32.
+// The decode GEMV streams every weight byte exactly once per step for the whole continuous batch
+// (HBM-bound: 633 MB/step for Qwen3-0.6B q8_0); one wave covers a K=1024 row with ONE 16 B/lane load.
+#include "common.h"
+#include "kernels.h"
+
+namespace fa {
+
+// ------------------------------------------------------------------------------------------------
+// per-row RMSNorm (ggml_rms_norm: 1/sqrtf(mean(x^2)+eps), then ggml_mul by w) + q8_0 quantisation.
+// lane handles 16 consecutive values per 1024-chunk: x[c*1024 + lane*16 + j]; a 32-block = 2 lanes.
+template <int NCH>
+__device__ __forceinline__ void norm_quant_row(const float* __restrict__ x, const float* __restrict__ w, float eps,
+                                               int lane, int8_t* __restrict__ q_out, float* __restrict__ d_out) {
+  float v[NCH][16];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const float4* p = reinterpret_cast<const float4*>(x + c * 1024 + lane * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float4 f = p[j];
+      v[c][4 * j] = f.x;
+      v[c][4 * j + 1] = f.y;
+      v[c][4 * j + 2] = f.z;
+      v[c][4 * j + 3] = f.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ss += v[c][j] * v[c][j];
+  }
+  if (w) {
+    ss = wave_sum(ss);
+    const float mean = ss / (float)(NCH * 1024);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const float4* wp = reinterpret_cast<const float4*>(w + c * 1024 + lane * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float4 f = wp[j];
+        v[c][4 * j] = (v[c][4 * j] * scale) * f.x;
+        v[c][4 * j + 1] = (v[c][4 * j + 1] * scale) * f.y;
+        v[c][4 * j + 2] = (v[c][4 * j + 2] * scale) * f.z;
+        v[c][4 * j + 3] = (v[c][4 * j + 3] * scale) * f.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a = fmaxf(a, fabsf(v[c][j]));
+    a = fmaxf(a, __shfl_xor(a, 1, 64));
+    const float d = a / 127.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    int32_t packed[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int b0 = (int)roundf(__fmul_rn(v[c][4 * j], id)) & 0xFF;
+      int b1 = (int)roundf(__fmul_rn(v[c][4 * j + 1], id)) & 0xFF;
+      int b2 = (int)roundf(__fmul_rn(v[c][4 * j + 2], id)) & 0xFF;
+      int b3 = (int)roundf(__fmul_rn(v[c][4 * j + 3], id)) & 0xFF;
+      packed[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    }
+    *reinterpret_cast<int4*>(q_out + c * 1024 + lane * 16) = make_int4(packed[0], packed[1], packed[2], packed[3]);
+    if (!(lane & 1)) d_out[c * 32 + (lane >> 1)] = __half2float(__float2half_rn(d));
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void k_prep_q8(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                                 float eps, int M, int8_t* __restrict__ xq, float* __restrict__ xd) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int K = NCH * 1024;
+  norm_quant_row<NCH>(x + (int64_t)row * ldx, w, eps, threadIdx.x & 63, xq + (int64_t)row * K, xd + (int64_t)row * (K / 32));
+}
+
+void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s) {
+  dim3 grid(cdiv(M, 4));
+  switch (K) {
+    case 1024: hipLaunchKernelGGL(k_prep_q8<1>, grid, dim3(256), 0, s, x, ldx, w, eps, M, xq, xd); break;
+    case 2048: hipLaunchKernelGGL(k_prep_q8<2>, grid, dim3(256), 0, s, x, ldx, w, eps, M, xq, xd); break;
+    case 3072: hipLaunchKernelGGL(k_prep_q8<3>, grid, dim3(256), 0, s, x, ldx, w, eps, M, xq, xd); break;
+    default: FA_REQUIRE(false, "prep_q8: K must be 1024/2048/3072");
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// q8_0 GEMV / small-M GEMM. Block = 4 waves; block (bx, by) covers rows [bx*4*rpw, ...) and tokens
+// [by*MT, by*MT+MT). The activation tile is quantised into LDS by the prologue, either from f32 rows
+// (FUSED: rmsnorm+quant recomputed per block, cheap for decode M<=4) or copied from global xq/xd.
+// Epilogues: 0 store, 1 residual add (out = res + y, in place allowed), 2 SwiGLU (gate & up rows),
+//            3 store + per-wave argmax partial (lm_head, greedy sampling).
+
+
+__device__ __forceinline__ int dot16(const int4& a, const int4& b, int acc) {
+  acc = __builtin_amdgcn_sdot4(a.x, b.x, acc, false);
+  acc = __builtin_amdgcn_sdot4(a.y, b.y, acc, false);
+  acc = __builtin_amdgcn_sdot4(a.z, b.z, acc, false);
+  acc = __builtin_amdgcn_sdot4(a.w, b.w, acc, false);
+  return acc;
+}
+
+template <int NCH, int MT, bool FUSED, int EPI>
+__global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
+  constexpr int K = NCH * 1024, NB = K / 32;
+  __shared__ int8_t s_q[MT * K];
+  __shared__ float s_d[MT * NB];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m0 = blockIdx.y * MT;
+  const int mt = min(MT, a.M - m0);
+  // ---- prologue: activation tile -> LDS (int8 q + f32 d)
+  if (FUSED) {
+    for (int m = wave; m < mt; m += 4)
+      norm_quant_row<NCH>(a.x + (int64_t)(m0 + m) * a.ldx, a.norm_w, a.eps, lane, s_q + m * K, s_d + m * NB);
+  } else {
+    const int4* src = reinterpret_cast<const int4*>(a.xq + (int64_t)m0 * K);
+    int4* dst = reinterpret_cast<int4*>(s_q);
+    for (int i = threadIdx.x; i < mt * K / 16; i += 256) dst[i] = src[i];
+    for (int i = threadIdx.x; i < mt * NB; i += 256) s_d[i] = a.xd[(int64_t)m0 * NB + i];
+  }
+  __syncthreads();
+
+  const int row_base = (blockIdx.x * 4 + wave) * a.rpw;
+  float best_v = -INFINITY;
+  int best_i = 0x7fffffff;
+  for (int r0 = 0; r0 < a.rpw; r0 += 4) {
+    int4 wv[4][NCH], uv[4][NCH];
+    float dw[4][NCH], du[4][NCH];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = row_base + r0 + rr;
+      const bool ok = (r0 + rr < a.rpw) && row < a.O;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if (ok) {
+          wv[rr][c] = *reinterpret_cast<const int4*>(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
+          dw[rr][c] = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+          if (EPI == 2) {
+            uv[rr][c] = *reinterpret_cast<const int4*>(a.wq2 + (int64_t)row * K + c * 1024 + lane * 16);
+            du[rr][c] = __half2float(a.wd2[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+          }
+        } else {
+          wv[rr][c] = make_int4(0, 0, 0, 0);
+          dw[rr][c] = 0.f;
+          if (EPI == 2) { uv[rr][c] = make_int4(0, 0, 0, 0); du[rr][c] = 0.f; }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m >= mt) break;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f}, acc2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int4 xv = *reinterpret_cast<const int4*>(s_q + m * K + c * 1024 + lane * 16);
+        const float xdv = s_d[m * NB + c * 32 + (lane >> 1)];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          int si = dot16(wv[rr][c], xv, 0);
+          si += __shfl_xor(si, 1, 64);
+          if (!(lane & 1)) acc[rr] += (float)si * (dw[rr][c] * xdv);
+          if (EPI == 2) {
+            int su = dot16(uv[rr][c], xv, 0);
+            su += __shfl_xor(su, 1, 64);
+            if (!(lane & 1)) acc2[rr] += (float)su * (du[rr][c] * xdv);
+          }
+        }
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = row_base + r0 + rr;
+        float y = wave_sum(acc[rr]);
+        float y2 = EPI == 2 ? wave_sum(acc2[rr]) : 0.f;
+        if (lane == 0 && (r0 + rr < a.rpw) && row < a.O) {
+          float* op = a.out + (int64_t)(m0 + m) * a.ldo + row;
+          if (EPI == 0 || EPI == 3) *op = y;
+          else if (EPI == 1) *op = a.res[(int64_t)(m0 + m) * a.ldr + row] + y;
+          else *op = (y / (1.0f + expf(-y))) * y2;
+          if (EPI == 3 && MT == 1) argmax_combine(best_v, best_i, y, row);
+        }
+      }
+    }
+  }
+  if (EPI == 3 && MT == 1 && lane == 0) {
+    const int part = blockIdx.x * 4 + wave;
+    a.pval[(int64_t)m0 * a.n_part + part] = best_v;
+    a.pidx[(int64_t)m0 * a.n_part + part] = best_i;
+  }
+}
+
+template <int NCH, int MT, bool FUSED, int EPI>
+static void launch_gemv(const GemvArgs& a, hipStream_t s) {
+  dim3 grid(cdiv(a.O, 4 * a.rpw), cdiv(a.M, MT));
+  hipLaunchKernelGGL((k_gemv_q8<NCH, MT, FUSED, EPI>), grid, dim3(256), 0, s, a);
+}
+
+template <int MT, bool FUSED, int EPI>
+static void launch_gemv_k(int K, const GemvArgs& a, hipStream_t s) {
+  switch (K) {
+    case 1024: launch_gemv<1, MT, FUSED, EPI>(a, s); break;
+    case 2048: launch_gemv<2, MT, FUSED, EPI>(a, s); break;
+    case 3072: launch_gemv<3, MT, FUSED, EPI>(a, s); break;
+    default: FA_REQUIRE(false, "gemv_q8: K must be 1024/2048/3072");
+  }
+}
+
+int gemv_rows_per_wave(int O) {
+  // target ~256-1024 blocks of 4 waves
+  int rpw = (O + 4 * 256 - 1) / (4 * 256);
+  if (rpw > 4) rpw = ((rpw + 3) / 4) * 4;
+  if (O >= 65536) rpw = 40;
+  return rpw < 1 ? 1 : rpw;
+}
+
+void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
+  const bool fused = a.x != nullptr;
+  if (a.M <= 4 && fused) {
+    // decode path: tokens handled one per block row
+    switch (epi) {
+      case 0: launch_gemv_k<1, true, 0>(K, a, s); break;
+      case 1: launch_gemv_k<1, true, 1>(K, a, s); break;
+      case 2: launch_gemv_k<1, true, 2>(K, a, s); break;
+      case 3: launch_gemv_k<1, true, 3>(K, a, s); break;
+    }
+    return;
+  }
+  FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
+  switch (epi) {
+    case 0: launch_gemv_k<8, false, 0>(K, a, s); break;
+    case 1: launch_gemv_k<8, false, 1>(K, a, s); break;
+    case 2: launch_gemv_k<8, false, 2>(K, a, s); break;
+    default: FA_REQUIRE(false, "gemv_q8: argmax epilogue needs M<=4");
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// q/k RMSNorm per head (attn_q_norm/attn_k_norm) + NEOX RoPE + KV-cache store (fp16).
+// One wave per (token, head-slot); head slots 0..H-1 = q heads, H..H+KV-1 = k heads, then v heads.
+__global__ void k_qk_rope_store(const float* __restrict__ qkv, int M, int H, int KV, float eps,
+                                const float* __restrict__ qn, const float* __restrict__ kn,
+                                const float* __restrict__ rcos, const float* __restrict__ rsin,
+                                const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+                                float* __restrict__ qout, __half* __restrict__ kc, __half* __restrict__ vc,
+                                int64_t seq_stride /* elements per seq per layer */) {
+  constexpr int D = 128;
+  const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int m = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int n_slots = H + 2 * KV;
+  if (slot >= n_slots || m >= M) return;
+  const float* src = qkv + (int64_t)m * (H + 2 * KV) * D + slot * D;
+  const int pos = tok_pos[m];
+  const int64_t cbase = (int64_t)tok_seq[m] * seq_stride + (int64_t)pos * KV * D;
+  float x0 = src[lane], x1 = src[lane + 64];
+  if (slot >= H + KV) {  // V: store as-is
+    const int g = slot - H - KV;
+    vc[cbase + g * D + lane] = __float2half_rn(x0);
+    vc[cbase + g * D + lane + 64] = __float2half_rn(x1);
+    return;
+  }
+  const float* w = slot < H ? qn : kn;
+  const float ss = wave_sum(x0 * x0 + x1 * x1);
+  const float scale = 1.0f / sqrtf(ss / (float)D + eps);
+  x0 = (x0 * scale) * w[lane];
+  x1 = (x1 * scale) * w[lane + 64];
+  const float c = rcos[(int64_t)pos * 64 + lane], sn = rsin[(int64_t)pos * 64 + lane];
+  const float y0 = x0 * c - x1 * sn, y1 = x0 * sn + x1 * c;
+  if (slot < H) {
+    qout[((int64_t)m * H + slot) * D + lane] = y0;
+    qout[((int64_t)m * H + slot) * D + lane + 64] = y1;
+  } else {
+    const int g = slot - H;
+    kc[cbase + g * D + lane] = __float2half_rn(y0);
+    kc[cbase + g * D + lane + 64] = __float2half_rn(y1);
+  }
+}
+
+void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
+                   const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
+                   int64_t seq_stride, hipStream_t s) {
+  dim3 grid(cdiv(H + 2 * KV, 4), M);
+  hipLaunchKernelGGL(k_qk_rope_store, grid, dim3(256), 0, s, qkv, M, H, KV, eps, qn, kn, rcos, rsin, tok_seq, tok_pos,
+                     qout, kc, vc, seq_stride);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Causal GQA attention over the fp16 KV cache: block = (token m, kv head g), handles the H/KV q heads
+// of the group. 4 waves split the keys [0, pos] in 64-key chunks (lane = key for QK, lane = dim pair
+// for PV); partial online-softmax states merged in LDS. scores = q.k / sqrt(128).
+constexpr int GQ = 2;  // q heads per kv head (Qwen3-0.6B: 16/8)
+__global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ q, const __half* __restrict__ kc,
+                                                     const __half* __restrict__ vc, float* __restrict__ out, int H,
+                                                     int KV, const int* __restrict__ tok_seq,
+                                                     const int* __restrict__ tok_pos, int64_t seq_stride, float scale) {
+  constexpr int D = 128;
+  const int g = blockIdx.x, m = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int pos = tok_pos[m];
+  const int n_keys = pos + 1;
+  const __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
+  const __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
+  __shared__ float s_q[GQ][D];
+  __shared__ float s_p[4][GQ][64];
+  __shared__ float s_m[4][GQ], s_l[4][GQ];
+  __shared__ float s_o[4][GQ][D];
+  for (int i = threadIdx.x; i < GQ * D; i += 256) s_q[i / D][i % D] = q[((int64_t)m * H + g * GQ + i / D) * D + i % D] * scale;
+  __syncthreads();
+  float m_run[GQ], l_run[GQ], o0[GQ], o1[GQ];
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) { m_run[j] = -INFINITY; l_run[j] = 0.f; o0[j] = 0.f; o1[j] = 0.f; }
+  for (int k0 = wave * 64; k0 < n_keys; k0 += 256) {
+    const int key = k0 + lane;
+    float sc[GQ];
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) sc[j] = 0.f;
+    if (key < n_keys) {
+      const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)key * KV * D);
+#pragma unroll
+      for (int c = 0; c < D / 8; ++c) {
+        int4 raw = kp[c];
+        const __half2* hp = reinterpret_cast<const __half2*>(&raw);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float2 kf = __half22float2(hp[e]);
+#pragma unroll
+          for (int j = 0; j < GQ; ++j) sc[j] += kf.x * s_q[j][c * 8 + 2 * e] + kf.y * s_q[j][c * 8 + 2 * e + 1];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < GQ; ++j) sc[j] = -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      const float mt = wave_max(sc[j]);
+      const float mn = fmaxf(m_run[j], mt);
+      const float alpha = m_run[j] == -INFINITY ? 0.f : expf(m_run[j] - mn);
+      const float p = sc[j] == -INFINITY ? 0.f : expf(sc[j] - mn);
+      l_run[j] = l_run[j] * alpha + wave_sum(p);
+      m_run[j] = mn;
+      o0[j] *= alpha;
+      o1[j] *= alpha;
+      s_p[wave][j][lane] = p;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // PV: lane owns dims (2 lane, 2 lane + 1)
+    const int nk = min(64, n_keys - k0);
+    for (int kk = 0; kk < nk; ++kk) {
+      const float2 vf = __half22float2(*reinterpret_cast<const __half2*>(vb + (int64_t)(k0 + kk) * KV * D + 2 * lane));
+#pragma unroll
+      for (int j = 0; j < GQ; ++j) {
+        const float p = s_p[wave][j][kk];
+        o0[j] += p * vf.x;
+        o1[j] += p * vf.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) {
+    if (lane == 0) { s_m[wave][j] = m_run[j]; s_l[wave][j] = l_run[j]; }
+    s_o[wave][j][2 * lane] = o0[j];
+    s_o[wave][j][2 * lane + 1] = o1[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < GQ * D; i += 256) {
+    const int j = i / D, d = i % D;
+    float M = -INFINITY;
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][j]);
+    float L = 0.f, acc = 0.f;
+    for (int w = 0; w < 4; ++w) {
+      const float sc = s_m[w][j] == -INFINITY ? 0.f : expf(s_m[w][j] - M);
+      L += sc * s_l[w][j];
+      acc += sc * s_o[w][j][d];
+    }
+    out[((int64_t)m * H + g * GQ + j) * D + d] = acc / L;
+  }
+}
+
+void attn_decode(const float* q, const __half* kc, const __half* vc, float* out, int M, int H, int KV,
+                 const int* tok_seq, const int* tok_pos, int64_t seq_stride, hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ, "attn_decode: n_head must be 2*n_head_kv");
+  const float scale = 1.0f / sqrtf(128.0f);
+  hipLaunchKernelGGL(k_attn_decode, dim3(KV, M), dim3(256), 0, s, q, kc, vc, out, H, KV, tok_seq, tok_pos, seq_stride,
+                     scale);
+}
+
+// ------------------------------------------------------------------------------------------------
+// D0 embedding rows from q8_0 token_embd. fp16_round: numpy f16 product (llama.py:782-784).
+__global__ void k_embed(const int8_t* __restrict__ qs, const __half* __restrict__ d, const int* __restrict__ ids, int n,
+                        int E, int fp16_round, float* __restrict__ out) {
+  const int m = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n || i >= E) return;
+  const int64_t row = ids[m];
+  const float dv = __half2float(d[row * (E / 32) + i / 32]);
+  float v = dv * (float)qs[row * E + i];
+  if (fp16_round) v = __half2float(__float2half_rn(v));
+  out[(int64_t)m * E + i] = v;
+}
+
+void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
+                hipStream_t s) {
+  hipLaunchKernelGGL(k_embed, dim3(cdiv(E, 256), n), dim3(256), 0, s, qs, d, ids, n, E, fp16_round, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// D6 sampling. Greedy: reduce the lm_head's per-wave argmax partials. Temperature > 0: top-k (by
+// bisection on the value threshold) -> top-p -> temperature -> categorical draw with a counter-based RNG
+// (llama.cpp's mt19937 draw is seeded from np.random per call, decoder.py:89, i.e. nondeterministic:
+// parity is defined at temperature 0 only).
+__device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+
+__global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logits, int64_t ldl, int V,
+                                                 const float* __restrict__ pval, const int* __restrict__ pidx, int n_part,
+                                                 float temperature, int top_k, float top_p, uint32_t seed,
+                                                 const int* __restrict__ step_ctr, int* __restrict__ tok_out,
+                                                 int* __restrict__ tok_hist, int hist_stride) {
+  const int m = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ float s_thr;
+  __shared__ int s_cnt[16];
+  int tok;
+  if (temperature <= 0.f || top_k == 1) {
+    float v = -INFINITY;
+    int i = 0x7fffffff;
+    for (int t = threadIdx.x; t < n_part; t += 1024) argmax_combine(v, i, pval[(int64_t)m * n_part + t], pidx[(int64_t)m * n_part + t]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      float v2 = __shfl_xor(v, o, 64);
+      int i2 = __shfl_xor(i, o, 64);
+      argmax_combine(v, i, v2, i2);
+    }
+    if (lane == 0) { sv[wave] = v; si[wave] = i; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 16; ++w) argmax_combine(v, i, sv[w], si[w]);
+      si[0] = i;
+    }
+    __syncthreads();
+    tok = si[0];
+  } else {
+    const float* lg = logits + (int64_t)m * ldl;
+    // max
+    float mx = -INFINITY;
+    for (int t = threadIdx.x; t < V; t += 1024) mx = fmaxf(mx, lg[t]);
+    mx = wave_max(mx);
+    if (lane == 0) sv[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) { float a = sv[0]; for (int w = 1; w < 16; ++w) a = fmaxf(a, sv[w]); sv[0] = a; }
+    __syncthreads();
+    mx = sv[0];
+    __syncthreads();
+    // threshold for top-k by bisection: count(lg >= thr) >= k
+    float lo = mx - 1e4f, hi = mx;
+    const int k = top_k <= 0 ? V : min(top_k, V);
+    for (int it = 0; it < 40; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      int c = 0;
+      for (int t = threadIdx.x; t < V; t += 1024) c += lg[t] >= mid;
+      c = wave_sum_i(c);
+      if (lane == 0) s_cnt[wave] = c;
+      __syncthreads();
+      if (threadIdx.x == 0) { int a = 0; for (int w = 0; w < 16; ++w) a += s_cnt[w]; s_cnt[0] = a; }
+      __syncthreads();
+      if (s_cnt[0] >= k) lo = mid; else hi = mid;
+      __syncthreads();
+    }
+    const float thr = lo;
+    // softmax mass of the candidates at temperature (top_p >= 1 is a no-op in llama.cpp)
+    float z = 0.f;
+    for (int t = threadIdx.x; t < V; t += 1024) if (lg[t] >= thr) z += expf((lg[t] - mx) / temperature);
+    z = wave_sum(z);
+    if (lane == 0) sv[wave] = z;
+    __syncthreads();
+    if (threadIdx.x == 0) { float a = 0; for (int w = 0; w < 16; ++w) a += sv[w]; sv[0] = a; }
+    __syncthreads();
+    z = sv[0];
+    const uint32_t ctr = step_ctr ? (uint32_t)step_ctr[m] : 0u;
+    const float u = (float)(hash_u32(seed ^ hash_u32(ctr * 0x9E3779B9u + (uint32_t)m)) >> 8) * 5.9604644775390625e-08f;
+    if (threadIdx.x == 0) {
+      // sequential inverse-CDF over candidates in index order (one thread: only ~k candidates pass)
+      float acc = 0.f;
+      int pick = -1, last = 0;
+      const float target = u * z;
+      for (int t = 0; t < V; ++t) {
+        if (lg[t] >= thr) {
+          acc += expf((lg[t] - mx) / temperature);
+          last = t;
+          if (acc > target) { pick = t; break; }
+        }
+      }
+      si[0] = pick < 0 ? last : pick;
+    }
+    __syncthreads();
+    tok = si[0];
+  }
+  if (threadIdx.x == 0) {
+    tok_out[m] = tok;
+    if (tok_hist) {
+      const int c = step_ctr ? step_ctr[m] : 0;
+      tok_hist[(int64_t)m * hist_stride + c] = tok;
+    }
+  }
+}
+
+void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
+                   float temperature, int top_k, float top_p, uint32_t seed, const int* step_ctr, int* tok_out,
+                   int* tok_hist, int hist_stride, hipStream_t s) {
+  hipLaunchKernelGGL(k_sample, dim3(M), dim3(1024), 0, s, logits, ldl, V, pval, pidx, n_part, temperature, top_k, top_p,
+                     seed, step_ctr, tok_out, tok_hist, hist_stride);
+}
+
+// advance per-token positions / counters after a decode step
+__global__ void k_advance(int* __restrict__ tok_pos, int* __restrict__ step_ctr, int M) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) { tok_pos[m] += 1; step_ctr[m] += 1; }
+}
+void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s) {
+  hipLaunchKernelGGL(k_advance, dim3(cdiv(M, 64)), dim3(64), 0, s, tok_pos, step_ctr, M);
+}
+
+}  // namespace fa

@@ -1,0 +1,254 @@
+"""ctypes binding of libfunasr_hip.so (include/funasr_hip.h).
+
+This is the product's only compute path: if the library (built in-tree by __graft_entry__.build())
+is missing, every call raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FUNASR_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libfunasr_hip.so"))
+
+EXPORTS = [
+    "fa_engine_create", "fa_engine_destroy", "fa_last_error", "fa_set_log_callback", "fa_weights_synthetic",
+    "fa_set_tensor_f32", "fa_set_tensor_q8_0", "fa_load_gguf", "fa_get_tensor_q8_0", "fa_encode",
+    "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
+    "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
+    "fa_profile_read", "fa_synchronize", "fa_align_timestamps",
+]
+
+
+class EncoderConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_mels", "lfr_m", "lfr_n", "d_in", "d_model", "n_heads", "d_ffn", "n_blocks", "n_tp_blocks", "fsmn_k",
+        "d_llm", "adaptor_ffn", "adaptor_blocks", "adaptor_heads", "ctc_blocks", "ctc_heads", "ctc_ffn", "ctc_vocab")]
+
+
+class LlmConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab", "n_ctx", "max_seqs")] + [
+        ("rope_theta", ctypes.c_float), ("rms_eps", ctypes.c_float)]
+
+
+class Sampling(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_p", ctypes.c_float), ("top_k", ctypes.c_int32),
+                ("seed", ctypes.c_uint32)]
+
+
+_lib = None
+LOG_CB = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.c_char_p, ctypes.c_void_p)
+
+
+def load():
+    """Load the engine library; raises if it is absent or does not export the full C-ABI."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libfunasr_hip.so not found at {LIB_PATH}: run __graft_entry__.build() first")
+    lib = ctypes.CDLL(LIB_PATH)
+    missing = [s for s in EXPORTS if not hasattr(lib, s)]
+    if missing:
+        raise RuntimeError(f"libfunasr_hip.so lacks symbols {missing}")
+    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    lib.fa_last_error.restype = ctypes.c_char_p
+    lib.fa_engine_create.argtypes = [I32, ctypes.POINTER(EncoderConfig), ctypes.POINTER(LlmConfig), I32, I64,
+                                     ctypes.POINTER(P)]
+    lib.fa_engine_destroy.argtypes = [P]
+    lib.fa_set_log_callback.argtypes = [LOG_CB, P]
+    lib.fa_weights_synthetic.argtypes = [P, ctypes.c_uint32]
+    lib.fa_set_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_set_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_get_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_load_gguf.argtypes = [P, ctypes.c_char_p]
+    lib.fa_encode.argtypes = [P, P, P, I32, I64, P, I64, P, I64, P, P, P]
+    lib.fa_encode_device.argtypes = [P, P, P, I32, I64]
+    lib.fa_encode_fetch.argtypes = [P, P, I64, P, I64, P, P, P]
+    lib.fa_ctc_collapse.argtypes = [P, I32, P, P, I64, P]
+    lib.fa_set_debug.argtypes = [P, I32]
+    lib.fa_encode_tap.argtypes = [P, I32, P, I64]
+    lib.fa_embd_rows.argtypes = [P, P, I32, I32, P]
+    lib.fa_llm_reset.argtypes = [P, I32]
+    lib.fa_llm_prefill.argtypes = [P, I32, P, I32, ctypes.POINTER(Sampling), P, P]
+    lib.fa_llm_generate.argtypes = [P, P, I32, I32, ctypes.POINTER(Sampling), P]
+    lib.fa_llm_logits.argtypes = [P, I32, P]
+    lib.fa_llm_n_past.argtypes = [P, I32, P]
+    lib.fa_profile_enable.argtypes = [P, I32]
+    lib.fa_profile_read.argtypes = [P, I32, P, P, P, P]
+    lib.fa_synchronize.argtypes = [P]
+    lib.fa_align_timestamps.argtypes = [P, P, I32, P, I32, P, P]
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {_lib.fa_last_error().decode(errors='replace')}")
+
+
+ENC_FIELDS = [f for f, _ in EncoderConfig._fields_]
+LLM_INT_FIELDS = ["n_layer", "n_embd", "n_head", "n_head_kv", "head_dim", "n_ff", "n_vocab", "n_ctx", "max_seqs"]
+
+
+class Engine:
+    """One device-bound engine (one per GPU). Owns all device memory; explicit close()."""
+
+    def __init__(self, enc_cfg, llm_cfg, max_batch=1, max_samples=16000 * 62, device=0):
+        lib = load()
+        self.enc_cfg = dict(enc_cfg)
+        self.llm_cfg = dict(llm_cfg)
+        self.llm_cfg.setdefault("n_ctx", 2048)
+        self.llm_cfg.setdefault("max_seqs", 1)
+        ec = EncoderConfig(**{k: int(self.enc_cfg[k]) for k in ENC_FIELDS})
+        lc = LlmConfig(**{k: int(self.llm_cfg[k]) for k in LLM_INT_FIELDS}, rope_theta=float(self.llm_cfg["rope_theta"]),
+                       rms_eps=float(self.llm_cfg["rms_eps"]))
+        h = ctypes.c_void_p()
+        _check(lib.fa_engine_create(device, ctypes.byref(ec), ctypes.byref(lc), max_batch, max_samples, ctypes.byref(h)),
+               "fa_engine_create")
+        self.h = h
+        self.max_batch = max_batch
+        self.max_samples = max_samples
+        self.lib = lib
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fa_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- weights
+    def synthetic_weights(self, seed=0):
+        _check(self.lib.fa_weights_synthetic(self.h, seed), "fa_weights_synthetic")
+
+    def set_tensor(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        _check(self.lib.fa_set_tensor_f32(self.h, name.encode(), _ptr(a), a.size), f"fa_set_tensor_f32({name})")
+
+    def set_tensor_q8_0(self, name, blocks):
+        b = np.ascontiguousarray(blocks, dtype=np.uint8)
+        _check(self.lib.fa_set_tensor_q8_0(self.h, name.encode(), _ptr(b), b.size), f"fa_set_tensor_q8_0({name})")
+
+    def get_tensor_q8_0(self, name, n_elements):
+        out = np.empty(n_elements // 32 * 34, np.uint8)
+        _check(self.lib.fa_get_tensor_q8_0(self.h, name.encode(), _ptr(out), out.size), "fa_get_tensor_q8_0")
+        return out
+
+    def load_gguf(self, path):
+        _check(self.lib.fa_load_gguf(self.h, os.fspath(path).encode()), "fa_load_gguf")
+
+    # ---- encoder
+    @staticmethod
+    def frame_counts(n):
+        t_mel = n // 160 + 1
+        t_lfr = (t_mel + 5) // 6
+        o1 = 1 + (t_lfr - 3 + 2) // 2
+        tgt = (1 + (o1 - 3 + 2) // 2 - 1) // 2 + 1
+        ctc_len = ((max(n, 16000) // 160 + 1) + 5) // 6
+        return t_lfr, tgt, ctc_len
+
+    def encode(self, clips, want_enc=False, debug_lfr=False):
+        """clips: list of 1-D float32 arrays. Returns dict(audio_embd=[...], ctc_ids=[...], enc=[...])."""
+        B = len(clips)
+        assert 1 <= B <= self.max_batch
+        stride = max(max(len(c) for c in clips), 1)
+        pcm = np.zeros((B, stride), np.float32)
+        for i, c in enumerate(clips):
+            pcm[i, :len(c)] = c
+        ns = np.array([len(c) for c in clips], np.int64)
+        counts = [self.frame_counts(int(n)) for n in ns]
+        tgt_stride = max(c[1] for c in counts)
+        ids_stride = max(c[2] for c in counts)
+        d_llm, d = self.enc_cfg["d_llm"], self.enc_cfg["d_model"]
+        emb = np.zeros((B, tgt_stride, d_llm), np.float32)
+        ids = np.zeros((B, ids_stride), np.int32)
+        tl = np.zeros(B, np.int32)
+        tg = np.zeros(B, np.int32)
+        enc = np.zeros((B, ids_stride, d), np.float32) if want_enc else None
+        if debug_lfr:
+            _check(self.lib.fa_set_debug(self.h, 1), "fa_set_debug")
+        _check(self.lib.fa_encode(self.h, _ptr(pcm), _ptr(ns), B, stride, _ptr(emb), tgt_stride, _ptr(ids), ids_stride,
+                                  _ptr(tl), _ptr(tg), _ptr(enc)), "fa_encode")
+        out = dict(audio_embd=[emb[b, :tg[b]] for b in range(B)], ctc_ids=[ids[b, :tl[b]] for b in range(B)],
+                   t_lfr=tl, target_len=tg)
+        if want_enc:
+            out["enc"] = [enc[b, :tl[b]] for b in range(B)]
+        if debug_lfr:
+            t0 = counts[0][2]
+            lfr = np.zeros((max(c[2] for c in counts), self.enc_cfg["d_in"]), np.float32)
+            _check(self.lib.fa_encode_tap(self.h, 0, _ptr(lfr), lfr.size), "fa_encode_tap")
+            out["lfr_embedded"] = lfr[:t0]
+            _check(self.lib.fa_set_debug(self.h, 0), "fa_set_debug")
+        return out
+
+    def ctc_collapse(self, blank_id, n_clips):
+        stride = self.frame_counts(self.max_samples)[2] + 1
+        ids = np.zeros((n_clips, stride), np.int32)
+        fr = np.zeros((n_clips, stride), np.int32)
+        n = np.zeros(n_clips, np.int32)
+        _check(self.lib.fa_ctc_collapse(self.h, blank_id, _ptr(ids), _ptr(fr), stride, _ptr(n)), "fa_ctc_collapse")
+        return [(ids[b, :n[b]], fr[b, :n[b]]) for b in range(n_clips)]
+
+    # ---- decoder
+    def embd_rows(self, ids, fp16_round=True):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        out = np.empty((ids.size, self.llm_cfg["n_embd"]), np.float32)
+        _check(self.lib.fa_embd_rows(self.h, _ptr(ids), ids.size, 1 if fp16_round else 0, _ptr(out)), "fa_embd_rows")
+        return out
+
+    def llm_reset(self, seq=0):
+        _check(self.lib.fa_llm_reset(self.h, seq), "fa_llm_reset")
+
+    @staticmethod
+    def _sampling(temperature=0.0, top_k=50, top_p=1.0, seed=0):
+        return Sampling(temperature=float(temperature), top_p=float(top_p), top_k=int(top_k), seed=int(seed) & 0xFFFFFFFF)
+
+    def llm_prefill(self, seq, embd, want_logits=False, **samp):
+        e = np.ascontiguousarray(embd, dtype=np.float32)
+        tok = ctypes.c_int32()
+        lg = np.empty(self.llm_cfg["n_vocab"], np.float32) if want_logits else None
+        s = self._sampling(**samp)
+        _check(self.lib.fa_llm_prefill(self.h, seq, _ptr(e), e.shape[0], ctypes.byref(s), ctypes.byref(tok), _ptr(lg)),
+               "fa_llm_prefill")
+        return (tok.value, lg) if want_logits else tok.value
+
+    def llm_generate(self, seqs, n_steps, **samp):
+        sq = np.ascontiguousarray(seqs, dtype=np.int32)
+        out = np.empty((sq.size, n_steps), np.int32)
+        s = self._sampling(**samp)
+        _check(self.lib.fa_llm_generate(self.h, _ptr(sq), sq.size, n_steps, ctypes.byref(s), _ptr(out)),
+               "fa_llm_generate")
+        return out
+
+    def llm_logits(self, row=0):
+        out = np.empty(self.llm_cfg["n_vocab"], np.float32)
+        _check(self.lib.fa_llm_logits(self.h, row, _ptr(out)), "fa_llm_logits")
+        return out
+
+    def llm_n_past(self, seq=0):
+        v = ctypes.c_int32()
+        _check(self.lib.fa_llm_n_past(self.h, seq, ctypes.byref(v)), "fa_llm_n_past")
+        return v.value
+
+    # ---- profiling
+    def profile_enable(self, on=True):
+        _check(self.lib.fa_profile_enable(self.h, 1 if on else 0), "fa_profile_enable")
+
+    def profile_read(self, cls):
+        ms, n, b, f = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        _check(self.lib.fa_profile_read(self.h, cls, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), ctypes.byref(f)),
+               "fa_profile_read")
+        return dict(ms=ms.value, launches=n.value, bytes=b.value, flops=f.value)
+
+    def synchronize(self):
+        _check(self.lib.fa_synchronize(self.h), "fa_synchronize")

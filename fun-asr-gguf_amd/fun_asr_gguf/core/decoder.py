@@ -1,0 +1,212 @@
+"""Per-segment hot path: encode -> CTC -> prompt -> LLM -> align
+(StreamDecoder.decode_stream, /root/reference/fun_asr_gguf/core/decoder.py:132-246).
+
+Differences in *mechanism* only (results are the reference's):
+  * encoder + CTC head + CTC argmax + greedy collapse run on the GPU in one fa_encode call;
+  * the LLM loop samples on the device and returns tokens in chunks (no per-token host round trip);
+    stop / repetition-breaker decisions are then replayed on the host in token order exactly as the
+    reference's loop takes them (decoder.py:91-114), so tokens the device produced after a stop are
+    discarded and never reach the output;
+  * decode_streams() runs several segments as one encoder batch + one continuous decoder batch.
+"""
+import codecs
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from ..nano_ctc import align_timestamps, decode_ctc_pairs
+from ..nano_dataclass import DecodeResult, LLMDecodeResult, RecognitionStream, Timings
+
+STOP_TOKENS = (151643, 151645)          # decoder.py:53
+ABORT_MARK = "====解码有误，强制熔断===="   # decoder.py:210
+GEN_CHUNK = 32
+
+
+class PieceStream:
+    """ASRStreamDecoder (llama.py:661-690): incremental UTF-8 decode of token pieces."""
+
+    def __init__(self, vocab, reporter=None):
+        self.vocab = vocab
+        self.reporter = reporter
+        self.dec = codecs.getincrementaldecoder("utf-8")(errors="replace")
+        self.generated_text = ""
+        self.tokens_generated = 0
+        self.tokens = []
+
+    def push(self, tid):
+        piece = self.dec.decode(self.vocab.token_to_bytes(tid), final=False)
+        self.tokens.append(piece)
+        self.tokens_generated += 1
+        self.generated_text += piece
+        if self.reporter:
+            self.reporter.stream(piece)
+        return piece
+
+    def flush(self):
+        rem = self.dec.decode(b"", final=True)
+        self.tokens.append(rem)
+        self.generated_text += rem
+        return rem
+
+
+class _SeqState:
+    def __init__(self, vocab, n_predict, eos, ignore_eos, reporter):
+        self.ps = PieceStream(vocab, reporter)
+        self.n_predict = n_predict
+        self.eos = eos
+        self.ignore_eos = ignore_eos
+        self.sampled = 0
+        self.done = False
+        self.aborted = False
+
+    def feed(self, tokens):
+        for t in tokens:
+            if self.done:
+                return
+            self.sampled += 1
+            t = int(t)
+            if not self.ignore_eos and (t == self.eos or t in STOP_TOKENS):
+                self.done = True
+                return
+            self.ps.push(t)
+            if len(self.ps.tokens) > 30 and len(set(self.ps.tokens[-30:])) <= 3:
+                self.aborted = True
+                self.done = True
+                return
+            if self.sampled >= self.n_predict:
+                self.done = True
+
+    def remaining(self):
+        return 0 if self.done else self.n_predict - self.sampled
+
+
+class LLMDecoder:
+    def __init__(self, models):
+        self.models = models
+
+    def _sampling(self, temperature, top_p, top_k):
+        seed = int(np.random.randint(0, 2 ** 31 - 1))  # decoder.py:89: fresh seed per call
+        return dict(temperature=temperature, top_p=top_p, top_k=top_k, seed=seed)
+
+    def decode_many(self, embds, n_predict, temperature=0.3, top_p=1.0, top_k=50, reporter=None, stream_output=False):
+        """Prefill every sequence, then decode them as one continuous batch. -> [LLMDecodeResult]"""
+        eng = self.models.engine
+        cfg = self.models.config
+        samp = self._sampling(temperature, top_p, top_k)
+        states, res = [], []
+        for s, e in enumerate(embds):
+            r = LLMDecodeResult()
+            t0 = time.perf_counter()
+            eng.llm_reset(s)
+            first = eng.llm_prefill(s, e, **samp)
+            r.t_inject = time.perf_counter() - t0
+            st = _SeqState(self.models.vocab, n_predict, self.models.eos_token, cfg.ignore_eos,
+                           reporter if stream_output and len(embds) == 1 else None)
+            st.feed([first])
+            states.append(st)
+            res.append(r)
+        t_gen = time.perf_counter()
+        while True:
+            active = [s for s, st in enumerate(states) if not st.done]
+            if not active:
+                break
+            chunk = min(GEN_CHUNK, max(states[s].remaining() for s in active))
+            toks = eng.llm_generate(active, chunk, **samp)
+            for row, s in enumerate(active):
+                states[s].feed(toks[row])
+        dt = time.perf_counter() - t_gen
+        for st, r in zip(states, res):
+            st.ps.flush()
+            r.text = st.ps.generated_text
+            r.n_gen = st.ps.tokens_generated
+            r.t_gen = dt
+            r.is_aborted = st.aborted
+        return res
+
+    def decode(self, full_embd, n_input_tokens, n_predict, stream_output=False, reporter=None, temperature=0.3,
+               top_p=1.0, top_k=50):
+        return self.decode_many([full_embd], n_predict, temperature, top_p, top_k, reporter, stream_output)[0]
+
+
+class StreamDecoder:
+    def __init__(self, models):
+        self.models = models
+        self.llm_decoder = LLMDecoder(models)
+
+    def decode_stream(self, stream: RecognitionStream, language=None, context=None, verbose=True, reporter=None,
+                      temperature=0.3, top_p=1.0, top_k=50) -> DecodeResult:
+        return self.decode_streams([stream], language, context, verbose, reporter, temperature, top_p, top_k)[0]
+
+    def decode_streams(self, streams: List[RecognitionStream], language=None, context=None, verbose=True,
+                       reporter=None, temperature=0.3, top_p=1.0, top_k=50) -> List[DecodeResult]:
+        m = self.models
+        eng = m.engine
+        B = len(streams)
+        timings = [Timings() for _ in range(B)]
+        # 1. encode (+ CTC head + argmax) — one device batch
+        t = time.perf_counter()
+        out = eng.encode([s.audio_data for s in streams])
+        dt = time.perf_counter() - t
+        for tm in timings:
+            tm.encode = dt
+            tm.ctc_infer = 0.0  # fused into the encode call
+        # 2. CTC collapse on device + host token map + hotwords
+        t = time.perf_counter()
+        ctc_results, hotwords = [[] for _ in range(B)], [[] for _ in range(B)]
+        if m.config.enable_ctc:
+            blank = max(m.ctc_id2token.keys()) if m.ctc_id2token else 0
+            pairs = eng.ctc_collapse(blank, B)
+            for b in range(B):
+                txt, ctc_results[b] = decode_ctc_pairs(pairs[b][0], pairs[b][1], m.ctc_id2token)
+                hotwords[b] = m.match_hotwords(txt, m.config.max_hotwords)
+        dt = time.perf_counter() - t
+        for tm in timings:
+            tm.ctc = tm.ctc_decode = dt / B
+        # 3. prompt
+        t = time.perf_counter()
+        embds, n_ps = [], []
+        for b in range(B):
+            pe, se, n_p, n_s, _ = m.prompt_builder.build_prompt(hotwords[b], language, context)
+            embds.append(np.concatenate([pe, out["audio_embd"][b].astype(np.float32), se], 0))
+            n_ps.append((n_p, n_s))
+        dt = time.perf_counter() - t
+        for tm in timings:
+            tm.prepare = dt / B
+        # 4. LLM with the reference's retry policy (decoder.py:201-211), per sequence
+        n_predict = m.config.n_predict
+        temps = [temperature] * B
+        final = [None] * B
+        pending = list(range(B))
+        for attempt in range(6):
+            rs = self.llm_decoder.decode_many([embds[b] for b in pending], n_predict, temps[pending[0]], top_p, top_k,
+                                              reporter, verbose)
+            nxt = []
+            for b, r in zip(pending, rs):
+                if r.is_aborted and attempt < 5:
+                    temps[b] += 0.3
+                    nxt.append(b)
+                elif r.is_aborted:
+                    r.text += ABORT_MARK
+                    final[b] = r
+                else:
+                    final[b] = r
+            if not nxt:
+                break
+            pending = nxt
+        results = []
+        for b in range(B):
+            r = final[b]
+            text = r.text.strip()
+            tm = timings[b]
+            tm.inject, tm.llm_generate = r.t_inject, r.t_gen
+            t = time.perf_counter()
+            aligned = align_timestamps(ctc_results[b], text) if ctc_results[b] else None
+            tm.align = time.perf_counter() - t
+            toks = [a["char"] for a in aligned] if aligned else []
+            ts = [a["start"] for a in aligned] if aligned else []
+            streams[b].set_result(text=text, timestamps=ts, tokens=toks)
+            results.append(DecodeResult(text=text, ctc_results=ctc_results[b], aligned=aligned,
+                                        audio_embd=out["audio_embd"][b], n_prefix=n_ps[b][0], n_suffix=n_ps[b][1],
+                                        n_gen=r.n_gen, timings=tm, hotwords=hotwords[b], is_aborted=r.is_aborted))
+        return results

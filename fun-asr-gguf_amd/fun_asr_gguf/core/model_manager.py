@@ -1,0 +1,120 @@
+"""Engine initialisation (ModelManager.initialize, /root/reference/fun_asr_gguf/core/model_manager.py:36-100).
+
+Creates the device-bound native engine and fills its weights:
+  * "synthetic" (or a missing path) -> the repo's deterministic synthetic weights (oracle/synth.py spec);
+  * encoder/CTC: a PyTorch/safetensors state dict (model.pt keys audio_encoder.*, audio_adaptor.*,
+    ctc_decoder.*, ctc.ctc_lo.* -> ctc_proj.ctc_lo.*, as HybridSenseVoice.load_weights,
+    model_definition.py:231-238), loaded with weights_only=True;
+  * decoder: a GGUF file (q8_0/f16/f32 tensors + tokenizer metadata) through fa_load_gguf.
+Any failure returns False (the reference swallows init exceptions the same way, :98-100).
+"""
+import logging
+import os
+import time
+
+from .. import _native
+from ..model_config import MODELS
+from ..nano_ctc import load_ctc_tokens
+from ..prompt_utils import PromptBuilder
+from ..vocab import CTCSyntheticTokens, GGUFVocab, SyntheticVocab
+
+log = logging.getLogger("fun_asr_gguf")
+
+
+def _is_synthetic(p):
+    return p is None or str(p).startswith("synthetic")
+
+
+def load_encoder_state_dict(engine, path):
+    if str(path).endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        sd = load_file(path)
+    else:
+        import torch
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        if "state_dict" in sd:
+            sd = sd["state_dict"]
+        sd = {k: v.float().numpy() for k, v in sd.items() if hasattr(v, "float")}
+    n = 0
+    for k, v in sd.items():
+        if k.startswith(("audio_encoder.", "audio_adaptor.", "ctc_decoder.")):
+            name = k
+        elif k.startswith("ctc.ctc_lo."):
+            name = k.replace("ctc.ctc_lo", "ctc_proj.ctc_lo")
+        else:
+            continue
+        engine.set_tensor(name, v)
+        n += 1
+    return n
+
+
+class ModelManager:
+    def __init__(self, config):
+        self.config = config
+        self.engine = None
+        self.vocab = None
+        self.eos_token = None
+        self.ctc_id2token = None
+        self.prompt_builder = None
+        self.hotwords = []
+        self.enc_cfg = None
+        self.llm_cfg = None
+        self._initialized = False
+
+    def initialize(self, verbose=True):
+        if self._initialized:
+            return True
+        try:
+            t0 = time.perf_counter()
+            c = self.config
+            enc_cfg, llm_cfg = MODELS[c.model]
+            self.enc_cfg = dict(enc_cfg)
+            self.llm_cfg = dict(llm_cfg, n_ctx=c.n_ctx, max_seqs=max(1, c.max_batch))
+            gguf_kv = None
+            if not _is_synthetic(c.decoder_gguf_path):
+                from ..vocab import read_gguf_metadata
+                gguf_kv = read_gguf_metadata(c.decoder_gguf_path)
+                self.llm_cfg["n_vocab"] = len(gguf_kv["tokenizer.ggml.tokens"])
+            # segments up to segment_size + 2 s (orchestrator short path) fit one encode
+            self.engine = _native.Engine(self.enc_cfg, self.llm_cfg, max_batch=max(1, c.max_batch),
+                                         max_samples=c.sample_rate * 64, device=c.device)
+            self.engine.synthetic_weights(c.synthetic_seed)
+            if not _is_synthetic(c.encoder_onnx_path):
+                if str(c.encoder_onnx_path).endswith(".onnx"):
+                    raise NotImplementedError("ONNX initializer ingestion is not implemented; pass model.pt")
+                load_encoder_state_dict(self.engine, c.encoder_onnx_path)
+            if gguf_kv is not None:
+                self.engine.load_gguf(c.decoder_gguf_path)
+                self.vocab = GGUFVocab(kv=gguf_kv)
+            else:
+                self.vocab = SyntheticVocab(self.llm_cfg["n_vocab"])
+            self.eos_token = self.vocab.eos
+            if _is_synthetic(c.tokens_path) or not os.path.exists(c.tokens_path):
+                self.ctc_id2token = CTCSyntheticTokens(self.enc_cfg["ctc_vocab"])
+            else:
+                self.ctc_id2token = load_ctc_tokens(c.tokens_path)
+            self.prompt_builder = PromptBuilder(self.vocab, self.engine)
+            if c.hotwords_path and os.path.exists(c.hotwords_path):
+                with open(c.hotwords_path, encoding="utf-8") as f:
+                    self.hotwords = [ln.strip() for ln in f if ln.strip() and not ln.startswith("#")]
+            self._initialized = True
+            if verbose:
+                print(f"✓ 模型加载完成 (耗时: {time.perf_counter() - t0:.2f}s)")
+            return True
+        except Exception as e:  # same contract as the reference: report and return False
+            log.exception("initialize failed")
+            if verbose:
+                print(f"✗ 初始化失败: {e}")
+            return False
+
+    def match_hotwords(self, ctc_text, k):
+        """Hotwords that occur verbatim in the CTC text (phoneme retrieval is out of scope)."""
+        if not ctc_text or not self.hotwords:
+            return []
+        return [h for h in self.hotwords if h in ctc_text][:k]
+
+    def cleanup(self):
+        if self.engine is not None:
+            self.engine.close()
+        self.engine = None
+        self._initialized = False

@@ -1,0 +1,62 @@
+"""Segment/clip data parallelism across the GPUs of one node.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on ROCm, "gloo" in CPU tests).
+Segments are assigned longest-first to the least-loaded rank (LPT); every rank decodes its share as one
+device batch; the only exchange is the result gather to rank 0 (gather_object of small per-segment
+records: text, char timestamps, hotwords, CTC tokens, timings), after which rank 0 merges. No data-path
+collective: the PCM chunks are cut from the same input on every rank.
+"""
+from dataclasses import asdict
+
+from .nano_ctc import Token
+from .nano_dataclass import DecodeResult, Timings
+
+
+def lpt_assign(lengths, world):
+    """Longest-processing-time-first: -> list of index lists, one per rank (deterministic)."""
+    order = sorted(range(len(lengths)), key=lambda i: (-lengths[i], i))
+    load = [0.0] * world
+    out = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(i)
+        load[r] += lengths[i]
+    return [sorted(x) for x in out]
+
+
+def to_record(d):
+    return dict(text=d.text, aligned=d.aligned, hotwords=d.hotwords, n_gen=d.n_gen, is_aborted=d.is_aborted,
+                ctc=[(t.text, t.start) for t in (d.ctc_results or [])], timings=asdict(d.timings),
+                n_prefix=d.n_prefix, n_suffix=d.n_suffix)
+
+
+def from_record(r):
+    return DecodeResult(text=r["text"], aligned=r["aligned"], hotwords=r["hotwords"], n_gen=r["n_gen"],
+                        is_aborted=r["is_aborted"], ctc_results=[Token(t, s) for t, s in r["ctc"]],
+                        timings=Timings(**r["timings"]), n_prefix=r["n_prefix"], n_suffix=r["n_suffix"])
+
+
+def gather_to_root(records_by_index, n_total, dist, group=None):
+    """records_by_index: {segment index: record} of this rank -> full ordered list on rank 0, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    bucket = [None] * world if rank == 0 else None
+    dist.gather_object(records_by_index, bucket, dst=0, group=group)
+    if rank != 0:
+        return None
+    merged = {}
+    for part in bucket:
+        merged.update(part)
+    assert len(merged) == n_total, f"gather lost segments: {len(merged)} of {n_total}"
+    return [merged[i] for i in range(n_total)]
+
+
+def sharded_decode(orch, chunks, language, context, verbose, temperature, top_p, top_k, dist):
+    """Decode `chunks` across the ranks of `dist` (the torch.distributed module, initialised)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    mine = lpt_assign([len(c) for c in chunks], world)[rank]
+    local = orch.decode_segments([chunks[i] for i in mine], language, context, verbose, temperature, top_p,
+                                 top_k) if mine else []
+    recs = {i: to_record(d) for i, d in zip(mine, local)}
+    full = gather_to_root(recs, len(chunks), dist)
+    return None if full is None else [from_record(r) for r in full]

@@ -1,0 +1,141 @@
+/*
+ * funasr_hip.h — C-ABI of the MI355X-native Fun-ASR hot-path engine (libfunasr_hip.so).
+ *
+ * Replaces the two native runtimes the reference drives from Python on its per-segment hot path
+ * (SURVEY.md §8(b)):
+ *   - onnxruntime sessions for the encoder+adaptor graph and the CTC graph
+ *       /root/reference/fun_asr_gguf/nano_onnx.py:78-133 (encode_audio -> run_with_ort_values)
+ *       /root/reference/fun_asr_gguf/core/decoder.py:27 (ctc_sess.run -> indices int32)
+ *   - llama.cpp b7798 bound by ctypes (llama.py:150-349): llama_model_load_from_file,
+ *     llama_init_from_model, llama_batch_init/set_embd, llama_decode, llama_memory_clear,
+ *     llama_sampler_* , llama_get_logits (llama.py:462-659)
+ *
+ * Conventions: plain pointers + sizes, no torch types. Host buffers are owned by the caller and
+ * read-only during a call; every device allocation is owned by the engine. Every fa_* returns 0 on
+ * success and a negative code on failure; fa_last_error() returns a thread-local message.
+ * Calls on one engine are serialised by the caller (the reference engine is not re-entrant either:
+ * one KV cache, decoder.py:71). One engine per GPU.
+ */
+#ifndef FUNASR_HIP_H
+#define FUNASR_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FA_OK 0
+#define FA_ERR_ARG -1
+#define FA_ERR_HIP -2
+#define FA_ERR_STATE -3
+#define FA_ERR_IO -4
+#define FA_ERR_NOTFOUND -5
+
+typedef struct fa_engine fa_engine;
+
+/* Encoder/adaptor/CTC dimensions (model_definition.py:191-229). */
+typedef struct fa_encoder_config {
+  int32_t n_mels, lfr_m, lfr_n, d_in, d_model, n_heads, d_ffn, n_blocks, n_tp_blocks, fsmn_k;
+  int32_t d_llm, adaptor_ffn, adaptor_blocks, adaptor_heads;
+  int32_t ctc_blocks, ctc_heads, ctc_ffn, ctc_vocab;
+} fa_encoder_config;
+
+/* Qwen3 decoder dimensions (GGUF qwen3 arch). n_ctx matches LlamaContext(n_ctx=2048),
+ * model_manager.py:63-69; max_seqs is the continuous-batch width (1 in the reference). */
+typedef struct fa_llm_config {
+  int32_t n_layer, n_embd, n_head, n_head_kv, head_dim, n_ff, n_vocab, n_ctx, max_seqs;
+  float rope_theta, rms_eps;
+} fa_llm_config;
+
+/* Sampler chain of LlamaSampler (llama.py:577-605): temperature <= 0 -> greedy;
+ * else top_k -> top_p -> temp -> dist(seed). */
+typedef struct fa_sampling {
+  float temperature, top_p;
+  int32_t top_k;
+  uint32_t seed;
+} fa_sampling;
+
+/* ---- lifecycle (replaces load_onnx_models nano_onnx.py:21-76, LlamaModel/LlamaContext llama.py:352-488) */
+int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_config* llm,
+                     int32_t max_batch, int64_t max_samples, fa_engine** out);
+int fa_engine_destroy(fa_engine* e);
+const char* fa_last_error(void);
+/* llama_log_set-style callback (llama.py:692-732): level 2 error, 3 warn, 4 info, 5 debug. */
+int fa_set_log_callback(void (*cb)(int32_t level, const char* msg, void* user), void* user);
+
+/* ---- weights */
+/* Deterministic synthetic weights generated on device (spec: oracle/synth.py; real weights absent). */
+int fa_weights_synthetic(fa_engine* e, uint32_t seed);
+/* Upload one tensor by reference state_dict / GGUF name. Decoder 2-D tensors given as f32 are
+ * quantised to q8_0 on device with the ggml reference quantiser (gguf/quants.py:378-393). */
+int fa_set_tensor_f32(fa_engine* e, const char* name, const float* host, int64_t n);
+int fa_set_tensor_q8_0(fa_engine* e, const char* name, const uint8_t* blocks, int64_t n_bytes);
+/* Decoder weights from a GGUF v3 file (q8_0 / f32 / f16 tensors) — replaces llama_model_load_from_file. */
+int fa_load_gguf(fa_engine* e, const char* path);
+/* Copy a decoder tensor back as ggml q8_0 blocks (test hook). */
+int fa_get_tensor_q8_0(fa_engine* e, const char* name, uint8_t* out, int64_t n_bytes);
+
+/* ---- encoder operator (replaces encoder_sess.run_with_ort_values + ctc_sess.run)
+ * pcm: batch clips, clip b at pcm + b*stride with n_samples[b] valid samples (16 kHz f32).
+ * Outputs (host, may be NULL to skip):
+ *   audio_embd_out [batch, tgt_stride, d_llm]   adaptor rows < target_len[b] (nano_onnx.py:129-131)
+ *   ctc_ids_out    [batch, ids_stride]          argmax ids for frames < t_lfr[b] (model_definition.py:337)
+ *   enc_out        [batch, ids_stride, d_model] encoder output (test hook)
+ * t_lfr_out/target_len_out [batch]. A padded batch reproduces the unpadded per-clip result. */
+int fa_encode(fa_engine* e, const float* pcm, const int64_t* n_samples, int32_t batch, int64_t stride,
+              float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out, int64_t ids_stride,
+              int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out);
+/* Same, but pcm is a DEVICE pointer (inputs already resident in HBM) and the ids/lengths are left on
+ * device; fa_encode_fetch copies them out. Used by the benchmark and the batch scheduler. */
+int fa_encode_device(fa_engine* e, const float* d_pcm, const int64_t* n_samples, int32_t batch, int64_t stride);
+int fa_encode_fetch(fa_engine* e, float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out,
+                    int64_t ids_stride, int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out);
+/* Greedy CTC collapse on device (nano_ctc.py:65-104): for clip b, compacted (id, first_frame) pairs
+ * with blanks (= blank_id) and repeats removed; n_out[b] = count. */
+int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* frames_out, int64_t out_stride,
+                    int32_t* n_out);
+/* Debug hooks (tests): flags bit 0 keeps clip 0's embedded LFR features (x*sqrt(512)+PE, [T, d_in]) of
+ * the next fa_encode; fa_encode_tap(e, 0, out, n) copies them out. */
+int fa_set_debug(fa_engine* e, int32_t flags);
+int fa_encode_tap(fa_engine* e, int32_t which, float* out, int64_t n);
+
+/* ---- decoder operator (replaces llama_decode / llama_sampler_sample / llama_memory_clear) */
+/* Embedding rows from token_embd (q8_0). fp16_round=1 reproduces the numpy f16 product of
+ * get_token_embeddings_gguf (llama.py:782-784) used for prompt rows; 0 = ggml get_rows (f32). */
+int fa_embd_rows(fa_engine* e, const int32_t* ids, int32_t n, int32_t fp16_round, float* out);
+/* llama_memory_clear for one sequence slot. */
+int fa_llm_reset(fa_engine* e, int32_t seq);
+/* Prefill a sequence with n_tokens input embeddings [n_tokens, n_embd] f32 (LlamaBatch.set_embd with
+ * token=NULL, logits on the last row only; llama.py:536-558, decoder.py:70-80), then sample the first
+ * token with `s`. logits_out (nullable) receives the last-row logits [n_vocab]. */
+int fa_llm_prefill(fa_engine* e, int32_t seq, const float* embd, int32_t n_tokens, const fa_sampling* s,
+                   int32_t* tok_out, float* logits_out);
+/* Run n_steps decode steps for n_seqs sequences in one continuous batch: each step feeds every
+ * sequence's last sampled token at its next position and samples the next one on device
+ * (decoder.py:91-98). tokens_out [n_seqs, n_steps]. No host round trip inside the call. */
+int fa_llm_generate(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
+                    int32_t* tokens_out);
+/* Logits of the most recent forward for a sequence slot (test hook) [n_vocab]. */
+int fa_llm_logits(fa_engine* e, int32_t seq, float* out);
+/* Current length (n_past) of a sequence slot. */
+int fa_llm_n_past(fa_engine* e, int32_t seq, int32_t* out);
+
+/* ---- host-side char alignment (replaces nano_ctc.align_timestamps, nano_ctc.py:118-232)
+ * ctc_keys/llm_keys: per-char integer keys (equal iff the chars' .lower() strings are equal);
+ * ctc_starts: per-CTC-char start seconds (token start + i*0.08). starts_out[n_llm] receives each LLM
+ * char's start; aligned_out[n_llm] (nullable) the matched CTC char index or -1. Bit-identical to the
+ * reference (same tie order, same float64 evaluation order). Pure host code, no device needed. */
+int fa_align_timestamps(const int32_t* ctc_keys, const double* ctc_starts, int32_t n_ctc, const int32_t* llm_keys,
+                        int32_t n_llm, double* starts_out, int32_t* aligned_out);
+
+/* ---- timing hooks for bench.py roofline (HIP events on the engine's stream) */
+/* Enable per-kernel-class event timing; fa_profile_read returns accumulated ms and launch counts for
+ * class ids: 0 q8 GEMV (decode), 1 f32 GEMM (encoder), 2 encoder attention, 3 decode attention. */
+int fa_profile_enable(fa_engine* e, int32_t on);
+int fa_profile_read(fa_engine* e, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops);
+int fa_synchronize(fa_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

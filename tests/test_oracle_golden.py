@@ -72,3 +72,17 @@ def test_qwen3_oracle_anchored_on_hf():
     assert cos.min() >= 0.999
     assert (lg.argmax(-1) == ref.argmax(-1)).mean() >= 0.9
     assert m.greedy(h["prompt"], 6) == list(h["greedy"])
+
+
+def test_qwen3_q8_noise_floor():
+    """Documents the decoder's numerical noise floor used by the GPU parity tolerances: 1e-6 additive
+    input noise moves q8_0-activation logits by O(0.05) (rounding flips), but keeps cosine > 0.9995."""
+    cfg = synth.LLM_TINY
+    m = qwen3.Qwen3Q8(synth.make_weights(synth.llm_tensors(cfg)), cfg, n_ctx=64)
+    rng = np.random.default_rng(3)
+    p = (rng.standard_normal((16, 1024)) * 0.5).astype(np.float32)
+    a = m.forward(p, 0)
+    m.reset()
+    b = m.forward(p + (rng.standard_normal(p.shape) * 1e-6).astype(np.float32), 0)
+    cos = float(a @ b / np.linalg.norm(a) / np.linalg.norm(b))
+    assert 0.9995 < cos < 1.0 and np.abs(a - b).max() > 1e-3
