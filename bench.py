@@ -1,0 +1,195 @@
+"""Benchmark of the Fun-ASR hot path on MI355X (BASELINE.json metric: RTF and audio-sec/s/GPU on 60 s
+16 kHz clips). Workload = configs[1]: one 60 s clip per step per GPU through the full product path
+(FunASREngine.decode_stream: GPU frontend + fp32 encoder + adaptor + CTC head/argmax/collapse, prompt,
+q8_0 Qwen3 prefill of 73 + 126 + 5 tokens, 253 greedy decode steps with EOS ignored, native alignment).
+Synthetic seeded audio and synthetic weights of the full architecture (no checkpoints ship).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Prints ONE JSON line on rank 0. value = total audio seconds of all ranks / max-over-ranks wall time of the
+K timed steps (inputs resident in HBM: fa_pcm_upload before the timed region).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "fun-asr-gguf_amd")]
+
+import numpy as np  # noqa: E402
+
+CLIP_S = 60.0
+SR = 16000
+N_PREFIX, N_SUFFIX, N_GEN = 73, 5, 253   # README.md:244-268 (204 input tokens, 253 generated)
+HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md chip table (spec)
+FP32_MFMA_PEAK_TFS = 157.3
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample_clip_s=10.0, n_steps=4):
+    """Oracle (numpy, 'port') on a bounded sample: full encoder on a 10 s clip, prefill of 204 tokens,
+    n_steps decode steps; extrapolated to one 60 s clip (encoder x6, + prefill + 253 steps)."""
+    from oracle import encoder as oenc, qwen3 as oqw, synth
+    from fun_asr_gguf.synthetic import synth_audio
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    W = synth.make_weights(synth.encoder_tensors(synth.ENC_FULL))
+    a = synth_audio(int(sample_clip_s * SR), 0)
+    t = time.perf_counter()
+    r = oenc.encode(a, W, synth.ENC_FULL)
+    t_enc = time.perf_counter() - t
+    del W
+    m = oqw.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_FULL)), synth.LLM_FULL, n_ctx=512)
+    rng = np.random.default_rng(0)
+    prompt = np.concatenate([m.embed_prompt(rng.integers(0, 151936, N_PREFIX)), np.repeat(r["audio_embd"], 6, 0)[:126],
+                             m.embed_prompt(rng.integers(0, 151936, N_SUFFIX))], 0)
+    t = time.perf_counter()
+    lg = m.forward(prompt, 0)
+    t_pre = time.perf_counter() - t
+    pos = prompt.shape[0]
+    t = time.perf_counter()
+    for _ in range(n_steps):
+        lg = m.forward(m.embed_tokens([int(np.argmax(lg))]), pos)
+        pos += 1
+    t_step = (time.perf_counter() - t) / n_steps
+    t_clip = t_enc * (CLIP_S / sample_clip_s) + t_pre + N_GEN * t_step
+    return {"value": round(CLIP_S / t_clip, 4), "unit": "audio_s/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/ numpy fp32 encoder on a {sample_clip_s:.0f} s clip ({t_enc:.2f} s) + q8_0 Qwen3 prefill "
+                      f"204 tok ({t_pre:.2f} s) + {n_steps} decode steps ({t_step:.2f} s/step), extrapolated to one "
+                      f"60 s clip = {t_clip:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--model", default="full")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    from fun_asr_gguf import FunASREngine
+    from fun_asr_gguf.nano_dataclass import RecognitionStream
+    from fun_asr_gguf.synthetic import synth_audio
+
+    eng = FunASREngine("synthetic", "synthetic", "synthetic", "synthetic", n_predict=N_GEN, device=local,
+                       model=args.model, ignore_eos=True)
+    if not eng.initialize(verbose=False):
+        raise RuntimeError("engine init failed")
+    m = eng.models
+    rng = np.random.default_rng(1234)
+    m.prompt_builder.fixed_ids = (list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_PREFIX)),
+                                  list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_SUFFIX)))
+    clip = synth_audio(int(CLIP_S * SR), rank)
+    st = RecognitionStream()
+    st.accept_waveform(SR, clip)
+    handle = m.engine.upload([clip])
+    dec = eng.orchestrator.decoder
+
+    def step():
+        return dec.decode_streams([st], verbose=False, temperature=0.0, resident=handle)[0]
+
+    for _ in range(args.warmup):
+        res = step()
+    assert res.n_gen == N_GEN, res.n_gen
+    m.engine.synchronize()
+    barrier()
+    # ---- timed region (production path: hipGraph decode steps, no timing events)
+    t0 = time.perf_counter()
+    stage = np.zeros(6)
+    for _ in range(args.steps):
+        res = step()
+        tm = res.timings
+        stage += [tm.encode, tm.ctc, tm.prepare, tm.inject, tm.llm_generate, tm.align]
+    m.engine.synchronize()
+    dt = time.perf_counter() - t0
+    barrier()
+    # ---- roofline pass: same steps with HIP events on the engine stream around every launch of each
+    # kernel class (decode: event nodes captured inside the step graph, replayed on the last step of every
+    # 32-step chunk, i.e. a uniform sample of the decode launches)
+    m.engine.profile_enable(True)
+    tp = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    m.engine.synchronize()
+    dt_prof = time.perf_counter() - tp
+    prof = {c: m.engine.profile_read(c) for c in range(4)}
+    m.engine.profile_enable(False)
+    barrier()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    audio_s = CLIP_S * args.steps * world
+    value = audio_s / dt
+    ms_step = dt / args.steps * 1e3
+    # dominant kernel class by measured device time
+    names = {0: "q8_0 GEMV/GEMM (decoder)", 1: "f32 MFMA GEMM (encoder)", 2: "f32 MFMA attention (encoder)",
+             3: "decode attention"}
+    dom = max(prof, key=lambda c: prof[c]["ms"])
+    p = prof[dom]
+    if dom == 0:
+        avg_s = p["ms"] / max(1, p["launches"]) / 1e3
+        ach = p["bytes"] / max(1, p["launches"]) / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    else:
+        avg_s = p["ms"] / max(1, p["launches"]) / 1e3
+        ach = p["flops"] / max(1, p["launches"]) / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFS, 4), "traffic": None}
+    roof.update(kernel=names[dom], avg_launch_us=round(avg_s * 1e6, 2), launches=p["launches"],
+                per_launch=("q8_0 weight bytes" if dom == 0 else "algorithmic FLOPs"))
+    out = {"metric": "audio-sec/s (RTF = 1/value per GPU) on 60 s 16 kHz clips", "value": round(value, 3),
+           "unit": "audio_s/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32 encoder / q8_0 x q8_0 int-dot decoder", "data": "synthetic (seeded chirps; synthetic weights)",
+           "rtf": round(1.0 / (value / world), 6),
+           "config": {"workload": "configs[1]: single 60 s clip per GPU per step, fp32 encoder + CTC + q8_0 LLM "
+                                  "(73+126+5 prefill, 253 greedy steps, EOS ignored)",
+                      "model": "Fun-ASR-Nano (SenseVoiceSmall enc 70 SANM blocks + Qwen3-0.6B q8_0)",
+                      "global_batch": world, "seq_len": int(CLIP_S * SR), "parallelism": f"dp{world}"},
+           "stage_ms": {k: round(v / args.steps * 1e3, 3) for k, v in zip(
+               ["encode", "ctc", "prompt", "prefill", "generate", "align"], stage)},
+           "profiled_pass_ms_per_step": round(dt_prof / args.steps * 1e3, 3),
+           "kernel_class_avg_us": {names[c]: round(prof[c]["ms"] * 1e3 / max(1, prof[c]["launches"]), 2) for c in prof},
+           "roofline": roof}
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
+    print(json.dumps(out, ensure_ascii=False), flush=True)
+    eng.cleanup()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -110,6 +111,7 @@ struct Engine {
   int *d_tmel = nullptr, *d_tlfr = nullptr, *d_tgt = nullptr, *d_ctclen = nullptr;
   int *d_col_ids = nullptr, *d_col_frames = nullptr, *d_col_n = nullptr;
   int debug_flags = 0;
+  int64_t pcm_uploaded = 0;
   float* tap_lfr = nullptr;
   // last encode geometry
   int last_batch = 0, last_tstride = 0;
@@ -128,6 +130,8 @@ struct Engine {
   float* lxd = nullptr;
   float* pval = nullptr;
   int* pidx = nullptr;
+  float* attn_part = nullptr;
+  int n_chunks_max = 0;
   int *d_tok_seq = nullptr, *d_tok_pos = nullptr, *d_step = nullptr, *d_tok_cur = nullptr, *d_tok_hist = nullptr,
       *d_ids = nullptr;
   int hist_max = 0;
@@ -139,7 +143,7 @@ struct Engine {
     double ms = 0, bytes = 0, flops = 0;
     int64_t launches = 0;
   } pcls[4];
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool, graph_events;
   struct Pending {
     int cls;
     hipEvent_t a, b;
@@ -147,6 +151,12 @@ struct Engine {
   };
   std::vector<Pending> pending;
   size_t ev_next = 0;
+  struct StepGraph {
+    hipGraphExec_t exec = nullptr;
+    std::vector<Pending> events;  // profiled variant: (class, start, end) event pairs inside the graph
+  };
+  std::unordered_map<int, StepGraph> step_graphs, prof_graphs;
+  bool use_graphs = true;
 
   template <class T>
   T* alloc(size_t n) {
@@ -157,10 +167,13 @@ struct Engine {
   }
   ~Engine() {
     if (stream) hipStreamSynchronize(stream);
-    for (auto& e : ev_pool) {
-      hipEventDestroy(e.first);
-      hipEventDestroy(e.second);
-    }
+    for (auto& g : step_graphs) hipGraphExecDestroy(g.second.exec);
+    for (auto& g : prof_graphs) hipGraphExecDestroy(g.second.exec);
+    for (auto* pool : {&ev_pool, &graph_events})
+      for (auto& e : *pool) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+      }
     for (void* p : allocs) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -499,6 +512,8 @@ struct Engine {
     n_part = cdiv(lc.n_vocab, 4 * rpw) * 4;
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
+    n_chunks_max = cdiv(lc.n_ctx, 64);
+    attn_part = alloc<float>((size_t)m_max * H * n_chunks_max * (D + 2));
     d_tok_seq = alloc<int>(m_max);
     d_tok_pos = alloc<int>(m_max);
     d_step = alloc<int>(m_max);
@@ -671,12 +686,14 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------------------------------------
-  // decoder forward over M token rows (embeddings already in lx). Logits for rows listed in
-  // `logit_rows` (indices into the M rows), one per sequence slot in the same order.
-  void llm_forward(int M, const std::vector<int>& logit_rows) {
+  // decoder forward over M token rows (embeddings already in lx, positions in d_tok_pos)
+  void llm_forward(int M, bool decode, int max_pos) {
+    // decode: every row is a different sequence (continuous batch), logits for all rows;
+    // prefill: rows are consecutive positions of one sequence, logits for the last row only.
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
     const bool small = M <= 4;
+    const int n_chunks = decode ? n_chunks_max : cdiv(max_pos + 1, 64);
     for (int l = 0; l < lc.n_layer; ++l) {
       const LlmLayerW& w = layers[l];
       __half* kc = kcache + (size_t)l * layer_stride;
@@ -690,12 +707,14 @@ struct Engine {
       if (small) { a.x = lx; a.ldx = E; a.norm_w = w.attn_norm; }
       else { prep_q8(lx, E, w.attn_norm, lc.rms_eps, M, E, lxq, lxd, stream); a.xq = lxq; a.xd = lxd; }
       gemv(a, E, 0);
-      qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
-                    seq_stride, stream);
       {
         hipEvent_t ev;
         prof_begin(3, &ev);
-        attn_decode(lq, kc, vc, latt, M, H, KV, d_tok_seq, d_tok_pos, seq_stride, stream);
+        if (!decode)
+          qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
+                        seq_stride, stream);
+        attn_split(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
+                   d_tok_seq, d_tok_pos, seq_stride, attn_part, n_chunks, latt, stream);
         prof_end(3, 0, 0);
       }
       // x += Wo . attn
@@ -720,15 +739,67 @@ struct Engine {
       else { prep_q8(lact, F, nullptr, 0.f, M, F, lxq, lxd, stream); dn.xq = lxq; dn.xd = lxd; }
       gemv(dn, F, 1);
     }
-    // lm_head (tied token_embd) on the requested rows, fused argmax partials
-    for (size_t i = 0; i < logit_rows.size(); ++i) {
-      GemvArgs h{};
-      h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
-      h.rpw = gemv_rows_per_wave(lc.n_vocab);
-      h.x = lx + (size_t)logit_rows[i] * E; h.ldx = E; h.norm_w = out_norm;
-      h.out = logits + (size_t)i * lc.n_vocab; h.ldo = lc.n_vocab;
-      h.pval = pval + (size_t)i * n_part; h.pidx = pidx + (size_t)i * n_part; h.n_part = n_part;
-      gemv(h, E, 3);
+    // lm_head (tied token_embd) with fused argmax partials: all rows (decode) or the last row (prefill)
+    const int n_rows = decode ? M : 1;
+    const float* xrow = decode ? lx : lx + (size_t)(M - 1) * E;
+    GemvArgs h{};
+    h.M = n_rows; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
+    h.rpw = gemv_rows_per_wave(lc.n_vocab);
+    h.out = logits; h.ldo = lc.n_vocab;
+    h.pval = pval; h.pidx = pidx; h.n_part = n_part;
+    if (n_rows <= 4) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
+    else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
+    gemv(h, E, 3);
+  }
+
+  // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
+  void decode_step(int n, const fa_sampling* s) {
+    embed_rows(tok_embd.q, tok_embd.d, d_tok_cur, n, lc.n_embd, 0, lx, stream);
+    llm_forward(n, true, 0);
+    sample(n, s, d_step, d_tok_cur, d_tok_hist);
+    advance_positions(d_tok_pos, d_step, n, stream);
+  }
+
+  // hipGraph of one decode step (all per-step state lives in device memory, grids are n_past-independent).
+  // The profiled variant also captures event-record nodes around each timed kernel class, so the event
+  // timestamps are taken by the GPU between back-to-back graph nodes (no host launch gaps inside).
+  StepGraph& step_graph(int n, const fa_sampling* s, bool profiled) {
+    auto& cache = profiled ? prof_graphs : step_graphs;
+    auto it = cache.find(n);
+    if (it != cache.end()) return it->second;
+    StepGraph sg;
+    const bool save_prof = prof;
+    const size_t ev0 = ev_next;
+    prof = profiled;
+    std::vector<Pending> saved;
+    saved.swap(pending);
+    hipGraph_t g;
+    FA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    decode_step(n, s);
+    FA_HIP(hipStreamEndCapture(stream, &g));
+    prof = save_prof;
+    if (profiled) {
+      // keep this graph's events out of the shared pool: they belong to the graph from now on
+      sg.events.swap(pending);
+      std::vector<std::pair<hipEvent_t, hipEvent_t>> mine(ev_pool.begin() + ev0, ev_pool.begin() + ev_next);
+      ev_pool.erase(ev_pool.begin() + ev0, ev_pool.begin() + ev_next);
+      graph_events.insert(graph_events.end(), mine.begin(), mine.end());
+      ev_next = ev0;
+    }
+    pending.swap(saved);
+    FA_HIP(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
+    FA_HIP(hipGraphDestroy(g));
+    return cache[n] = sg;
+  }
+
+  void collect_graph_events(const StepGraph& sg) {
+    for (const auto& p : sg.events) {
+      float ms = 0;
+      FA_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+      pcls[p.cls].ms += ms;
+      pcls[p.cls].bytes += p.bytes;
+      pcls[p.cls].flops += p.flops;
+      pcls[p.cls].launches++;
     }
   }
 
@@ -798,6 +869,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_REQUIRE(llm->n_embd % 1024 == 0 && llm->n_ff % 1024 == 0, "decoder widths must be multiples of 1024");
     FA_HIP(hipSetDevice(device));
     FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();
     e->build_encoder();
@@ -906,7 +978,23 @@ int fa_load_gguf(fa_engine* h, const char* path) {
 
 int fa_encode_device(fa_engine* h, const float* d_pcm, const int64_t* n_samples, int32_t batch, int64_t stride) {
   FA_API_BEGIN
-  h->e->encode_device(d_pcm, n_samples, batch, stride);
+  Engine* e = h->e;
+  if (!d_pcm) {
+    FA_REQUIRE((int64_t)batch * stride <= e->pcm_uploaded, "fa_encode_device(NULL): upload the PCM first");
+    d_pcm = e->d_pcm;
+  }
+  e->encode_device(d_pcm, n_samples, batch, stride);
+  FA_API_END
+}
+
+int fa_pcm_upload(fa_engine* h, const float* pcm, int64_t n_floats) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(pcm && n_floats >= 1 && n_floats <= (int64_t)e->max_batch * std::max<int64_t>(e->max_samples, 16000),
+             "fa_pcm_upload: size");
+  FA_HIP(hipMemcpyAsync(e->d_pcm, pcm, n_floats * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  e->pcm_uploaded = n_floats;
   FA_API_END
 }
 
@@ -948,6 +1036,7 @@ int fa_encode(fa_engine* h, const float* pcm, const int64_t* n_samples, int32_t 
   FA_REQUIRE(pcm && n_samples && batch >= 1 && batch <= e->max_batch && stride >= 1, "fa_encode args");
   FA_REQUIRE(stride <= std::max<int64_t>(e->max_samples, 16000), "stride > max_samples");
   FA_HIP(hipMemcpyAsync(e->d_pcm, pcm, (size_t)batch * stride * 4, hipMemcpyHostToDevice, e->stream));
+  e->pcm_uploaded = (int64_t)batch * stride;
   e->encode_device(e->d_pcm, n_samples, batch, stride);
   int r = fa_encode_fetch(h, audio_embd_out, tgt_stride, ctc_ids_out, ids_stride, t_lfr_out, target_len_out, enc_out);
   if (r != FA_OK) return r;
@@ -1027,7 +1116,7 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   for (int i = 0; i < n_tokens; ++i) ps[i] = e->n_past[seq] + i;
   FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
-  e->llm_forward(n_tokens, {n_tokens - 1});
+  e->llm_forward(n_tokens, false, e->n_past[seq] + n_tokens - 1);
   e->sample(1, s, nullptr, e->d_tok_cur, nullptr);
   int tok = 0;
   FA_HIP(hipMemcpyAsync(&tok, e->d_tok_cur, 4, hipMemcpyDeviceToHost, e->stream));
@@ -1046,7 +1135,7 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   FA_API_BEGIN
   Engine* e = h->e;
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs && n_steps >= 1 && n_steps <= e->hist_max, "generate args");
-  std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0), rows(n_seqs);
+  std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = seqs[i];
     FA_REQUIRE(q >= 0 && q < e->lc.max_seqs, "seq out of range");
@@ -1055,21 +1144,26 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
     sq[i] = q;
     ps[i] = e->n_past[q];
     cur[i] = e->last_tok[q];
-    rows[i] = i;
   }
   FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_cur, cur.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
-  for (int st = 0; st < n_steps; ++st) {
-    fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_tok_cur, n_seqs, e->lc.n_embd, 0, e->lx, e->stream);
-    e->llm_forward(n_seqs, rows);
-    e->sample(n_seqs, s, e->d_step, e->d_tok_cur, e->d_tok_hist);
-    fa::advance_positions(e->d_tok_pos, e->d_step, n_seqs, e->stream);
+  // sampling parameters are baked into a captured graph: graphs only for the greedy path.
+  // With profiling on, the last step of the call replays the profiled graph variant (sampled timing).
+  // (event nodes inside graphs do not time individual nodes on ROCm 7.2: profiling runs eager)
+  const bool graph = e->use_graphs && !e->prof && (!s || s->temperature <= 0.f);
+  const Engine::StepGraph* pg = nullptr;
+  if (graph) {
+    const Engine::StepGraph& sg = e->step_graph(n_seqs, s, false);
+    for (int st = 0; st < n_steps; ++st) FA_HIP(hipGraphLaunch(sg.exec, e->stream));
+  } else {
+    for (int st = 0; st < n_steps; ++st) e->decode_step(n_seqs, s);
   }
   std::vector<int> hist((size_t)n_seqs * e->hist_max);
   FA_HIP(hipMemcpyAsync(hist.data(), e->d_tok_hist, hist.size() * 4, hipMemcpyDeviceToHost, e->stream));
   FA_HIP(hipStreamSynchronize(e->stream));
+  if (pg) e->collect_graph_events(*pg);
   e->prof_collect();
   for (int i = 0; i < n_seqs; ++i) {
     for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hist[(size_t)i * e->hist_max + st];

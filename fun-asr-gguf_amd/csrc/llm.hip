@@ -105,6 +105,90 @@ __device__ __forceinline__ int dot16(const int4& a, const int4& b, int acc) {
   return acc;
 }
 
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+// streamed-once weights: non-temporal 16 B loads (MI355X_MICROARCH.md row nt-weights)
+__device__ __forceinline__ int4 ld_nt16(const int8_t* p) {
+  const i32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(p));
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+
+template <int NCH, int EPI>
+struct RowGroup {
+  int4 w[4][NCH];
+  int4 u[4][NCH];
+  float dw[4][NCH];
+  float du[4][NCH];
+};
+
+template <int NCH, int EPI>
+__device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int r0, int lane, RowGroup<NCH, EPI>& G) {
+  constexpr int K = NCH * 1024, NB = K / 32;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = row_base + r0 + rr;
+    const bool ok = (r0 + rr < a.rpw) && row < a.O;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (ok) {
+        G.w[rr][c] = ld_nt16(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
+        G.dw[rr][c] = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+        if (EPI == 2) {
+          G.u[rr][c] = ld_nt16(a.wq2 + (int64_t)row * K + c * 1024 + lane * 16);
+          G.du[rr][c] = __half2float(a.wd2[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+        }
+      } else {
+        G.w[rr][c] = make_int4(0, 0, 0, 0);
+        G.dw[rr][c] = 0.f;
+        if (EPI == 2) {
+          G.u[rr][c] = make_int4(0, 0, 0, 0);
+          G.du[rr][c] = 0.f;
+        }
+      }
+    }
+  }
+}
+
+template <int NCH, int MT, int EPI>
+__device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, int r0, int lane, int m0, int mt,
+                                              const int8_t* s_q, const float* s_d, const RowGroup<NCH, EPI>& G,
+                                              float (&best_v)[MT], int (&best_i)[MT]) {
+  constexpr int K = NCH * 1024, NB = K / 32;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m >= mt) break;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f}, acc2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int4 xv = *reinterpret_cast<const int4*>(s_q + m * K + c * 1024 + lane * 16);
+      const float xdv = s_d[m * NB + c * 32 + (lane >> 1)];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        int si = dot16(G.w[rr][c], xv, 0);
+        si += __shfl_xor(si, 1, 64);
+        if (!(lane & 1)) acc[rr] += (float)si * (G.dw[rr][c] * xdv);
+        if (EPI == 2) {
+          int su = dot16(G.u[rr][c], xv, 0);
+          su += __shfl_xor(su, 1, 64);
+          if (!(lane & 1)) acc2[rr] += (float)su * (G.du[rr][c] * xdv);
+        }
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = row_base + r0 + rr;
+      const float y = wave_sum(acc[rr]);
+      const float y2 = EPI == 2 ? wave_sum(acc2[rr]) : 0.f;
+      if (lane == 0 && (r0 + rr < a.rpw) && row < a.O) {
+        float* op = a.out + (int64_t)(m0 + m) * a.ldo + row;
+        if (EPI == 0 || EPI == 3) *op = y;
+        else if (EPI == 1) *op = a.res[(int64_t)(m0 + m) * a.ldr + row] + y;
+        else *op = (y / (1.0f + expf(-y))) * y2;
+        if (EPI == 3) argmax_combine(best_v[m], best_i[m], y, row);
+      }
+    }
+  }
+}
+
 template <int NCH, int MT, bool FUSED, int EPI>
 __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   constexpr int K = NCH * 1024, NB = K / 32;
@@ -113,6 +197,10 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int m0 = blockIdx.y * MT;
   const int mt = min(MT, a.M - m0);
+  const int row_base = (blockIdx.x * 4 + wave) * a.rpw;
+  // weights do not depend on the activations: issue the first row group before the prologue
+  RowGroup<NCH, EPI> G0, G1;
+  load_group<NCH, EPI>(a, row_base, 0, lane, G0);
   // ---- prologue: activation tile -> LDS (int8 q + f32 d)
   if (FUSED) {
     for (int m = wave; m < mt; m += 4)
@@ -124,72 +212,30 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
     for (int i = threadIdx.x; i < mt * NB; i += 256) s_d[i] = a.xd[(int64_t)m0 * NB + i];
   }
   __syncthreads();
-
-  const int row_base = (blockIdx.x * 4 + wave) * a.rpw;
-  float best_v = -INFINITY;
-  int best_i = 0x7fffffff;
-  for (int r0 = 0; r0 < a.rpw; r0 += 4) {
-    int4 wv[4][NCH], uv[4][NCH];
-    float dw[4][NCH], du[4][NCH];
+  float best_v[MT];
+  int best_i[MT];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = row_base + r0 + rr;
-      const bool ok = (r0 + rr < a.rpw) && row < a.O;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        if (ok) {
-          wv[rr][c] = *reinterpret_cast<const int4*>(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
-          dw[rr][c] = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
-          if (EPI == 2) {
-            uv[rr][c] = *reinterpret_cast<const int4*>(a.wq2 + (int64_t)row * K + c * 1024 + lane * 16);
-            du[rr][c] = __half2float(a.wd2[(int64_t)row * NB + c * 32 + (lane >> 1)]);
-          }
-        } else {
-          wv[rr][c] = make_int4(0, 0, 0, 0);
-          dw[rr][c] = 0.f;
-          if (EPI == 2) { uv[rr][c] = make_int4(0, 0, 0, 0); du[rr][c] = 0.f; }
-        }
-      }
-    }
+  for (int m = 0; m < MT; ++m) {
+    best_v[m] = -INFINITY;
+    best_i[m] = 0x7fffffff;
+  }
+  // two-deep register pipeline over 4-row groups (static buffer names, no runtime-indexed arrays)
+  for (int r0 = 0; r0 < a.rpw; r0 += 8) {
+    if (r0 + 4 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 4, lane, G1);
+    compute_group<NCH, MT, EPI>(a, row_base, r0, lane, m0, mt, s_q, s_d, G0, best_v, best_i);
+    if (r0 + 4 >= a.rpw) break;
+    if (r0 + 8 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 8, lane, G0);
+    compute_group<NCH, MT, EPI>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i);
+  }
+  if (EPI == 3 && lane == 0) {
+    const int part = blockIdx.x * 4 + wave;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      if (m >= mt) break;
-      float acc[4] = {0.f, 0.f, 0.f, 0.f}, acc2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int4 xv = *reinterpret_cast<const int4*>(s_q + m * K + c * 1024 + lane * 16);
-        const float xdv = s_d[m * NB + c * 32 + (lane >> 1)];
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          int si = dot16(wv[rr][c], xv, 0);
-          si += __shfl_xor(si, 1, 64);
-          if (!(lane & 1)) acc[rr] += (float)si * (dw[rr][c] * xdv);
-          if (EPI == 2) {
-            int su = dot16(uv[rr][c], xv, 0);
-            su += __shfl_xor(su, 1, 64);
-            if (!(lane & 1)) acc2[rr] += (float)su * (du[rr][c] * xdv);
-          }
-        }
-      }
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = row_base + r0 + rr;
-        float y = wave_sum(acc[rr]);
-        float y2 = EPI == 2 ? wave_sum(acc2[rr]) : 0.f;
-        if (lane == 0 && (r0 + rr < a.rpw) && row < a.O) {
-          float* op = a.out + (int64_t)(m0 + m) * a.ldo + row;
-          if (EPI == 0 || EPI == 3) *op = y;
-          else if (EPI == 1) *op = a.res[(int64_t)(m0 + m) * a.ldr + row] + y;
-          else *op = (y / (1.0f + expf(-y))) * y2;
-          if (EPI == 3 && MT == 1) argmax_combine(best_v, best_i, y, row);
-        }
+      if (m < mt) {
+        a.pval[(int64_t)(m0 + m) * a.n_part + part] = best_v[m];
+        a.pidx[(int64_t)(m0 + m) * a.n_part + part] = best_i[m];
       }
     }
-  }
-  if (EPI == 3 && MT == 1 && lane == 0) {
-    const int part = blockIdx.x * 4 + wave;
-    a.pval[(int64_t)m0 * a.n_part + part] = best_v;
-    a.pidx[(int64_t)m0 * a.n_part + part] = best_i;
   }
 }
 
@@ -234,7 +280,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     case 0: launch_gemv_k<8, false, 0>(K, a, s); break;
     case 1: launch_gemv_k<8, false, 1>(K, a, s); break;
     case 2: launch_gemv_k<8, false, 2>(K, a, s); break;
-    default: FA_REQUIRE(false, "gemv_q8: argmax epilogue needs M<=4");
+    case 3: launch_gemv_k<8, false, 3>(K, a, s); break;
   }
 }
 
@@ -387,6 +433,207 @@ void attn_decode(const float* q, const __half* kc, const __half* vc, float* out,
   const float scale = 1.0f / sqrtf(128.0f);
   hipLaunchKernelGGL(k_attn_decode, dim3(KV, M), dim3(256), 0, s, q, kc, vc, out, H, KV, tok_seq, tok_pos, seq_stride,
                      scale);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Split-K decode attention (flash-decoding): block = one wave = (64-key chunk, kv head g, token m).
+// DECODE mode (each token row is its own sequence): the block normalises + ropes the token's q heads
+// of group g itself (cheap, redundant per chunk) and the block whose chunk holds the token's position
+// also normalises/ropes k, and writes K/V of that position to the fp16 cache before reading the chunk.
+// PREFILL mode: q comes pre-roped from qk_rope_store, the cache is already complete.
+// Each block writes (m, l, o[128]) per q head of the group; k_attn_combine merges the chunks.
+constexpr int ACH = 64;  // keys per chunk
+__global__ __launch_bounds__(64) void k_attn_split(const float* __restrict__ qsrc, int decode_mode,
+                                                   const float* __restrict__ qn, const float* __restrict__ kn,
+                                                   float eps, const float* __restrict__ rcos,
+                                                   const float* __restrict__ rsin, __half* __restrict__ kc,
+                                                   __half* __restrict__ vc, int H, int KV,
+                                                   const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+                                                   int64_t seq_stride, float scale, float* __restrict__ part,
+                                                   int n_chunks) {
+  constexpr int D = 128;
+  const int chunk = blockIdx.x, g = blockIdx.y, m = blockIdx.z;
+  const int lane = threadIdx.x;
+  const int pos = tok_pos[m];
+  const int k0 = chunk * ACH;
+  if (k0 > pos) return;
+  const int n_keys = min(ACH, pos + 1 - k0);
+  // in decode mode the newest key (pos) is produced by this launch: its K/V come from registers/LDS
+  const int fresh = decode_mode ? pos - k0 : -1;  // index of the fresh key inside this chunk (or out of range)
+  __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
+  __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
+  __shared__ float s_q[GQ][D];
+  __shared__ float s_p[GQ][ACH];
+  __shared__ float s_kn[D], s_vn[D];
+  // ---- 1. issue every K and V load of the chunk up front (independent of q)
+  int4 kraw[D / 8];
+  const bool kok = lane < n_keys && lane != fresh;
+  {
+    const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)(k0 + lane) * KV * D);
+#pragma unroll
+    for (int c8 = 0; c8 < D / 8; ++c8) kraw[c8] = kok ? kp[c8] : make_int4(0, 0, 0, 0);
+  }
+  // V: lane = (kq = lane >> 4 : key phase 0..3, dq = lane & 15 : dims 8 dq .. 8 dq + 7); keys kq + 4 i
+  const int kq = lane >> 4, dq = lane & 15;
+  int4 vraw[ACH / 4];
+#pragma unroll
+  for (int i = 0; i < ACH / 4; ++i) {
+    const int k = kq + 4 * i;
+    vraw[i] = (k < n_keys && k != fresh)
+                  ? *reinterpret_cast<const int4*>(vb + (int64_t)(k0 + k) * KV * D + dq * 8)
+                  : make_int4(0, 0, 0, 0);
+  }
+  // ---- 2. q (and the fresh k/v): rms-norm per head, NEOX rope, scale
+  const float c = rcos[(int64_t)pos * 64 + lane], sn = rsin[(int64_t)pos * 64 + lane];
+  if (decode_mode) {
+    const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      const float* qp = row + (g * GQ + j) * D;
+      float x0 = qp[lane], x1 = qp[lane + 64];
+      const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + eps);
+      x0 = (x0 * sc) * qn[lane];
+      x1 = (x1 * sc) * qn[lane + 64];
+      s_q[j][lane] = (x0 * c - x1 * sn) * scale;
+      s_q[j][lane + 64] = (x0 * sn + x1 * c) * scale;
+    }
+    if (fresh >= 0 && fresh < ACH) {  // this chunk owns the new position: k norm/rope + KV store
+      const float* kp = row + (H + g) * D;
+      float x0 = kp[lane], x1 = kp[lane + 64];
+      const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + eps);
+      x0 = (x0 * sc) * kn[lane];
+      x1 = (x1 * sc) * kn[lane + 64];
+      const __half k0h = __float2half_rn(x0 * c - x1 * sn), k1h = __float2half_rn(x0 * sn + x1 * c);
+      const float* vp = row + (H + KV + g) * D;
+      const __half v0h = __float2half_rn(vp[lane]), v1h = __float2half_rn(vp[lane + 64]);
+      __half* kd = kb + (int64_t)pos * KV * D;
+      __half* vd = vb + (int64_t)pos * KV * D;
+      kd[lane] = k0h;
+      kd[lane + 64] = k1h;
+      vd[lane] = v0h;
+      vd[lane + 64] = v1h;
+      // the fresh row is consumed with the same fp16 rounding the cache holds
+      s_kn[lane] = __half2float(k0h);
+      s_kn[lane + 64] = __half2float(k1h);
+      s_vn[lane] = __half2float(v0h);
+      s_vn[lane + 64] = __half2float(v1h);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      const float* qp = qsrc + ((int64_t)m * H + g * GQ + j) * D;
+      s_q[j][lane] = qp[lane] * scale;
+      s_q[j][lane + 64] = qp[lane + 64] * scale;
+    }
+  }
+  __syncthreads();
+  // ---- 3. scores: lane = key
+  float sc[GQ];
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) sc[j] = 0.f;
+  if (lane == fresh) {
+#pragma unroll 8
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int j = 0; j < GQ; ++j) sc[j] += s_kn[d] * s_q[j][d];
+  } else {
+#pragma unroll
+    for (int c8 = 0; c8 < D / 8; ++c8) {
+      const __half2* hp = reinterpret_cast<const __half2*>(&kraw[c8]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float2 kf = __half22float2(hp[e]);
+#pragma unroll
+        for (int j = 0; j < GQ; ++j) sc[j] += kf.x * s_q[j][c8 * 8 + 2 * e] + kf.y * s_q[j][c8 * 8 + 2 * e + 1];
+      }
+    }
+  }
+  float mx[GQ], l[GQ];
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) {
+    if (lane >= n_keys) sc[j] = -INFINITY;
+    mx[j] = wave_max(sc[j]);
+    const float p = lane < n_keys ? __expf(sc[j] - mx[j]) : 0.f;
+    l[j] = wave_sum(p);
+    s_p[j][lane] = p;
+  }
+  __syncthreads();
+  // ---- 4. PV: 8 dims x 16 keys per lane, then reduce over the 4 key phases
+  float acc[GQ][8];
+#pragma unroll
+  for (int j = 0; j < GQ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < ACH / 4; ++i) {
+    const int k = kq + 4 * i;
+    float v[8];
+    if (k == fresh) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = s_vn[dq * 8 + e];
+    } else {
+      const __half2* hp = reinterpret_cast<const __half2*>(&vraw[i]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float2 f = __half22float2(hp[e]);
+        v[2 * e] = f.x;
+        v[2 * e + 1] = f.y;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      const float p = s_p[j][k];  // 0 beyond n_keys
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] += p * v[e];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < GQ; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc[j][e] += __shfl_xor(acc[j][e], 16, 64);
+      acc[j][e] += __shfl_xor(acc[j][e], 32, 64);
+    }
+  // partial record per (m, q head, chunk): [m, l, o[128]]
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) {
+    float* rec = part + (((int64_t)m * H + g * GQ + j) * n_chunks + chunk) * (D + 2);
+    if (lane == 0) {
+      rec[0] = mx[j];
+      rec[1] = l[j];
+    }
+    if (kq == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rec[2 + dq * 8 + e] = acc[j][e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(128) void k_attn_combine(const float* __restrict__ part, const int* __restrict__ tok_pos,
+                                                      int H, int n_chunks, float* __restrict__ out) {
+  constexpr int D = 128;
+  const int h = blockIdx.x, m = blockIdx.y, d = threadIdx.x;
+  const int nc = tok_pos[m] / ACH + 1;
+  const float* rec = part + ((int64_t)m * H + h) * n_chunks * (D + 2);
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, rec[c * (D + 2)]);
+  float L = 0.f, acc = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float w = __expf(rec[c * (D + 2)] - M);
+    L += w * rec[c * (D + 2) + 1];
+    acc += w * rec[c * (D + 2) + 2 + d];
+  }
+  out[((int64_t)m * H + h) * D + d] = acc / L;
+}
+
+void attn_split(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
+                const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
+                int64_t seq_stride, float* part, int n_chunks, float* out, hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ, "attn_split: n_head must be 2*n_head_kv");
+  const float scale = 1.0f / sqrtf(128.0f);
+  hipLaunchKernelGGL(k_attn_split, dim3(n_chunks, KV, M), dim3(64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos, rsin,
+                     kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, part, n_chunks);
+  hipLaunchKernelGGL(k_attn_combine, dim3(H, M), dim3(128), 0, s, part, tok_pos, H, n_chunks, out);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -16,7 +16,7 @@ EXPORTS = [
     "fa_set_tensor_f32", "fa_set_tensor_q8_0", "fa_load_gguf", "fa_get_tensor_q8_0", "fa_encode",
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
     "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
-    "fa_profile_read", "fa_synchronize", "fa_align_timestamps",
+    "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload",
 ]
 
 
@@ -79,6 +79,7 @@ def load():
     lib.fa_profile_read.argtypes = [P, I32, P, P, P, P]
     lib.fa_synchronize.argtypes = [P]
     lib.fa_align_timestamps.argtypes = [P, P, I32, P, I32, P, P]
+    lib.fa_pcm_upload.argtypes = [P, P, I64]
     _lib = lib
     return lib
 
@@ -157,28 +158,49 @@ class Engine:
         ctc_len = ((max(n, 16000) // 160 + 1) + 5) // 6
         return t_lfr, tgt, ctc_len
 
-    def encode(self, clips, want_enc=False, debug_lfr=False):
-        """clips: list of 1-D float32 arrays. Returns dict(audio_embd=[...], ctc_ids=[...], enc=[...])."""
+    @staticmethod
+    def _pack(clips):
         B = len(clips)
-        assert 1 <= B <= self.max_batch
         stride = max(max(len(c) for c in clips), 1)
         pcm = np.zeros((B, stride), np.float32)
         for i, c in enumerate(clips):
             pcm[i, :len(c)] = c
-        ns = np.array([len(c) for c in clips], np.int64)
+        return pcm, np.array([len(c) for c in clips], np.int64)
+
+    def upload(self, clips):
+        """Make clips resident in the engine's HBM PCM buffer; -> handle for encode(resident=handle)."""
+        pcm, ns = self._pack(clips)
+        _check(self.lib.fa_pcm_upload(self.h, _ptr(pcm), pcm.size), "fa_pcm_upload")
+        return dict(ns=ns, stride=pcm.shape[1])
+
+    def encode(self, clips, want_enc=False, debug_lfr=False, resident=None):
+        """clips: list of 1-D float32 arrays (or resident=upload() handle, clips = their lengths only).
+        Returns dict(audio_embd=[...], ctc_ids=[...], t_lfr, target_len[, enc, lfr_embedded])."""
+        if resident is not None:
+            ns, stride, pcm = resident["ns"], resident["stride"], None
+        else:
+            pcm, ns = self._pack(clips)
+            stride = pcm.shape[1]
+        B = len(ns)
+        assert 1 <= B <= self.max_batch
         counts = [self.frame_counts(int(n)) for n in ns]
         tgt_stride = max(c[1] for c in counts)
         ids_stride = max(c[2] for c in counts)
         d_llm, d = self.enc_cfg["d_llm"], self.enc_cfg["d_model"]
-        emb = np.zeros((B, tgt_stride, d_llm), np.float32)
-        ids = np.zeros((B, ids_stride), np.int32)
+        emb = np.empty((B, tgt_stride, d_llm), np.float32)
+        ids = np.empty((B, ids_stride), np.int32)
         tl = np.zeros(B, np.int32)
         tg = np.zeros(B, np.int32)
         enc = np.zeros((B, ids_stride, d), np.float32) if want_enc else None
         if debug_lfr:
             _check(self.lib.fa_set_debug(self.h, 1), "fa_set_debug")
-        _check(self.lib.fa_encode(self.h, _ptr(pcm), _ptr(ns), B, stride, _ptr(emb), tgt_stride, _ptr(ids), ids_stride,
-                                  _ptr(tl), _ptr(tg), _ptr(enc)), "fa_encode")
+        if pcm is None:
+            _check(self.lib.fa_encode_device(self.h, None, _ptr(ns), B, stride), "fa_encode_device")
+            _check(self.lib.fa_encode_fetch(self.h, _ptr(emb), tgt_stride, _ptr(ids), ids_stride, _ptr(tl), _ptr(tg),
+                                            _ptr(enc)), "fa_encode_fetch")
+        else:
+            _check(self.lib.fa_encode(self.h, _ptr(pcm), _ptr(ns), B, stride, _ptr(emb), tgt_stride, _ptr(ids),
+                                      ids_stride, _ptr(tl), _ptr(tg), _ptr(enc)), "fa_encode")
         out = dict(audio_embd=[emb[b, :tg[b]] for b in range(B)], ctc_ids=[ids[b, :tl[b]] for b in range(B)],
                    t_lfr=tl, target_len=tg)
         if want_enc:

@@ -89,7 +89,7 @@ class ASREngineConfig:
     n_ctx: int = 2048
     model: str = "full"            # "full" (Fun-ASR-Nano dims) or "tiny" (test dims)
     synthetic_seed: int = 0
-    ignore_eos: bool = False       # benchmark protocol: pin the decode length
+    ignore_eos: bool = False       # benchmark protocol: pin the decode length (no stop tokens, no breaker)
 
 
 @dataclass

@@ -28,9 +28,12 @@ class PromptBuilder:
     def __init__(self, vocab, engine):
         self.vocab = vocab
         self.engine = engine
+        self.fixed_ids = None  # benchmark protocol: (prefix_ids, suffix_ids) pinned when no tokenizer exists
 
     def build_ids(self, hotwords=None, language=None, context=None):
         p, s = prompt_texts(hotwords, language, context)
+        if self.fixed_ids is not None:
+            return list(self.fixed_ids[0]), list(self.fixed_ids[1]), p
         return self.vocab.tokenize(p), self.vocab.tokenize(s), p
 
     def build_prompt(self, hotwords=None, language=None, context=None):

@@ -85,9 +85,12 @@ int fa_get_tensor_q8_0(fa_engine* e, const char* name, uint8_t* out, int64_t n_b
 int fa_encode(fa_engine* e, const float* pcm, const int64_t* n_samples, int32_t batch, int64_t stride,
               float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out, int64_t ids_stride,
               int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out);
-/* Same, but pcm is a DEVICE pointer (inputs already resident in HBM) and the ids/lengths are left on
+/* Same, but pcm is a DEVICE pointer (NULL = the engine's buffer filled by fa_pcm_upload) (inputs already resident in HBM) and the ids/lengths are left on
  * device; fa_encode_fetch copies them out. Used by the benchmark and the batch scheduler. */
 int fa_encode_device(fa_engine* e, const float* d_pcm, const int64_t* n_samples, int32_t batch, int64_t stride);
+/* Upload PCM into the engine's own HBM buffer (same layout as fa_encode); a following
+ * fa_encode_device(e, NULL, ...) encodes from it. Lets callers keep inputs resident across calls. */
+int fa_pcm_upload(fa_engine* e, const float* pcm, int64_t n_floats);
 int fa_encode_fetch(fa_engine* e, float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out,
                     int64_t ids_stride, int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out);
 /* Greedy CTC collapse on device (nano_ctc.py:65-104): for clip b, compacted (id, first_frame) pairs
