@@ -64,6 +64,20 @@ def cpu_baseline(sample_clip_s=10.0, n_steps=4):
                       f"60 s clip = {t_clip:.1f} s"}
 
 
+def pmc_traffic():
+    """Per-launch HBM bytes of the decode GEMV class from the committed PMC pass (scripts/pmc_traffic.py,
+    rocprofv3 --pmc FETCH_SIZE with the gfx950 x2 correction), or None when no summary is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemv*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return round(d["decode_layer_gemv_mean"]["traffic_bytes"])
+    except Exception:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,7 +125,7 @@ def main():
 
     for _ in range(args.warmup):
         res = step()
-    assert res.n_gen == N_GEN, res.n_gen
+        assert res.n_gen == N_GEN, res.n_gen
     m.engine.synchronize()
     barrier()
     # ---- timed region (production path: hipGraph decode steps, no timing events)
@@ -158,7 +172,7 @@ def main():
         avg_s = p["ms"] / max(1, p["launches"]) / 1e3
         ach = p["bytes"] / max(1, p["launches"]) / avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic()}
     else:
         avg_s = p["ms"] / max(1, p["launches"]) / 1e3
         ach = p["flops"] / max(1, p["launches"]) / avg_s / 1e12

@@ -59,9 +59,9 @@ void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const floa
                    int64_t seq_stride, hipStream_t s);
 void attn_decode(const float* q, const __half* kc, const __half* vc, float* out, int M, int H, int KV,
                  const int* tok_seq, const int* tok_pos, int64_t seq_stride, hipStream_t s);
-void attn_split(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
+void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* part, int n_chunks, float* out, hipStream_t s);
+                int64_t seq_stride, float* out, hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,

@@ -70,6 +70,60 @@ __device__ __forceinline__ void norm_quant_row(const float* __restrict__ x, cons
   }
 }
 
+// Block-cooperative variant (256 threads, one row): thread t owns K/256 consecutive values; a 32-value
+// quant block spans 32/(K/256) threads. Same arithmetic as norm_quant_row, the sum of squares is reduced
+// over the whole block. Used by the decode GEMV prologue (M == 1) so all 4 waves share the row.
+template <int NCH>
+__device__ __forceinline__ void norm_quant_row_block(const float* __restrict__ x, const float* __restrict__ w,
+                                                     float eps, int8_t* __restrict__ q_out, float* __restrict__ d_out,
+                                                     float* __restrict__ s_red) {
+  constexpr int PER = NCH * 4;          // values per thread (K = NCH * 1024)
+  constexpr int TPB = 32 / PER;         // threads per quant block (8, 4 or 2 for NCH 1, 2, 3 -> NCH 3 uses 12/32)
+  const int t = threadIdx.x;
+  float v[PER];
+  if (NCH == 3) {
+    // K = 3072: 12 values per thread do not tile 32-blocks evenly; use 256 threads x 12 = 3072 with
+    // blocks of 32 spanning 8/3 threads -> fall back to per-wave chunks (3 waves x 1024)
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < PER; j += 4) {
+    const float4 f = *reinterpret_cast<const float4*>(x + t * PER + j);
+    v[j] = f.x; v[j + 1] = f.y; v[j + 2] = f.z; v[j + 3] = f.w;
+  }
+  if (w) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) ss += v[j] * v[j];
+    ss = wave_sum(ss);
+    if ((t & 63) == 0) s_red[t >> 6] = ss;
+    __syncthreads();
+    ss = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const float scale = 1.0f / sqrtf(ss / (float)(NCH * 1024) + eps);
+#pragma unroll
+    for (int j = 0; j < PER; j += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(w + t * PER + j);
+      v[j] = (v[j] * scale) * f.x;
+      v[j + 1] = (v[j + 1] * scale) * f.y;
+      v[j + 2] = (v[j + 2] * scale) * f.z;
+      v[j + 3] = (v[j + 3] * scale) * f.w;
+    }
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) a = fmaxf(a, fabsf(v[j]));
+#pragma unroll
+  for (int o = 1; o < TPB; o <<= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+  const float d = a / 127.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  int8_t qv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) qv[j] = (int8_t)roundf(__fmul_rn(v[j], id));
+  if (PER == 4) *reinterpret_cast<int32_t*>(q_out + t * PER) = *reinterpret_cast<int32_t*>(qv);
+  else *reinterpret_cast<int2*>(q_out + t * PER) = *reinterpret_cast<int2*>(qv);
+  if ((t % TPB) == 0) d_out[t / TPB] = __half2float(__float2half_rn(d));
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void k_prep_q8(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                  float eps, int M, int8_t* __restrict__ xq, float* __restrict__ xd) {
@@ -202,7 +256,14 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   RowGroup<NCH, EPI> G0, G1;
   load_group<NCH, EPI>(a, row_base, 0, lane, G0);
   // ---- prologue: activation tile -> LDS (int8 q + f32 d)
-  if (FUSED) {
+  if (FUSED && mt == 1 && NCH < 3) {
+    __shared__ float s_red[4];
+    norm_quant_row_block<NCH>(a.x + (int64_t)m0 * a.ldx, a.norm_w, a.eps, s_q, s_d, s_red);
+  } else if (FUSED && mt == 1 && !a.norm_w) {
+    // K = 3072 without norm (down proj): waves 0..2 quantise one 1024-chunk each
+    if (wave < NCH) norm_quant_row<1>(a.x + (int64_t)m0 * a.ldx + wave * 1024, nullptr, 0.f, lane, s_q + wave * 1024,
+                                      s_d + wave * 32);
+  } else if (FUSED) {
     for (int m = wave; m < mt; m += 4)
       norm_quant_row<NCH>(a.x + (int64_t)(m0 + m) * a.ldx, a.norm_w, a.eps, lane, s_q + m * K, s_d + m * NB);
   } else {
@@ -436,204 +497,237 @@ void attn_decode(const float* q, const __half* kc, const __half* vc, float* out,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Split-K decode attention (flash-decoding): block = one wave = (64-key chunk, kv head g, token m).
-// DECODE mode (each token row is its own sequence): the block normalises + ropes the token's q heads
-// of group g itself (cheap, redundant per chunk) and the block whose chunk holds the token's position
-// also normalises/ropes k, and writes K/V of that position to the fp16 cache before reading the chunk.
-// PREFILL mode: q comes pre-roped from qk_rope_store, the cache is already complete.
-// Each block writes (m, l, o[128]) per q head of the group; k_attn_combine merges the chunks.
-constexpr int ACH = 64;  // keys per chunk
-__global__ __launch_bounds__(64) void k_attn_split(const float* __restrict__ qsrc, int decode_mode,
-                                                   const float* __restrict__ qn, const float* __restrict__ kn,
-                                                   float eps, const float* __restrict__ rcos,
-                                                   const float* __restrict__ rsin, __half* __restrict__ kc,
-                                                   __half* __restrict__ vc, int H, int KV,
-                                                   const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
-                                                   int64_t seq_stride, float scale, float* __restrict__ part,
-                                                   int n_chunks) {
+// Decode/prefill attention over the fp16 KV cache. Block = (kv head g, token m), 8 waves; wave w takes the
+// 64-key chunks w, w+8, ... (lane = key for q.k, 16 lanes x 8 dims x 4 key phases for p.V) with its own
+// online softmax; the 8 partial states merge in LDS. Every K/V load of a chunk is issued before any math.
+// DECODE mode (each token row its own sequence): wave 0 rms-norms + ropes the group's 2 q heads; the wave
+// whose chunk holds the token's position also norms/ropes k, stores K/V of that position to the cache and
+// consumes the fresh row from LDS (with the cache's fp16 rounding). PREFILL mode: q comes pre-roped from
+// qk_rope_store and the cache is complete.
+constexpr int ACH = 64;   // keys per chunk
+constexpr int AWV = 8;    // waves per block
+__device__ __forceinline__ void load_k_chunk(const __half* __restrict__ kb, int KV, int k0, int n_keys, int fresh,
+                                             int lane, int4 (&kraw)[16]) {
   constexpr int D = 128;
-  const int chunk = blockIdx.x, g = blockIdx.y, m = blockIdx.z;
-  const int lane = threadIdx.x;
+  const bool kok = lane < n_keys && lane != fresh;
+  const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)(k0 + lane) * KV * D);
+#pragma unroll
+  for (int c8 = 0; c8 < 16; ++c8) kraw[c8] = kok ? kp[c8] : make_int4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void load_v_chunk(const __half* __restrict__ vb, int KV, int k0, int n_keys, int fresh,
+                                             int kq, int dq, int4 (&vraw)[16]) {
+  constexpr int D = 128;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = kq + 4 * i;
+    vraw[i] = (k < n_keys && k != fresh) ? *reinterpret_cast<const int4*>(vb + (int64_t)(k0 + k) * KV * D + dq * 8)
+                                         : make_int4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void rope_norm_head(const float* __restrict__ src, const float* __restrict__ nw, float eps,
+                                               float c, float sn, int lane, float& y0, float& y1) {
+  float x0 = src[lane], x1 = src[lane + 64];
+  const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / 128.0f + eps);
+  x0 = (x0 * sc) * nw[lane];
+  x1 = (x1 * sc) * nw[lane + 64];
+  y0 = x0 * c - x1 * sn;
+  y1 = x0 * sn + x1 * c;
+}
+
+__global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict__ qsrc, int decode_mode,
+                                                         const float* __restrict__ qn, const float* __restrict__ kn,
+                                                         float eps, const float* __restrict__ rcos,
+                                                         const float* __restrict__ rsin, __half* __restrict__ kc,
+                                                         __half* __restrict__ vc, int H, int KV,
+                                                         const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+                                                         int64_t seq_stride, float scale, float* __restrict__ out) {
+  constexpr int D = 128;
+  const int g = blockIdx.x, m = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pos = tok_pos[m];
-  const int k0 = chunk * ACH;
-  if (k0 > pos) return;
-  const int n_keys = min(ACH, pos + 1 - k0);
-  // in decode mode the newest key (pos) is produced by this launch: its K/V come from registers/LDS
-  const int fresh = decode_mode ? pos - k0 : -1;  // index of the fresh key inside this chunk (or out of range)
+  const int n_keys_all = pos + 1;
+  const int n_chunks = (n_keys_all + ACH - 1) / ACH;
   __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
   __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
-  __shared__ float s_q[GQ][D];
-  __shared__ float s_p[GQ][ACH];
-  __shared__ float s_kn[D], s_vn[D];
-  // ---- 1. issue every K and V load of the chunk up front (independent of q)
-  int4 kraw[D / 8];
-  const bool kok = lane < n_keys && lane != fresh;
-  {
-    const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)(k0 + lane) * KV * D);
-#pragma unroll
-    for (int c8 = 0; c8 < D / 8; ++c8) kraw[c8] = kok ? kp[c8] : make_int4(0, 0, 0, 0);
-  }
-  // V: lane = (kq = lane >> 4 : key phase 0..3, dq = lane & 15 : dims 8 dq .. 8 dq + 7); keys kq + 4 i
+  __shared__ float4 s_q4[AWV][GQ][D / 4];   // per-wave copy of the scaled, roped q heads
+  __shared__ float s_kn[D], s_vn[D];         // fresh K/V row (decode)
+  __shared__ float s_p[AWV][GQ][ACH];
+  __shared__ float s_ml[AWV][GQ][2];
+  __shared__ float s_o[AWV][GQ][D];
   const int kq = lane >> 4, dq = lane & 15;
-  int4 vraw[ACH / 4];
-#pragma unroll
-  for (int i = 0; i < ACH / 4; ++i) {
-    const int k = kq + 4 * i;
-    vraw[i] = (k < n_keys && k != fresh)
-                  ? *reinterpret_cast<const int4*>(vb + (int64_t)(k0 + k) * KV * D + dq * 8)
-                  : make_int4(0, 0, 0, 0);
-  }
-  // ---- 2. q (and the fresh k/v): rms-norm per head, NEOX rope, scale
-  const float c = rcos[(int64_t)pos * 64 + lane], sn = rsin[(int64_t)pos * 64 + lane];
-  if (decode_mode) {
-    const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
-#pragma unroll
-    for (int j = 0; j < GQ; ++j) {
-      const float* qp = row + (g * GQ + j) * D;
-      float x0 = qp[lane], x1 = qp[lane + 64];
-      const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + eps);
-      x0 = (x0 * sc) * qn[lane];
-      x1 = (x1 * sc) * qn[lane + 64];
-      s_q[j][lane] = (x0 * c - x1 * sn) * scale;
-      s_q[j][lane + 64] = (x0 * sn + x1 * c) * scale;
-    }
-    if (fresh >= 0 && fresh < ACH) {  // this chunk owns the new position: k norm/rope + KV store
-      const float* kp = row + (H + g) * D;
-      float x0 = kp[lane], x1 = kp[lane + 64];
-      const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / (float)D + eps);
-      x0 = (x0 * sc) * kn[lane];
-      x1 = (x1 * sc) * kn[lane + 64];
-      const __half k0h = __float2half_rn(x0 * c - x1 * sn), k1h = __float2half_rn(x0 * sn + x1 * c);
-      const float* vp = row + (H + KV + g) * D;
-      const __half v0h = __float2half_rn(vp[lane]), v1h = __float2half_rn(vp[lane + 64]);
-      __half* kd = kb + (int64_t)pos * KV * D;
-      __half* vd = vb + (int64_t)pos * KV * D;
-      kd[lane] = k0h;
-      kd[lane + 64] = k1h;
-      vd[lane] = v0h;
-      vd[lane + 64] = v1h;
-      // the fresh row is consumed with the same fp16 rounding the cache holds
-      s_kn[lane] = __half2float(k0h);
-      s_kn[lane + 64] = __half2float(k1h);
-      s_vn[lane] = __half2float(v0h);
-      s_vn[lane + 64] = __half2float(v1h);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < GQ; ++j) {
-      const float* qp = qsrc + ((int64_t)m * H + g * GQ + j) * D;
-      s_q[j][lane] = qp[lane] * scale;
-      s_q[j][lane + 64] = qp[lane + 64] * scale;
-    }
-  }
-  __syncthreads();
-  // ---- 3. scores: lane = key
-  float sc[GQ];
-#pragma unroll
-  for (int j = 0; j < GQ; ++j) sc[j] = 0.f;
-  if (lane == fresh) {
-#pragma unroll 8
-    for (int d = 0; d < D; ++d)
-#pragma unroll
-      for (int j = 0; j < GQ; ++j) sc[j] += s_kn[d] * s_q[j][d];
-  } else {
-#pragma unroll
-    for (int c8 = 0; c8 < D / 8; ++c8) {
-      const __half2* hp = reinterpret_cast<const __half2*>(&kraw[c8]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float2 kf = __half22float2(hp[e]);
-#pragma unroll
-        for (int j = 0; j < GQ; ++j) sc[j] += kf.x * s_q[j][c8 * 8 + 2 * e] + kf.y * s_q[j][c8 * 8 + 2 * e + 1];
-      }
-    }
-  }
-  float mx[GQ], l[GQ];
+  float mx[GQ], l[GQ], acc[GQ][8];
 #pragma unroll
   for (int j = 0; j < GQ; ++j) {
-    if (lane >= n_keys) sc[j] = -INFINITY;
-    mx[j] = wave_max(sc[j]);
-    const float p = lane < n_keys ? __expf(sc[j] - mx[j]) : 0.f;
-    l[j] = wave_sum(p);
-    s_p[j][lane] = p;
-  }
-  __syncthreads();
-  // ---- 4. PV: 8 dims x 16 keys per lane, then reduce over the 4 key phases
-  float acc[GQ][8];
-#pragma unroll
-  for (int j = 0; j < GQ; ++j)
+    mx[j] = -INFINITY;
+    l[j] = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
+  }
+  if (wave < n_chunks) {
+    const int fresh_chunk = decode_mode ? pos / ACH : -1;
+    // (1) issue the first chunk's K/V loads before any dependent work
+    int ch = wave;
+    int k0 = ch * ACH;
+    int n_keys = min(ACH, n_keys_all - k0);
+    int fresh = ch == fresh_chunk ? pos - k0 : -1;
+    int4 kraw[D / 8], vraw[ACH / 4];
+    load_k_chunk(kb, KV, k0, n_keys, fresh, lane, kraw);
+    // (2) this wave's own q (no block barrier); the fresh chunk's wave also produces K/V[pos]
+    {
+      float* sq = reinterpret_cast<float*>(s_q4[wave]);
+      if (decode_mode) {
+        const float c = rcos[(int64_t)pos * 64 + lane], sn = rsin[(int64_t)pos * 64 + lane];
+        const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
-  for (int i = 0; i < ACH / 4; ++i) {
-    const int k = kq + 4 * i;
-    float v[8];
-    if (k == fresh) {
+        for (int j = 0; j < GQ; ++j) {
+          float y0, y1;
+          rope_norm_head(row + (g * GQ + j) * D, qn, eps, c, sn, lane, y0, y1);
+          sq[j * D + lane] = y0 * scale;
+          sq[j * D + lane + 64] = y1 * scale;
+        }
+        if (fresh_chunk == wave) {
+          float y0, y1;
+          rope_norm_head(row + (H + g) * D, kn, eps, c, sn, lane, y0, y1);
+          const __half k0h = __float2half_rn(y0), k1h = __float2half_rn(y1);
+          const float* vp = row + (H + KV + g) * D;
+          const __half v0h = __float2half_rn(vp[lane]), v1h = __float2half_rn(vp[lane + 64]);
+          __half* kd = kb + (int64_t)pos * KV * D;
+          __half* vd = vb + (int64_t)pos * KV * D;
+          kd[lane] = k0h;
+          kd[lane + 64] = k1h;
+          vd[lane] = v0h;
+          vd[lane + 64] = v1h;
+          s_kn[lane] = __half2float(k0h);
+          s_kn[lane + 64] = __half2float(k1h);
+          s_vn[lane] = __half2float(v0h);
+          s_vn[lane + 64] = __half2float(v1h);
+        }
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = s_vn[dq * 8 + e];
-    } else {
-      const __half2* hp = reinterpret_cast<const __half2*>(&vraw[i]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float2 f = __half22float2(hp[e]);
-        v[2 * e] = f.x;
-        v[2 * e + 1] = f.y;
+        for (int j = 0; j < GQ; ++j) {
+          const float* qp = qsrc + ((int64_t)m * H + g * GQ + j) * D;
+          sq[j * D + lane] = qp[lane] * scale;
+          sq[j * D + lane + 64] = qp[lane + 64] * scale;
+        }
       }
+      __builtin_amdgcn_wave_barrier();
     }
+    for (;;) {
+      // (3) scores: lane = key
+      float sc[GQ] = {};
+      if (lane == fresh) {
+#pragma unroll 8
+        for (int d4 = 0; d4 < D / 4; ++d4)
 #pragma unroll
-    for (int j = 0; j < GQ; ++j) {
-      const float p = s_p[j][k];  // 0 beyond n_keys
+          for (int j = 0; j < GQ; ++j) {
+            const float4 q4 = s_q4[wave][j][d4];
+            sc[j] += s_kn[4 * d4] * q4.x + s_kn[4 * d4 + 1] * q4.y + s_kn[4 * d4 + 2] * q4.z + s_kn[4 * d4 + 3] * q4.w;
+          }
+      } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[j][e] += p * v[e];
+        for (int c8 = 0; c8 < D / 8; ++c8) {
+          const __half2* hp = reinterpret_cast<const __half2*>(&kraw[c8]);
+          const float2 k0f = __half22float2(hp[0]), k1f = __half22float2(hp[1]);
+          const float2 k2f = __half22float2(hp[2]), k3f = __half22float2(hp[3]);
+#pragma unroll
+          for (int j = 0; j < GQ; ++j) {
+            const float4 qa = s_q4[wave][j][2 * c8], qb = s_q4[wave][j][2 * c8 + 1];
+            sc[j] += k0f.x * qa.x + k0f.y * qa.y + k1f.x * qa.z + k1f.y * qa.w + k2f.x * qb.x + k2f.y * qb.y +
+                     k3f.x * qb.z + k3f.y * qb.w;
+          }
+        }
+      }
+      load_v_chunk(vb, KV, k0, n_keys, fresh, kq, dq, vraw);  // V latency overlaps the softmax reductions
+#pragma unroll
+      for (int j = 0; j < GQ; ++j) {
+        if (lane >= n_keys) sc[j] = -INFINITY;
+        const float mn = fmaxf(mx[j], wave_max(sc[j]));
+        const float alpha = mx[j] == -INFINITY ? 0.f : __expf(mx[j] - mn);
+        const float p = lane < n_keys ? __expf(sc[j] - mn) : 0.f;
+        l[j] = l[j] * alpha + wave_sum(p);
+        mx[j] = mn;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] *= alpha;
+        s_p[wave][j][lane] = p;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // (4) p.V: 8 dims x 16 keys per lane (4 key phases reduced at the end)
+#pragma unroll
+      for (int i = 0; i < ACH / 4; ++i) {
+        const int k = kq + 4 * i;
+        float v[8];
+        if (k == fresh) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = s_vn[dq * 8 + e];
+        } else {
+          const __half2* hp = reinterpret_cast<const __half2*>(&vraw[i]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float2 f = __half22float2(hp[e]);
+            v[2 * e] = f.x;
+            v[2 * e + 1] = f.y;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < GQ; ++j) {
+          const float p = s_p[wave][j][k];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[j][e] += p * v[e];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      ch += AWV;
+      if (ch >= n_chunks) break;
+      k0 = ch * ACH;
+      n_keys = min(ACH, n_keys_all - k0);
+      fresh = ch == fresh_chunk ? pos - k0 : -1;
+      load_k_chunk(kb, KV, k0, n_keys, fresh, lane, kraw);
     }
   }
+  // reduce the 4 key phases, publish per-wave (m, l, o), merge the waves
 #pragma unroll
-  for (int j = 0; j < GQ; ++j)
+  for (int j = 0; j < GQ; ++j) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       acc[j][e] += __shfl_xor(acc[j][e], 16, 64);
       acc[j][e] += __shfl_xor(acc[j][e], 32, 64);
     }
-  // partial record per (m, q head, chunk): [m, l, o[128]]
-#pragma unroll
-  for (int j = 0; j < GQ; ++j) {
-    float* rec = part + (((int64_t)m * H + g * GQ + j) * n_chunks + chunk) * (D + 2);
     if (lane == 0) {
-      rec[0] = mx[j];
-      rec[1] = l[j];
+      s_ml[wave][j][0] = mx[j];
+      s_ml[wave][j][1] = l[j];
     }
     if (kq == 0) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) rec[2 + dq * 8 + e] = acc[j][e];
+      for (int e = 0; e < 8; ++e) s_o[wave][j][dq * 8 + e] = acc[j][e];
     }
   }
-}
-
-__global__ __launch_bounds__(128) void k_attn_combine(const float* __restrict__ part, const int* __restrict__ tok_pos,
-                                                      int H, int n_chunks, float* __restrict__ out) {
-  constexpr int D = 128;
-  const int h = blockIdx.x, m = blockIdx.y, d = threadIdx.x;
-  const int nc = tok_pos[m] / ACH + 1;
-  const float* rec = part + ((int64_t)m * H + h) * n_chunks * (D + 2);
-  float M = -INFINITY;
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, rec[c * (D + 2)]);
-  float L = 0.f, acc = 0.f;
-  for (int c = 0; c < nc; ++c) {
-    const float w = __expf(rec[c * (D + 2)] - M);
-    L += w * rec[c * (D + 2) + 1];
-    acc += w * rec[c * (D + 2) + 2 + d];
+  __syncthreads();
+  if (threadIdx.x < GQ * D) {
+    const int j = threadIdx.x / D, d = threadIdx.x % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_ml[w][j][0]);
+    float L = 0.f, o = 0.f;
+#pragma unroll
+    for (int w = 0; w < AWV; ++w) {
+      const float mw = s_ml[w][j][0];
+      const float wt = mw == -INFINITY ? 0.f : __expf(mw - M);
+      L += wt * s_ml[w][j][1];
+      o += wt * s_o[w][j][d];
+    }
+    out[((int64_t)m * H + g * GQ + j) * D + d] = o / L;
   }
-  out[((int64_t)m * H + h) * D + d] = acc / L;
 }
 
-void attn_split(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
+void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* part, int n_chunks, float* out, hipStream_t s) {
-  FA_REQUIRE(H == KV * GQ, "attn_split: n_head must be 2*n_head_kv");
+                int64_t seq_stride, float* out, hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   const float scale = 1.0f / sqrtf(128.0f);
-  hipLaunchKernelGGL(k_attn_split, dim3(n_chunks, KV, M), dim3(64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos, rsin,
-                     kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, part, n_chunks);
-  hipLaunchKernelGGL(k_attn_combine, dim3(H, M), dim3(128), 0, s, part, tok_pos, H, n_chunks, out);
+  hipLaunchKernelGGL(k_attn_block, dim3(KV, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos, rsin, kc,
+                     vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,0 +1,79 @@
+// Production replica of one batch-1 decode step (Qwen3-0.6B q8_0): 28 layers with DISTINCT weights
+// (465 MB > 256 MB Infinity Cache, so weights stream from HBM like in the engine), n_past = 330.
+// mode "graph": per-step time of the hipGraph'd step; mode "eager N": N eager steps (for rocprofv3 PMC).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../fun-asr-gguf_amd/csrc/kernels.h"
+namespace fa {
+void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
+void log(int, const std::string&) {}
+}
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using namespace fa;
+template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T))); return (T*)p; }
+int main(int argc, char** argv) {
+  hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048, L = 28;
+  float* tmp = dalloc<float>((size_t)V * E);
+  auto q8 = [&](int64_t rows, int64_t cols, uint32_t key, int8_t** q, __half** d) {
+    launch_synth_fill(tmp, rows * cols, key, 0.05f, 0.f, s);
+    *q = dalloc<int8_t>(rows * cols); *d = dalloc<__half>(rows * cols / 32);
+    launch_quant_q8_0(tmp, rows * cols, *q, *d, s);
+  };
+  struct LW { int8_t *qkv, *o, *g, *u, *d; __half *dqkv, *dO, *dg, *du, *dd; };
+  std::vector<LW> lw(L);
+  for (int l = 0; l < L; ++l) {
+    q8(QKV, E, 100 + l, &lw[l].qkv, &lw[l].dqkv); q8(E, H * D, 200 + l, &lw[l].o, &lw[l].dO);
+    q8(F, E, 300 + l, &lw[l].g, &lw[l].dg); q8(F, E, 400 + l, &lw[l].u, &lw[l].du); q8(E, F, 500 + l, &lw[l].d, &lw[l].dd);
+  }
+  int8_t* wemb; __half* demb; q8(V, E, 6, &wemb, &demb);
+  CK(hipStreamSynchronize(s)); CK(hipFree(tmp));
+  float* x = dalloc<float>(E); launch_synth_fill(x, E, 7, 1.f, 0.f, s);
+  float* nw = dalloc<float>(E); launch_synth_fill(nw, E, 8, 0.1f, 1.f, s);
+  float* qkv = dalloc<float>(QKV); float* att = dalloc<float>(H * D); float* act = dalloc<float>(F);
+  float* logits = dalloc<float>(V); float* pval = dalloc<float>(8192); int* pidx = dalloc<int>(8192);
+  __half* kc = dalloc<__half>((size_t)L * NCTX * KV * D); __half* vc = dalloc<__half>((size_t)L * NCTX * KV * D);
+  CK(hipMemset(kc, 0, (size_t)L * NCTX * KV * D * 2)); CK(hipMemset(vc, 0, (size_t)L * NCTX * KV * D * 2));
+  float* rc = dalloc<float>(NCTX * 64); float* rs = dalloc<float>(NCTX * 64);
+  launch_synth_fill(rc, NCTX * 64, 12, 1.f, 0.f, s); launch_synth_fill(rs, NCTX * 64, 13, 1.f, 0.f, s);
+  float* qn = dalloc<float>(D); launch_synth_fill(qn, D, 14, 0.1f, 1.f, s);
+  int* seq = dalloc<int>(1); int* pos = dalloc<int>(1); CK(hipMemset(seq, 0, 4));
+  int p0 = 330; CK(hipMemcpy(pos, &p0, 4, hipMemcpyHostToDevice));
+  CK(hipStreamSynchronize(s));
+  auto G = [&](const int8_t* q, const __half* d, int O, const float* xin, int ldx, const float* nrm, float* o, const float* res) {
+    GemvArgs a{}; a.M = 1; a.eps = 1e-6f; a.wq = q; a.wd = d; a.O = O; a.rpw = gemv_rows_per_wave(O);
+    a.x = xin; a.ldx = ldx; a.norm_w = nrm; a.out = o; a.ldo = O; a.res = res; a.ldr = O; return a; };
+  auto step = [&]() {
+    for (int l = 0; l < L; ++l) {
+      auto& w = lw[l];
+      gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
+      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV,
+                 seq, pos, (int64_t)NCTX * KV * D, att, s);
+      gemv_q8(G(w.o, w.dO, E, att, H * D, nullptr, x, x), H * D, 1, s);
+      auto gu = G(w.g, w.dg, F, x, E, nw, act, nullptr); gu.wq2 = w.u; gu.wd2 = w.du; gemv_q8(gu, E, 2, s);
+      gemv_q8(G(w.d, w.dd, E, act, F, nullptr, x, x), F, 1, s);
+    }
+    auto h = G(wemb, demb, V, x, E, nw, logits, nullptr); h.pval = pval; h.pidx = pidx;
+    h.n_part = (V + 4 * h.rpw - 1) / (4 * h.rpw) * 4; gemv_q8(h, E, 3, s);
+  };
+  const bool eager = argc > 1 && !strcmp(argv[1], "eager");
+  const int n = argc > 2 ? atoi(argv[2]) : 3;
+  if (eager) { for (int i = 0; i < n; ++i) step(); CK(hipStreamSynchronize(s)); printf("eager %d steps done\n", n); return 0; }
+  hipGraph_t g; hipGraphExec_t ex;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)); step(); CK(hipStreamEndCapture(s, &g));
+  CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  for (int i = 0; i < 5; ++i) CK(hipGraphLaunch(ex, s));
+  CK(hipStreamSynchronize(s));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  const int R = 50;
+  CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
+  const double bytes = (double)L * (QKV * E + E * H * D + 2.0 * F * E + E * F) * 34 / 32 + (double)V * E * 34 / 32;
+  printf("decode step (graph, 28 layers + lm_head, n_past 330): %.1f us  -> %.1f GB/s of q8_0 weights (%.1f MB)\n",
+         ms * 1e3 / R, bytes / (ms * 1e-3 / R) / 1e9, bytes / 1e6);
+  return 0;
+}
