@@ -33,20 +33,59 @@ struct arg_failure {};
 
 constexpr int WAVE = 64;
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+// Wave-wide reductions on DPP (row-local quad_perm / half-mirror / mirror) + 4 readlanes, instead of
+// __shfl_xor's ds_bpermute round trips through the LDS crossbar. Result is wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;
+
+__device__ __forceinline__ float row_sum16(float v) {  // sum over each 16-lane row, every lane of the row
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  v += dpp_f<DPP_MIRROR>(v);
   return v;
+}
+__device__ __forceinline__ float row_max16(float v) {
+  v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+  v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+  return v;
+}
+// max over aligned groups of N lanes (N = 2, 4, 8, 16), result in every lane of the group
+template <int N>
+__device__ __forceinline__ float group_max(float v) {
+  if (N >= 2) v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  if (N >= 4) v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+  if (N >= 8) v = fmaxf(v, dpp_f<DPP_HALF_MIRROR>(v));
+  if (N >= 16) v = fmaxf(v, dpp_f<DPP_MIRROR>(v));
+  return v;
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row_sum16(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = row_max16(v);
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 __device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_i<DPP_XOR1>(v);
+  v += dpp_i<DPP_XOR2>(v);
+  v += dpp_i<DPP_HALF_MIRROR>(v);
+  v += dpp_i<DPP_MIRROR>(v);
+  return (__builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16)) +
+         (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
 // (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).

@@ -134,6 +134,7 @@ struct Engine {
       *d_ids = nullptr;
   int hist_max = 0;
   std::vector<int> n_past, last_tok, logits_row;
+  AttnWork attn_wk;
 
   // profiling
   bool prof = false;
@@ -519,6 +520,11 @@ struct Engine {
     hist_max = 4096;
     d_tok_hist = alloc<int>((size_t)lc.max_seqs * hist_max);
     d_ids = alloc<int>(m_max);
+    attn_wk.max_tokens = m_max;
+    attn_wk.max_kv = KV;
+    attn_wk.counters = alloc<int>((size_t)m_max * KV);
+    FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * sizeof(int)));
+    attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
     n_past.assign(lc.max_seqs, 0);
     last_tok.assign(lc.max_seqs, -1);
   }
@@ -713,7 +719,7 @@ struct Engine {
           qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
                         seq_stride, stream);
         attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
-                   d_tok_seq, d_tok_pos, seq_stride, latt, stream);
+                   d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream);
         prof_end(3, 0, 0);
       }
       // x += Wo . attn

@@ -57,11 +57,18 @@ int gemv_rows_per_wave(int O);
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
                    int64_t seq_stride, hipStream_t s);
-void attn_decode(const float* q, const __half* kc, const __half* vc, float* out, int M, int H, int KV,
-                 const int* tok_seq, const int* tok_pos, int64_t seq_stride, hipStream_t s);
+// Split-key attention workspace: per (token, kv head) an arrival counter (zeroed once; the combining block
+// re-arms it) and ATTN_SPLITS partials of ATTN_PART_FLOATS floats (o[2][128], then m0, l0, m1, l1).
+#define ATTN_SPLITS 16
+#define ATTN_PART_FLOATS 260
+struct AttnWork {
+  int* counters = nullptr;    // [max_tokens][max_kv]
+  float* partials = nullptr;  // [max_tokens][max_kv][ATTN_SPLITS][ATTN_PART_FLOATS]
+  int max_tokens = 0, max_kv = 0;
+};
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* out, hipStream_t s);
+                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,

@@ -53,7 +53,7 @@ __device__ __forceinline__ void norm_quant_row(const float* __restrict__ x, cons
     float a = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) a = fmaxf(a, fabsf(v[c][j]));
-    a = fmaxf(a, __shfl_xor(a, 1, 64));
+    a = group_max<2>(a);
     const float d = a / 127.0f;
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
     int32_t packed[4];
@@ -112,8 +112,7 @@ __device__ __forceinline__ void norm_quant_row_block(const float* __restrict__ x
   float a = 0.f;
 #pragma unroll
   for (int j = 0; j < PER; ++j) a = fmaxf(a, fabsf(v[j]));
-#pragma unroll
-  for (int o = 1; o < TPB; o <<= 1) a = fmaxf(a, __shfl_xor(a, o, 64));
+  a = group_max<TPB>(a);
   const float d = a / 127.0f;
   const float id = d != 0.0f ? 1.0f / d : 0.0f;
   int8_t qv[PER];
@@ -177,26 +176,22 @@ struct RowGroup {
 template <int NCH, int EPI>
 __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int r0, int lane, RowGroup<NCH, EPI>& G) {
   constexpr int K = NCH * 1024, NB = K / 32;
+  // rows past the matrix/slice are loaded from a clamped valid row and their scales zeroed: no
+  // per-row branches around the loads (hipcc would wait vmcnt(0) at each, serialising the stream)
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
-    const int row = row_base + r0 + rr;
-    const bool ok = (r0 + rr < a.rpw) && row < a.O;
+    const int row0 = row_base + r0 + rr;
+    const bool ok = (r0 + rr < a.rpw) && row0 < a.O;
+    const int row = min(row0, a.O - 1);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      if (ok) {
-        G.w[rr][c] = ld_nt16(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
-        G.dw[rr][c] = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
-        if (EPI == 2) {
-          G.u[rr][c] = ld_nt16(a.wq2 + (int64_t)row * K + c * 1024 + lane * 16);
-          G.du[rr][c] = __half2float(a.wd2[(int64_t)row * NB + c * 32 + (lane >> 1)]);
-        }
-      } else {
-        G.w[rr][c] = make_int4(0, 0, 0, 0);
-        G.dw[rr][c] = 0.f;
-        if (EPI == 2) {
-          G.u[rr][c] = make_int4(0, 0, 0, 0);
-          G.du[rr][c] = 0.f;
-        }
+      G.w[rr][c] = ld_nt16(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
+      const float dv = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+      G.dw[rr][c] = ok ? dv : 0.f;
+      if (EPI == 2) {
+        G.u[rr][c] = ld_nt16(a.wq2 + (int64_t)row * K + c * 1024 + lane * 16);
+        const float du = __half2float(a.wd2[(int64_t)row * NB + c * 32 + (lane >> 1)]);
+        G.du[rr][c] = ok ? du : 0.f;
       }
     }
   }
@@ -218,11 +213,11 @@ __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, i
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         int si = dot16(G.w[rr][c], xv, 0);
-        si += __shfl_xor(si, 1, 64);
+        si += dpp_i<DPP_XOR1>(si);
         if (!(lane & 1)) acc[rr] += (float)si * (G.dw[rr][c] * xdv);
         if (EPI == 2) {
           int su = dot16(G.u[rr][c], xv, 0);
-          su += __shfl_xor(su, 1, 64);
+          su += dpp_i<DPP_XOR1>(su);
           if (!(lane & 1)) acc2[rr] += (float)su * (G.du[rr][c] * xdv);
         }
       }
@@ -395,106 +390,6 @@ void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const floa
                      qout, kc, vc, seq_stride);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Causal GQA attention over the fp16 KV cache: block = (token m, kv head g), handles the H/KV q heads
-// of the group. 4 waves split the keys [0, pos] in 64-key chunks (lane = key for QK, lane = dim pair
-// for PV); partial online-softmax states merged in LDS. scores = q.k / sqrt(128).
-constexpr int GQ = 2;  // q heads per kv head (Qwen3-0.6B: 16/8)
-__global__ __launch_bounds__(256) void k_attn_decode(const float* __restrict__ q, const __half* __restrict__ kc,
-                                                     const __half* __restrict__ vc, float* __restrict__ out, int H,
-                                                     int KV, const int* __restrict__ tok_seq,
-                                                     const int* __restrict__ tok_pos, int64_t seq_stride, float scale) {
-  constexpr int D = 128;
-  const int g = blockIdx.x, m = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pos = tok_pos[m];
-  const int n_keys = pos + 1;
-  const __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
-  const __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
-  __shared__ float s_q[GQ][D];
-  __shared__ float s_p[4][GQ][64];
-  __shared__ float s_m[4][GQ], s_l[4][GQ];
-  __shared__ float s_o[4][GQ][D];
-  for (int i = threadIdx.x; i < GQ * D; i += 256) s_q[i / D][i % D] = q[((int64_t)m * H + g * GQ + i / D) * D + i % D] * scale;
-  __syncthreads();
-  float m_run[GQ], l_run[GQ], o0[GQ], o1[GQ];
-#pragma unroll
-  for (int j = 0; j < GQ; ++j) { m_run[j] = -INFINITY; l_run[j] = 0.f; o0[j] = 0.f; o1[j] = 0.f; }
-  for (int k0 = wave * 64; k0 < n_keys; k0 += 256) {
-    const int key = k0 + lane;
-    float sc[GQ];
-#pragma unroll
-    for (int j = 0; j < GQ; ++j) sc[j] = 0.f;
-    if (key < n_keys) {
-      const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)key * KV * D);
-#pragma unroll
-      for (int c = 0; c < D / 8; ++c) {
-        int4 raw = kp[c];
-        const __half2* hp = reinterpret_cast<const __half2*>(&raw);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float2 kf = __half22float2(hp[e]);
-#pragma unroll
-          for (int j = 0; j < GQ; ++j) sc[j] += kf.x * s_q[j][c * 8 + 2 * e] + kf.y * s_q[j][c * 8 + 2 * e + 1];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < GQ; ++j) sc[j] = -INFINITY;
-    }
-#pragma unroll
-    for (int j = 0; j < GQ; ++j) {
-      const float mt = wave_max(sc[j]);
-      const float mn = fmaxf(m_run[j], mt);
-      const float alpha = m_run[j] == -INFINITY ? 0.f : expf(m_run[j] - mn);
-      const float p = sc[j] == -INFINITY ? 0.f : expf(sc[j] - mn);
-      l_run[j] = l_run[j] * alpha + wave_sum(p);
-      m_run[j] = mn;
-      o0[j] *= alpha;
-      o1[j] *= alpha;
-      s_p[wave][j][lane] = p;
-    }
-    __builtin_amdgcn_wave_barrier();
-    // PV: lane owns dims (2 lane, 2 lane + 1)
-    const int nk = min(64, n_keys - k0);
-    for (int kk = 0; kk < nk; ++kk) {
-      const float2 vf = __half22float2(*reinterpret_cast<const __half2*>(vb + (int64_t)(k0 + kk) * KV * D + 2 * lane));
-#pragma unroll
-      for (int j = 0; j < GQ; ++j) {
-        const float p = s_p[wave][j][kk];
-        o0[j] += p * vf.x;
-        o1[j] += p * vf.y;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < GQ; ++j) {
-    if (lane == 0) { s_m[wave][j] = m_run[j]; s_l[wave][j] = l_run[j]; }
-    s_o[wave][j][2 * lane] = o0[j];
-    s_o[wave][j][2 * lane + 1] = o1[j];
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < GQ * D; i += 256) {
-    const int j = i / D, d = i % D;
-    float M = -INFINITY;
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, s_m[w][j]);
-    float L = 0.f, acc = 0.f;
-    for (int w = 0; w < 4; ++w) {
-      const float sc = s_m[w][j] == -INFINITY ? 0.f : expf(s_m[w][j] - M);
-      L += sc * s_l[w][j];
-      acc += sc * s_o[w][j][d];
-    }
-    out[((int64_t)m * H + g * GQ + j) * D + d] = acc / L;
-  }
-}
-
-void attn_decode(const float* q, const __half* kc, const __half* vc, float* out, int M, int H, int KV,
-                 const int* tok_seq, const int* tok_pos, int64_t seq_stride, hipStream_t s) {
-  FA_REQUIRE(H == KV * GQ, "attn_decode: n_head must be 2*n_head_kv");
-  const float scale = 1.0f / sqrtf(128.0f);
-  hipLaunchKernelGGL(k_attn_decode, dim3(KV, M), dim3(256), 0, s, q, kc, vc, out, H, KV, tok_seq, tok_pos, seq_stride,
-                     scale);
-}
 
 // ------------------------------------------------------------------------------------------------
 // Decode/prefill attention over the fp16 KV cache. Block = (kv head g, token m), 8 waves; wave w takes the
@@ -504,58 +399,215 @@ void attn_decode(const float* q, const __half* kc, const __half* vc, float* out,
 // whose chunk holds the token's position also norms/ropes k, stores K/V of that position to the cache and
 // consumes the fresh row from LDS (with the cache's fp16 rounding). PREFILL mode: q comes pre-roped from
 // qk_rope_store and the cache is complete.
-constexpr int ACH = 64;   // keys per chunk
-constexpr int AWV = 8;    // waves per block
-__device__ __forceinline__ void load_k_chunk(const __half* __restrict__ kb, int KV, int k0, int n_keys, int fresh,
-                                             int lane, int4 (&kraw)[16]) {
+#ifdef FA_ATTN_STAMPS
+__device__ unsigned long long g_attn_stamps[16];
+#define STAMP(i) do { if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_attn_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+constexpr int GQ = 2;     // query heads per kv head (Qwen3-0.6B: 16 / 8)
+constexpr int AWV = 4;    // waves per block
+constexpr int AGI = 16;   // 4-key groups per wave per pass (registers: 16 int4 of K + 16 of V)
+constexpr int ASPLIT = ATTN_SPLITS;  // key splits (blocks) per (token, kv head)
+constexpr int AMIN_G = 8;            // minimum 4-key groups per split (32 keys = 16 KB of K+V)
+constexpr int APART = ATTN_PART_FLOATS;  // per-split partial: o[GQ][128], m[GQ], l[GQ]
+// Within a split, keys are dealt to the waves in 4-key groups, round-robin (group q -> wave q % AWV).
+// Lane (kq = lane>>4, dq = lane&15) holds dims [8 dq, 8 dq + 8) of key 4 q + kq: each load instruction
+// reads 4 whole 256-B rows. Groups past the wave's share are loaded clamped (valid rows, compute skipped):
+// no branches around loads.
+template <int NI>
+__device__ __forceinline__ void load_kv_groups(const __half* __restrict__ base, int KV, int g0, int n_keys, int kq,
+                                               int dq, int4 (&t)[NI]) {
   constexpr int D = 128;
-  const bool kok = lane < n_keys && lane != fresh;
-  const int4* kp = reinterpret_cast<const int4*>(kb + (int64_t)(k0 + lane) * KV * D);
 #pragma unroll
-  for (int c8 = 0; c8 < 16; ++c8) kraw[c8] = kok ? kp[c8] : make_int4(0, 0, 0, 0);
-}
-
-__device__ __forceinline__ void load_v_chunk(const __half* __restrict__ vb, int KV, int k0, int n_keys, int fresh,
-                                             int kq, int dq, int4 (&vraw)[16]) {
-  constexpr int D = 128;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int k = kq + 4 * i;
-    vraw[i] = (k < n_keys && k != fresh) ? *reinterpret_cast<const int4*>(vb + (int64_t)(k0 + k) * KV * D + dq * 8)
-                                         : make_int4(0, 0, 0, 0);
+  for (int i = 0; i < NI; ++i) {
+    const int k = min(4 * (g0 + AWV * i) + kq, n_keys - 1);
+    t[i] = *reinterpret_cast<const int4*>(base + (int64_t)k * KV * D + dq * 8);
   }
 }
 
-__device__ __forceinline__ void rope_norm_head(const float* __restrict__ src, const float* __restrict__ nw, float eps,
-                                               float c, float sn, int lane, float& y0, float& y1) {
-  float x0 = src[lane], x1 = src[lane + 64];
+__device__ __forceinline__ void unpack8(const int4& r, float (&v)[8]) {
+  const __half2* hp = reinterpret_cast<const __half2*>(&r);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float2 f = __half22float2(hp[e]);
+    v[2 * e] = f.x;
+    v[2 * e + 1] = f.y;
+  }
+}
+
+// RMSNorm (q_norm / k_norm) + NeoX RoPE of one 128-dim head held as (x0 = dim lane, x1 = dim lane + 64).
+__device__ __forceinline__ void norm_rope(float x0, float x1, float w0, float w1, float eps, float c, float sn,
+                                          float& y0, float& y1) {
   const float sc = 1.0f / sqrtf(wave_sum(x0 * x0 + x1 * x1) / 128.0f + eps);
-  x0 = (x0 * sc) * nw[lane];
-  x1 = (x1 * sc) * nw[lane + 64];
+  x0 = (x0 * sc) * w0;
+  x1 = (x1 * sc) * w1;
   y0 = x0 * c - x1 * sn;
   y1 = x0 * sn + x1 * c;
 }
 
+// raw per-lane inputs of the q (and fresh k/v) prologue, loaded before the K/V stream is issued
+struct AttnQIn {
+  float x0[GQ], x1[GQ];             // q heads (dims lane, lane + 64)
+  float c, sn, w0, w1;              // rope cos/sin at pos, q_norm weights
+  float kx0, kx1, kw0, kw1, v0, v1; // fresh k (pre-norm), k_norm weights, fresh v (owner wave only)
+};
+
+// One wave's share of one key split: NI = its 4-key groups per pass rounded up to a power of two (loads of
+// the rounded-up slots are clamped duplicates, masked). Issues the K/V stream first, then finishes q while
+// it is in flight.
+template <int NI>
+__device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
+                                          int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
+                                          int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
+                                          __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
+                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8]) {
+  int4 kt[NI], vt[NI];
+  load_kv_groups<NI>(kb, KV, g0, n_keys, kq, dq, kt);
+  load_kv_groups<NI>(vb, KV, g0, n_keys, kq, dq, vt);
+  STAMP(2);
+  if (decode) {
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      float y0, y1;
+      norm_rope(qi.x0[j], qi.x1[j], qi.w0, qi.w1, eps, qi.c, qi.sn, y0, y1);
+      s_qw[j][lane] = y0 * scale;
+      s_qw[j][lane + 64] = y1 * scale;
+    }
+    if (fresh_here) {  // this wave owns K/V[pos]: store it to the cache and use it from LDS
+      float y0, y1;
+      norm_rope(qi.kx0, qi.kx1, qi.kw0, qi.kw1, eps, qi.c, qi.sn, y0, y1);
+      const __half k0h = __float2half_rn(y0), k1h = __float2half_rn(y1);
+      const __half v0h = __float2half_rn(qi.v0), v1h = __float2half_rn(qi.v1);
+      kd[lane] = k0h;
+      kd[lane + 64] = k1h;
+      vd[lane] = v0h;
+      vd[lane + 64] = v1h;
+      s_kn[lane] = __half2float(k0h);
+      s_kn[lane + 64] = __half2float(k1h);
+      s_vn[lane] = __half2float(v0h);
+      s_vn[lane + 64] = __half2float(v1h);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      s_qw[j][lane] = qi.x0[j] * scale;
+      s_qw[j][lane + 64] = qi.x1[j] * scale;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  float q[GQ][8];
+#pragma unroll
+  for (int j = 0; j < GQ; ++j) {
+    const float4 a0 = *reinterpret_cast<const float4*>(&s_qw[j][dq * 8]);
+    const float4 a1 = *reinterpret_cast<const float4*>(&s_qw[j][dq * 8 + 4]);
+    q[j][0] = a0.x; q[j][1] = a0.y; q[j][2] = a0.z; q[j][3] = a0.w;
+    q[j][4] = a1.x; q[j][5] = a1.y; q[j][6] = a1.z; q[j][7] = a1.w;
+  }
+  STAMP(3);
+  const int fresh = fresh_here ? pos : -1;
+  for (;;) {
+    // scores of key 4 (g0 + AWV i) + kq: 8-dim partial dot per lane, summed over the row's 16 lanes (DPP)
+    float sc[NI][GQ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int key = 4 * (g0 + AWV * i) + kq;
+      const bool valid = (g0 + AWV * i) < ge && key < n_keys;
+      float kv[8];
+      unpack8(kt[i], kv);
+      if (key == fresh) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) kv[e] = s_kn[dq * 8 + e];
+      }
+#pragma unroll
+      for (int j = 0; j < GQ; ++j) {
+        float pd = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pd += kv[e] * q[j][e];
+        pd = row_sum16(pd);
+        sc[i][j] = valid ? pd : -INFINITY;
+      }
+    }
+    STAMP(4);
+    // online softmax: row-local max/sum over i, then across the 4 rows (readlanes)
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
+      float cm = sc[0][j];
+#pragma unroll
+      for (int i = 1; i < NI; ++i) cm = fmaxf(cm, sc[i][j]);
+      cm = fmaxf(fmaxf(lane_f(cm, 0), lane_f(cm, 16)), fmaxf(lane_f(cm, 32), lane_f(cm, 48)));
+      const float mn = fmaxf(mx[j], cm);
+      const float alpha = mx[j] == -INFINITY ? 0.f : __expf(mx[j] - mn);
+      float ps = 0.f;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float p = sc[i][j] == -INFINITY ? 0.f : __expf(sc[i][j] - mn);
+        sc[i][j] = p;
+        ps += p;
+      }
+      ps = (lane_f(ps, 0) + lane_f(ps, 16)) + (lane_f(ps, 32) + lane_f(ps, 48));
+      l[j] = l[j] * alpha + ps;
+      mx[j] = mn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[j][e] *= alpha;
+    }
+    STAMP(5);
+    // p.V with p still in registers
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int key = 4 * (g0 + AWV * i) + kq;
+      float v[8];
+      unpack8(vt[i], v);
+      if (key == fresh) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = s_vn[dq * 8 + e];
+      }
+#pragma unroll
+      for (int j = 0; j < GQ; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] += sc[i][j] * v[e];
+    }
+    STAMP(6);
+    g0 += AWV * NI;
+    if (g0 >= ge) break;
+    load_kv_groups<NI>(kb, KV, g0, n_keys, kq, dq, kt);
+    load_kv_groups<NI>(vb, KV, g0, n_keys, kq, dq, vt);
+  }
+}
+
+// Decode / causal attention for one (kv head g, token m, key split sp): GQ = 2 query heads share the
+// K/V stream. Keys [0, pos] are cut into n_active contiguous splits of >= AMIN_G groups each (one block
+// per split, so a long context is fetched by up to ASPLIT CUs instead of one). A single active split writes
+// the output directly; otherwise each split stores its (m, l, o) partial with sc1 stores, waits, and adds
+// to the (m, g) counter (agent scope); the block whose add comes last combines the partials with sc1
+// loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1: no fences needed).
+// Prefill mode (decode_mode = 0): q is already normed/roped (qk_rope_store) and K/V[pos] are in the cache.
 __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict__ qsrc, int decode_mode,
                                                          const float* __restrict__ qn, const float* __restrict__ kn,
                                                          float eps, const float* __restrict__ rcos,
                                                          const float* __restrict__ rsin, __half* __restrict__ kc,
                                                          __half* __restrict__ vc, int H, int KV,
                                                          const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
-                                                         int64_t seq_stride, float scale, float* __restrict__ out) {
+                                                         int64_t seq_stride, float scale, float* __restrict__ out,
+                                                         int* __restrict__ counters, float* __restrict__ partials) {
   constexpr int D = 128;
-  const int g = blockIdx.x, m = blockIdx.y;
+  STAMP(0);
+  const int g = blockIdx.x % KV, sp = blockIdx.x / KV, m = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pos = tok_pos[m];
-  const int n_keys_all = pos + 1;
-  const int n_chunks = (n_keys_all + ACH - 1) / ACH;
+  const int n_keys = pos + 1;
+  const int n_groups = (n_keys + 3) >> 2;
+  const int gps = max(AMIN_G, (n_groups + ASPLIT - 1) / ASPLIT);  // groups per split
+  const int n_active = (n_groups + gps - 1) / gps;
+  if (sp >= n_active) return;                                      // uniform over the block
+  const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
+  STAMP(1);
   __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
   __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
-  __shared__ float4 s_q4[AWV][GQ][D / 4];   // per-wave copy of the scaled, roped q heads
+  __shared__ float s_q[AWV][GQ][D];          // per-wave q (scaled, roped) in natural dim order
   __shared__ float s_kn[D], s_vn[D];         // fresh K/V row (decode)
-  __shared__ float s_p[AWV][GQ][ACH];
   __shared__ float s_ml[AWV][GQ][2];
-  __shared__ float s_o[AWV][GQ][D];
+  __shared__ float s_o[AWV][4][GQ][D];       // [wave][key row kq][head][dim]
   const int kq = lane >> 4, dq = lane & 15;
   float mx[GQ], l[GQ], acc[GQ][8];
 #pragma unroll
@@ -565,169 +617,148 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
   }
-  if (wave < n_chunks) {
-    const int fresh_chunk = decode_mode ? pos / ACH : -1;
-    // (1) issue the first chunk's K/V loads before any dependent work
-    int ch = wave;
-    int k0 = ch * ACH;
-    int n_keys = min(ACH, n_keys_all - k0);
-    int fresh = ch == fresh_chunk ? pos - k0 : -1;
-    int4 kraw[D / 8], vraw[ACH / 4];
-    load_k_chunk(kb, KV, k0, n_keys, fresh, lane, kraw);
-    // (2) this wave's own q (no block barrier); the fresh chunk's wave also produces K/V[pos]
-    {
-      float* sq = reinterpret_cast<float*>(s_q4[wave]);
-      if (decode_mode) {
-        const float c = rcos[(int64_t)pos * 64 + lane], sn = rsin[(int64_t)pos * 64 + lane];
-        const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
-#pragma unroll
-        for (int j = 0; j < GQ; ++j) {
-          float y0, y1;
-          rope_norm_head(row + (g * GQ + j) * D, qn, eps, c, sn, lane, y0, y1);
-          sq[j * D + lane] = y0 * scale;
-          sq[j * D + lane + 64] = y1 * scale;
-        }
-        if (fresh_chunk == wave) {
-          float y0, y1;
-          rope_norm_head(row + (H + g) * D, kn, eps, c, sn, lane, y0, y1);
-          const __half k0h = __float2half_rn(y0), k1h = __float2half_rn(y1);
-          const float* vp = row + (H + KV + g) * D;
-          const __half v0h = __float2half_rn(vp[lane]), v1h = __float2half_rn(vp[lane + 64]);
-          __half* kd = kb + (int64_t)pos * KV * D;
-          __half* vd = vb + (int64_t)pos * KV * D;
-          kd[lane] = k0h;
-          kd[lane + 64] = k1h;
-          vd[lane] = v0h;
-          vd[lane + 64] = v1h;
-          s_kn[lane] = __half2float(k0h);
-          s_kn[lane + 64] = __half2float(k1h);
-          s_vn[lane] = __half2float(v0h);
-          s_vn[lane + 64] = __half2float(v1h);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < GQ; ++j) {
-          const float* qp = qsrc + ((int64_t)m * H + g * GQ + j) * D;
-          sq[j * D + lane] = qp[lane] * scale;
-          sq[j * D + lane + 64] = qp[lane + 64] * scale;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    for (;;) {
-      // (3) scores: lane = key
-      float sc[GQ] = {};
-      if (lane == fresh) {
-#pragma unroll 8
-        for (int d4 = 0; d4 < D / 4; ++d4)
-#pragma unroll
-          for (int j = 0; j < GQ; ++j) {
-            const float4 q4 = s_q4[wave][j][d4];
-            sc[j] += s_kn[4 * d4] * q4.x + s_kn[4 * d4 + 1] * q4.y + s_kn[4 * d4 + 2] * q4.z + s_kn[4 * d4 + 3] * q4.w;
-          }
-      } else {
-#pragma unroll
-        for (int c8 = 0; c8 < D / 8; ++c8) {
-          const __half2* hp = reinterpret_cast<const __half2*>(&kraw[c8]);
-          const float2 k0f = __half22float2(hp[0]), k1f = __half22float2(hp[1]);
-          const float2 k2f = __half22float2(hp[2]), k3f = __half22float2(hp[3]);
-#pragma unroll
-          for (int j = 0; j < GQ; ++j) {
-            const float4 qa = s_q4[wave][j][2 * c8], qb = s_q4[wave][j][2 * c8 + 1];
-            sc[j] += k0f.x * qa.x + k0f.y * qa.y + k1f.x * qa.z + k1f.y * qa.w + k2f.x * qb.x + k2f.y * qb.y +
-                     k3f.x * qb.z + k3f.y * qb.w;
-          }
-        }
-      }
-      load_v_chunk(vb, KV, k0, n_keys, fresh, kq, dq, vraw);  // V latency overlaps the softmax reductions
+  const int fresh_group = decode_mode ? (pos >> 2) : -1;
+  const bool fresh_here = fresh_group >= gb && fresh_group < ge && (fresh_group - gb) % AWV == wave;
+  const int g0 = gb + wave;
+  if (g0 < ge) {
+    AttnQIn qi;
+    if (decode_mode) {
+      const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
       for (int j = 0; j < GQ; ++j) {
-        if (lane >= n_keys) sc[j] = -INFINITY;
-        const float mn = fmaxf(mx[j], wave_max(sc[j]));
-        const float alpha = mx[j] == -INFINITY ? 0.f : __expf(mx[j] - mn);
-        const float p = lane < n_keys ? __expf(sc[j] - mn) : 0.f;
-        l[j] = l[j] * alpha + wave_sum(p);
-        mx[j] = mn;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[j][e] *= alpha;
-        s_p[wave][j][lane] = p;
+        qi.x0[j] = row[(g * GQ + j) * D + lane];
+        qi.x1[j] = row[(g * GQ + j) * D + lane + 64];
       }
-      __builtin_amdgcn_wave_barrier();
-      // (4) p.V: 8 dims x 16 keys per lane (4 key phases reduced at the end)
+      qi.c = rcos[(int64_t)pos * 64 + lane];
+      qi.sn = rsin[(int64_t)pos * 64 + lane];
+      qi.w0 = qn[lane];
+      qi.w1 = qn[lane + 64];
+      // fresh k/v values: loaded by every wave (clamped addresses, no branch), used by the owner only
+      qi.kx0 = row[(H + g) * D + lane];
+      qi.kx1 = row[(H + g) * D + lane + 64];
+      qi.kw0 = kn[lane];
+      qi.kw1 = kn[lane + 64];
+      qi.v0 = row[(H + KV + g) * D + lane];
+      qi.v1 = row[(H + KV + g) * D + lane + 64];
+    } else {
 #pragma unroll
-      for (int i = 0; i < ACH / 4; ++i) {
-        const int k = kq + 4 * i;
-        float v[8];
-        if (k == fresh) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = s_vn[dq * 8 + e];
-        } else {
-          const __half2* hp = reinterpret_cast<const __half2*>(&vraw[i]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float2 f = __half22float2(hp[e]);
-            v[2 * e] = f.x;
-            v[2 * e + 1] = f.y;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < GQ; ++j) {
-          const float p = s_p[wave][j][k];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[j][e] += p * v[e];
-        }
+      for (int j = 0; j < GQ; ++j) {
+        const float* qp = qsrc + ((int64_t)m * H + g * GQ + j) * D;
+        qi.x0[j] = qp[lane];
+        qi.x1[j] = qp[lane + 64];
       }
-      __builtin_amdgcn_wave_barrier();
-      ch += AWV;
-      if (ch >= n_chunks) break;
-      k0 = ch * ACH;
-      n_keys = min(ACH, n_keys_all - k0);
-      fresh = ch == fresh_chunk ? pos - k0 : -1;
-      load_k_chunk(kb, KV, k0, n_keys, fresh, lane, kraw);
     }
+    __half* kd = kb + (int64_t)pos * KV * D;
+    __half* vd = vb + (int64_t)pos * KV * D;
+    const int ni = (ge - g0 + AWV - 1) / AWV;
+    if (ni <= 1)
+      attn_wave<1>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+                   s_q[wave], s_kn, s_vn, mx, l, acc);
+    else if (ni <= 2)
+      attn_wave<2>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+                   s_q[wave], s_kn, s_vn, mx, l, acc);
+    else if (ni <= 4)
+      attn_wave<4>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+                   s_q[wave], s_kn, s_vn, mx, l, acc);
+    else
+      attn_wave<8>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+                   s_q[wave], s_kn, s_vn, mx, l, acc);
   }
-  // reduce the 4 key phases, publish per-wave (m, l, o), merge the waves
+  // publish per-wave (m, l) and per-row partial o
 #pragma unroll
   for (int j = 0; j < GQ; ++j) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      acc[j][e] += __shfl_xor(acc[j][e], 16, 64);
-      acc[j][e] += __shfl_xor(acc[j][e], 32, 64);
-    }
     if (lane == 0) {
       s_ml[wave][j][0] = mx[j];
       s_ml[wave][j][1] = l[j];
     }
-    if (kq == 0) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s_o[wave][j][dq * 8 + e] = acc[j][e];
-    }
+    float4* dst = reinterpret_cast<float4*>(&s_o[wave][kq][j][dq * 8]);
+    dst[0] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    dst[1] = make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
   }
+  STAMP(7);
   __syncthreads();
-  if (threadIdx.x < GQ * D) {
-    const int j = threadIdx.x / D, d = threadIdx.x % D;
-    float M = -INFINITY;
+  if (wave != 0) return;
+  STAMP(8);
+  // wave 0 merges the waves: lane -> head j = lane >> 5, dims [4 (lane & 31), +4)
+  const int j = lane >> 5, d0 = (lane & 31) * 4;
+  float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_ml[w][j][0]);
-    float L = 0.f, o = 0.f;
+  for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_ml[w][j][0]);
+  float L = 0.f;
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int w = 0; w < AWV; ++w) {
-      const float mw = s_ml[w][j][0];
-      const float wt = mw == -INFINITY ? 0.f : __expf(mw - M);
-      L += wt * s_ml[w][j][1];
-      o += wt * s_o[w][j][d];
+  for (int w = 0; w < AWV; ++w) {
+    const float mw = s_ml[w][j][0];
+    const float wt = mw == -INFINITY ? 0.f : __expf(mw - M);
+    L += wt * s_ml[w][j][1];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float4 t = *reinterpret_cast<const float4*>(&s_o[w][r][j][d0]);
+      o.x += wt * t.x;
+      o.y += wt * t.y;
+      o.z += wt * t.z;
+      o.w += wt * t.w;
     }
-    out[((int64_t)m * H + g * GQ + j) * D + d] = o / L;
   }
+  float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;
+  if (n_active == 1) {
+    *reinterpret_cast<float4*>(op) = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+    STAMP(9);
+    return;
+  }
+  // split partial -> global (sc1: bypass L1, the combiner reads it from another CU)
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  float* pbase = partials + ((int64_t)m * KV + g) * ASPLIT * APART;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pbase, 0, ASPLIT * APART * 4, 0x00020000);
+  constexpr int SC1 = 16;
+  const f4v ov = {o.x, o.y, o.z, o.w};
+  __builtin_amdgcn_raw_buffer_store_b128(ov, rs, (sp * APART + j * D + d0) * 4, 0, SC1);
+  const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
+  if (lane == 0) {
+    const f4v ml = {M, L, M1, L1};
+    __builtin_amdgcn_raw_buffer_store_b128(ml, rs, (sp * APART + GQ * D) * 4, 0, SC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) last = __hip_atomic_fetch_add(counters + m * KV + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  last = __builtin_amdgcn_readfirstlane(last);
+  if (last != n_active - 1) return;
+  STAMP(9);
+  // last split: combine all n_active partials
+  f4v pml[ASPLIT], po[ASPLIT];
+#pragma unroll
+  for (int t = 0; t < ASPLIT; ++t) {
+    const int tt = min(t, n_active - 1);
+    pml[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tt * APART + GQ * D) * 4, 0, SC1);
+    po[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tt * APART + j * D + d0) * 4, 0, SC1);
+  }
+  float MM = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < ASPLIT; ++t)
+    if (t < n_active) MM = fmaxf(MM, j ? pml[t].z : pml[t].x);
+  float LL = 0.f;
+  f4v oo = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < ASPLIT; ++t) {
+    if (t < n_active) {
+      const float mt = j ? pml[t].z : pml[t].x;
+      const float wt = mt == -INFINITY ? 0.f : __expf(mt - MM);
+      LL += wt * (j ? pml[t].w : pml[t].y);
+      oo += wt * po[t];
+    }
+  }
+  *reinterpret_cast<float4*>(op) = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
+  if (lane == 0) __hip_atomic_store(counters + m * KV + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* out, hipStream_t s) {
+                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s) {
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
+  FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
-  hipLaunchKernelGGL(k_attn_block, dim3(KV, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos, rsin, kc,
-                     vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out);
+  hipLaunchKernelGGL(k_attn_block, dim3(KV * ASPLIT, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos,
+                     rsin, kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out, wk.counters, wk.partials);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -30,6 +30,9 @@ static double time_graph(const char* name, std::function<void()> f, int reps = 2
 }
 int main() {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
+  CK(hipMalloc(&wk.counters, 64)); CK(hipMemset(wk.counters, 0, 64));
+  CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048;
   auto q8 = [&](int64_t rows, int64_t cols, uint32_t key, int8_t** q, __half** d) {
     float* tmp = dalloc<float>(rows * cols);
@@ -69,7 +72,16 @@ int main() {
   { auto a = G(wd, dd, E, act, nullptr, out, out); a.ldx = F;
     tot += time_graph("gemv down 1024x3072 (+res)", [&] { gemv_q8(a, F, 1, s); }, 200, E * F * 34.0 / 32); }
   tot += time_graph("attn_block decode n_past=330", [&] {
-    attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc, vc, 1, H, KV, seq, pos, (int64_t)NCTX * KV * D, att, s); });
+    attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc, vc, 1, H, KV, seq, pos, (int64_t)NCTX * KV * D, att, wk, s); });
+  time_graph("attn_block prefill-mode n_past=330", [&] {
+    attn_block(att, 0, qn, qn, 1e-6f, rc, rs, kc, vc, 1, H, KV, seq, pos, (int64_t)NCTX * KV * D, qkv, wk, s); });
+  int p1 = 40; CK(hipMemcpy(pos, &p1, 4, hipMemcpyHostToDevice));
+  time_graph("attn_block decode n_past=40", [&] {
+    attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc, vc, 1, H, KV, seq, pos, (int64_t)NCTX * KV * D, att, wk, s); });
+  p1 = 1000; CK(hipMemcpy(pos, &p1, 4, hipMemcpyHostToDevice));
+  time_graph("attn_block decode n_past=1000", [&] {
+    attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc, vc, 1, H, KV, seq, pos, (int64_t)NCTX * KV * D, att, wk, s); });
+  p1 = 330; CK(hipMemcpy(pos, &p1, 4, hipMemcpyHostToDevice));
   printf("%-34s %8.2f us  (x28 = %.1f us/step)\n", "layer sum", tot, tot * 28);
   { auto a = G(wemb, demb, V, x, nw, out, nullptr); a.ldx = E; a.pval = pval; a.pidx = pidx;
     a.n_part = (V + 4 * a.rpw - 1) / (4 * a.rpw) * 4;

@@ -17,6 +17,9 @@ using namespace fa;
 template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T))); return (T*)p; }
 int main(int argc, char** argv) {
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
+  CK(hipMalloc(&wk.counters, 64)); CK(hipMemset(wk.counters, 0, 64));
+  CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048, L = 28;
   float* tmp = dalloc<float>((size_t)V * E);
   auto q8 = [&](int64_t rows, int64_t cols, uint32_t key, int8_t** q, __half** d) {
@@ -52,7 +55,7 @@ int main(int argc, char** argv) {
       auto& w = lw[l];
       gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
       attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV,
-                 seq, pos, (int64_t)NCTX * KV * D, att, s);
+                 seq, pos, (int64_t)NCTX * KV * D, att, wk, s);
       gemv_q8(G(w.o, w.dO, E, att, H * D, nullptr, x, x), H * D, 1, s);
       auto gu = G(w.g, w.dg, F, x, E, nw, act, nullptr); gu.wq2 = w.u; gu.wd2 = w.du; gemv_q8(gu, E, 2, s);
       gemv_q8(G(w.d, w.dd, E, act, F, nullptr, x, x), F, 1, s);

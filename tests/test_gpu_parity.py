@@ -156,6 +156,27 @@ def test_llm_prefill_and_decode_teacher_forced_tiny(tiny_engine, llm_tiny_oracle
     assert tiny_engine.llm_n_past(0) == prompt.shape[0] + 12
 
 
+def test_llm_long_context_split_attention(tiny_engine, llm_tiny_oracle):
+    """400-token context: the decode/prefill attention cuts keys over 13 blocks and combines their partials
+    (last-arriving block); teacher-forced against the oracle at every step."""
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(5)
+    prompt = np.concatenate([m.embed_prompt(rng.integers(0, 4096, 150)),
+                             (rng.standard_normal((250, 1024)) * 0.5).astype(np.float32)], 0)
+    tiny_engine.llm_reset(1)
+    tok, lg = tiny_engine.llm_prefill(1, prompt, want_logits=True)
+    m.reset()
+    ref = m.forward(prompt, 0)
+    _check_step(lg, ref)
+    pos = prompt.shape[0]
+    for _ in range(5):
+        nxt = tiny_engine.llm_generate([1], 1)[0][0]
+        lg_new = tiny_engine.llm_logits(0)  # row 0 of the 1-sequence batch
+        ref = m.forward(m.embed_tokens([tok]), pos)
+        _check_step(lg_new, ref)
+        tok, pos = int(nxt), pos + 1
+
+
 def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
     rng = np.random.default_rng(4)
     prompts = [llm_tiny_oracle.embed_prompt(rng.integers(0, 4096, n)) for n in (9, 17, 5)]
