@@ -124,7 +124,7 @@ struct Engine {
   float *rcos = nullptr, *rsin = nullptr;
   __half *kcache = nullptr, *vcache = nullptr;
   int64_t seq_stride = 0, layer_stride = 0;
-  int m_max = 0, n_part = 0;
+  int m_max = 0, n_part = 0, n_part_cur = 0;  // partial stride allocated / written by the last lm_head
   float *lx = nullptr, *lqkv = nullptr, *lq = nullptr, *latt = nullptr, *lact = nullptr, *logits = nullptr;
   int8_t* lxq = nullptr;
   float* lxd = nullptr;
@@ -508,8 +508,7 @@ struct Engine {
     lxq = alloc<int8_t>((size_t)m_max * kmax);
     lxd = alloc<float>((size_t)m_max * kmax / 32);
     logits = alloc<float>((size_t)lc.max_seqs * lc.n_vocab);
-    const int rpw = gemv_rows_per_wave(lc.n_vocab);
-    n_part = cdiv(lc.n_vocab, 4 * rpw) * 4;
+    n_part = std::max(lm_head_parts(lc.n_vocab, 1), lm_head_parts(lc.n_vocab, lc.max_seqs));
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
 
@@ -752,7 +751,7 @@ struct Engine {
     h.M = n_rows; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
-    h.pval = pval; h.pidx = pidx; h.n_part = n_part;
+    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows);
     if (n_rows <= 4) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
     gemv(h, E, 3);
@@ -819,7 +818,7 @@ struct Engine {
 
   void sample(int M, const fa_sampling* s, const int* step_ctr, int* tok_out, int* hist) {
     const float temp = s ? s->temperature : 0.f;
-    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part, M, temp, s ? s->top_k : 1, s ? s->top_p : 1.f,
+    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, M, temp, s ? s->top_k : 1, s ? s->top_p : 1.f,
                   s ? s->seed : 0u, step_ctr, tok_out, hist, hist_max, stream);
   }
 };

@@ -4,6 +4,7 @@
 //   integer dot is exact (v_dot4_i32_i8), scaled by f32(dw)*f32(dx) and summed in f32.
 // The decode GEMV streams every weight byte exactly once per step for the whole continuous batch
 // (HBM-bound: 633 MB/step for Qwen3-0.6B q8_0); one wave covers a K=1024 row with ONE 16 B/lane load.
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 
@@ -311,6 +312,115 @@ static void launch_gemv_k(int K, const GemvArgs& a, hipStream_t s) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// q8_0 x q8_0 GEMM on the int8 matrix cores (M > 4: prefill and continuous-batch decode). gfx950's
+// v_mfma_i32_32x32x32_i8 has K = 32 = one q8_0 block, so each MFMA yields the EXACT integer block dot
+// for a 32-row x 32-token tile (the ggml per-block sumi); it is scaled by f32(dw) * f32(dx) and summed in
+// f32, as ggml_vec_dot_q8_0_q8_0 does. Operand map (verified with exact integers,
+// scripts/ubench/mfma_i8_probe.hip): lane l holds A[l&31][16(l>>5) + j], B[16(l>>5) + j][l&31];
+// D: col = l&31 (token), row = (reg&3) + 8(reg>>2) + 4(l>>5) (weight row).
+// Block = 4 waves over one 32x32 tile, each wave a contiguous quarter of K; partial tiles are summed in
+// LDS in fixed wave order (deterministic). Epilogues as k_gemv_q8.
+typedef int i32x16_t __attribute__((ext_vector_type(16)));
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K) {
+  constexpr int NG = EPI == 2 ? 4 : 8;  // q8_0 blocks per load group (gate+up: half, to stay in registers)
+  typedef typename std::conditional<NG == 8, uint4, uint2>::type ScaleVec;  // NG fp16 scales of one row
+  const int nb = K >> 5, nbw = nb >> 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
+  const int o_a = min(o0 + r, a.O - 1);
+  const int t_b = min(t0 + r, a.M - 1);
+  const int8_t* wa = a.wq + (int64_t)o_a * K + 16 * h;
+  const int8_t* wu = EPI == 2 ? a.wq2 + (int64_t)o_a * K + 16 * h : nullptr;
+  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h;
+  const float* xd = a.xd + (int64_t)t_b * nb;
+  int orow[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) orow[reg] = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
+  float acc[16], accu[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) acc[reg] = accu[reg] = 0.f;
+  const i32x16_t zero = {};
+  for (int b0 = wave * nbw; b0 < (wave + 1) * nbw; b0 += NG) {
+    i32x4_t A[NG], U[NG], B[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      A[j] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(wa + (b0 + j) * 32));
+      if (EPI == 2) U[j] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(wu + (b0 + j) * 32));
+      B[j] = *reinterpret_cast<const i32x4_t*>(xb + (b0 + j) * 32);
+    }
+    ScaleVec dw[16], du[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      dw[reg] = *reinterpret_cast<const ScaleVec*>(a.wd + (int64_t)orow[reg] * nb + b0);
+      if (EPI == 2) du[reg] = *reinterpret_cast<const ScaleVec*>(a.wd2 + (int64_t)orow[reg] * nb + b0);
+    }
+    float dx[NG];
+#pragma unroll
+    for (int j = 0; j < NG; j += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(xd + b0 + j);
+      dx[j] = v.x; dx[j + 1] = v.y; dx[j + 2] = v.z; dx[j + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
+      i32x16_t DU;
+      if (EPI == 2) DU = __builtin_amdgcn_mfma_i32_32x32x32_i8(U[j], B[j], zero, 0, 0, 0);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const __half* hw = reinterpret_cast<const __half*>(&dw[reg]);
+        acc[reg] += (float)D[reg] * (__half2float(hw[j]) * dx[j]);
+        if (EPI == 2) {
+          const __half* hu = reinterpret_cast<const __half*>(&du[reg]);
+          accu[reg] += (float)DU[reg] * (__half2float(hu[j]) * dx[j]);
+        }
+      }
+    }
+  }
+  // fixed-order reduction of the 4 K-quarters; thread t finalises regs [4 (t>>6), +4) of lane t&63
+  constexpr int NS = EPI == 2 ? 2 : 1;
+  __shared__ float s_red[NS][4][16][64];
+  __shared__ float s_out[32][33];  // EPI 3: [token][row] for the per-token argmax
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    s_red[0][wave][reg][lane] = acc[reg];
+    if (EPI == 2) s_red[NS - 1][wave][reg][lane] = accu[reg];
+  }
+  __syncthreads();
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = l & 31, tok = t0 + col;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int reg = 4 * g + q;
+    const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
+    const int row = o0 + rrow;
+    const float y = ((s_red[0][0][reg][l] + s_red[0][1][reg][l]) + s_red[0][2][reg][l]) + s_red[0][3][reg][l];
+    if (EPI == 3) s_out[col][rrow] = row < a.O ? y : -INFINITY;
+    if (row < a.O && tok < a.M) {
+      float* op = a.out + (int64_t)tok * a.ldo + row;
+      if (EPI == 0 || EPI == 3) *op = y;
+      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y;
+      else {
+        const float y2 =
+            ((s_red[NS - 1][0][reg][l] + s_red[NS - 1][1][reg][l]) + s_red[NS - 1][2][reg][l]) + s_red[NS - 1][3][reg][l];
+        *op = (y / (1.0f + expf(-y))) * y2;
+      }
+    }
+  }
+  if (EPI == 3) {
+    __syncthreads();
+    if (threadIdx.x < 32 && t0 + threadIdx.x < a.M) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int rr = 0; rr < 32; ++rr) argmax_combine(bv, bi, s_out[threadIdx.x][rr], o0 + rr);
+      a.pval[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bv;
+      a.pidx[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bi;
+    }
+  }
+}
+
 int gemv_rows_per_wave(int O) {
   // target ~256-1024 blocks of 4 waves
   int rpw = (O + 4 * 256 - 1) / (4 * 256);
@@ -322,6 +432,7 @@ int gemv_rows_per_wave(int O) {
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   const bool fused = a.x != nullptr;
   if (a.M <= 4 && fused) {
+    FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemv_q8: n_part");
     // decode path: tokens handled one per block row
     switch (epi) {
       case 0: launch_gemv_k<1, true, 0>(K, a, s); break;
@@ -332,13 +443,18 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     return;
   }
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
+  FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
+  FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
+  dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32));
   switch (epi) {
-    case 0: launch_gemv_k<8, false, 0>(K, a, s); break;
-    case 1: launch_gemv_k<8, false, 1>(K, a, s); break;
-    case 2: launch_gemv_k<8, false, 2>(K, a, s); break;
-    case 3: launch_gemv_k<8, false, 3>(K, a, s); break;
+    case 0: hipLaunchKernelGGL(k_gemm_q8_mfma<0>, grid, dim3(256), 0, s, a, K); break;
+    case 1: hipLaunchKernelGGL(k_gemm_q8_mfma<1>, grid, dim3(256), 0, s, a, K); break;
+    case 2: hipLaunchKernelGGL(k_gemm_q8_mfma<2>, grid, dim3(256), 0, s, a, K); break;
+    case 3: hipLaunchKernelGGL(k_gemm_q8_mfma<3>, grid, dim3(256), 0, s, a, K); break;
   }
 }
+
+int lm_head_parts(int O, int M) { return M <= 4 ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
 
 // ------------------------------------------------------------------------------------------------
 // q/k RMSNorm per head (attn_q_norm/attn_k_norm) + NEOX RoPE + KV-cache store (fp16).
@@ -595,6 +711,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
   const int g = blockIdx.x % KV, sp = blockIdx.x / KV, m = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int pos = tok_pos[m];
+  const int seq = tok_seq[m];
+  asm volatile("" ::"s"(pos), "s"(seq));  // issue both scalar loads together, ahead of the early-exit branch
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
   const int gps = max(AMIN_G, (n_groups + ASPLIT - 1) / ASPLIT);  // groups per split
@@ -602,8 +720,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
   if (sp >= n_active) return;                                      // uniform over the block
   const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
   STAMP(1);
-  __half* kb = kc + (int64_t)tok_seq[m] * seq_stride + g * D;
-  __half* vb = vc + (int64_t)tok_seq[m] * seq_stride + g * D;
+  __half* kb = kc + (int64_t)seq * seq_stride + g * D;
+  __half* vb = vc + (int64_t)seq * seq_stride + g * D;
   __shared__ float s_q[AWV][GQ][D];          // per-wave q (scaled, roped) in natural dim order
   __shared__ float s_kn[D], s_vn[D];         // fresh K/V row (decode)
   __shared__ float s_ml[AWV][GQ][2];

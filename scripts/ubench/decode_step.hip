@@ -50,33 +50,47 @@ int main(int argc, char** argv) {
   auto G = [&](const int8_t* q, const __half* d, int O, const float* xin, int ldx, const float* nrm, float* o, const float* res) {
     GemvArgs a{}; a.M = 1; a.eps = 1e-6f; a.wq = q; a.wd = d; a.O = O; a.rpw = gemv_rows_per_wave(O);
     a.x = xin; a.ldx = ldx; a.norm_w = nrm; a.out = o; a.ldo = O; a.res = res; a.ldr = O; return a; };
+  int mask = 63;  // 1 qkv, 2 attn, 4 o, 8 gate/up, 16 down, 32 lm_head (ablation: time a subset of the chain)
   auto step = [&]() {
     for (int l = 0; l < L; ++l) {
       auto& w = lw[l];
-      gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
-      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV,
+      if (mask & 1) gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
+      if (mask & 2) attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV,
                  seq, pos, (int64_t)NCTX * KV * D, att, wk, s);
-      gemv_q8(G(w.o, w.dO, E, att, H * D, nullptr, x, x), H * D, 1, s);
-      auto gu = G(w.g, w.dg, F, x, E, nw, act, nullptr); gu.wq2 = w.u; gu.wd2 = w.du; gemv_q8(gu, E, 2, s);
-      gemv_q8(G(w.d, w.dd, E, act, F, nullptr, x, x), F, 1, s);
+      if (mask & 4) gemv_q8(G(w.o, w.dO, E, att, H * D, nullptr, x, x), H * D, 1, s);
+      auto gu = G(w.g, w.dg, F, x, E, nw, act, nullptr); gu.wq2 = w.u; gu.wd2 = w.du;
+      if (mask & 8) gemv_q8(gu, E, 2, s);
+      if (mask & 16) gemv_q8(G(w.d, w.dd, E, act, F, nullptr, x, x), F, 1, s);
     }
     auto h = G(wemb, demb, V, x, E, nw, logits, nullptr); h.pval = pval; h.pidx = pidx;
-    h.n_part = (V + 4 * h.rpw - 1) / (4 * h.rpw) * 4; gemv_q8(h, E, 3, s);
+    h.n_part = (V + 4 * h.rpw - 1) / (4 * h.rpw) * 4;
+    if (mask & 32) gemv_q8(h, E, 3, s);
   };
   const bool eager = argc > 1 && !strcmp(argv[1], "eager");
   const int n = argc > 2 ? atoi(argv[2]) : 3;
   if (eager) { for (int i = 0; i < n; ++i) step(); CK(hipStreamSynchronize(s)); printf("eager %d steps done\n", n); return 0; }
-  hipGraph_t g; hipGraphExec_t ex;
-  CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)); step(); CK(hipStreamEndCapture(s, &g));
-  CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-  for (int i = 0; i < 5; ++i) CK(hipGraphLaunch(ex, s));
-  CK(hipStreamSynchronize(s));
-  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-  const int R = 50;
-  CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
-  CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
   const double bytes = (double)L * (QKV * E + E * H * D + 2.0 * F * E + E * F) * 34 / 32 + (double)V * E * 34 / 32;
-  printf("decode step (graph, 28 layers + lm_head, n_past 330): %.1f us  -> %.1f GB/s of q8_0 weights (%.1f MB)\n",
-         ms * 1e3 / R, bytes / (ms * 1e-3 / R) / 1e9, bytes / 1e6);
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  const char* names[] = {"full step", "qkv x28", "attn x28", "o x28", "gate/up x28", "down x28", "lm_head", "layers w/o attn",
+                         "qkv+attn x28"};
+  const int masks[] = {63, 1, 2, 4, 8, 16, 32, 29, 3};
+  for (int t = 0; t < 9; ++t) {
+    mask = masks[t];
+    hipGraph_t g; hipGraphExec_t ex;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)); step(); CK(hipStreamEndCapture(s, &g));
+    CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+    for (int i = 0; i < 5; ++i) CK(hipGraphLaunch(ex, s));
+    CK(hipStreamSynchronize(s));
+    const int R = 50;
+    CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
+    if (t == 0)
+      printf("decode step (graph, 28 layers + lm_head, n_past 330): %.1f us  -> %.1f GB/s of q8_0 weights (%.1f MB)\n",
+             ms * 1e3 / R, bytes / (ms * 1e-3 / R) / 1e9, bytes / 1e6);
+    else
+      printf("  %-18s %8.1f us  (%.2f us per launch)\n", names[t], ms * 1e3 / R,
+             ms * 1e3 / R / (t == 6 ? 1 : (t == 7 ? 4 * L : (t == 8 ? 2 * L : L))));
+    CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
+  }
   return 0;
 }

@@ -32,7 +32,7 @@ def _rel(a, b):
 @pytest.fixture(scope="module")
 def tiny_engine():
     from fun_asr_gguf import _native
-    eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=512, max_seqs=4), max_batch=4,
+    eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=512, max_seqs=8), max_batch=4,
                          max_samples=16000 * 4)
     eng.synthetic_weights(0)
     yield eng
@@ -175,6 +175,32 @@ def test_llm_long_context_split_attention(tiny_engine, llm_tiny_oracle):
         ref = m.forward(m.embed_tokens([tok]), pos)
         _check_step(lg_new, ref)
         tok, pos = int(nxt), pos + 1
+
+
+def test_llm_batched_decode_mfma_teacher_forced(tiny_engine, llm_tiny_oracle):
+    """6 sequences decode as one M=6 batch: every GEMM (and the lm_head + argmax partials) runs on the int8
+    MFMA path; each row's logits are checked against the oracle run of that sequence alone."""
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(6)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (7, 19, 33, 12, 70, 45)]
+    toks = []
+    for s_, p in enumerate(prompts):
+        tiny_engine.llm_reset(s_)
+        toks.append(tiny_engine.llm_prefill(s_, p))
+    seqs = list(range(len(prompts)))
+    fed = [[t] for t in toks]  # tokens fed so far per sequence (first = the prefill's sampled token)
+    for _ in range(3):
+        nxt = tiny_engine.llm_generate(seqs, 1)[:, 0]
+        for s_, p in enumerate(prompts):
+            lg = tiny_engine.llm_logits(s_)
+            m.reset()
+            m.forward(p, 0)
+            for k, t in enumerate(fed[s_]):
+                ref = m.forward(m.embed_tokens([t]), p.shape[0] + k)
+            _check_step(lg, ref)
+            assert int(nxt[s_]) == int(np.argmax(lg))
+        for s_ in seqs:
+            fed[s_].append(int(nxt[s_]))
 
 
 def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
