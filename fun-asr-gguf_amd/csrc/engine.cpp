@@ -135,6 +135,9 @@ struct Engine {
   int hist_max = 0;
   std::vector<int> n_past, last_tok, logits_row;
   AttnWork attn_wk;
+  float* gk_part = nullptr;  // MFMA GEMM split-K workspace
+  int* gk_cnt = nullptr;
+  int64_t gk_part_n = 0, gk_cnt_n = 0;
 
   // profiling
   bool prof = false;
@@ -524,6 +527,12 @@ struct Engine {
     attn_wk.counters = alloc<int>((size_t)m_max * KV);
     FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
+    // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)
+    gk_cnt_n = 256;
+    gk_part_n = (int64_t)256 * 8 * 2 * 1024;
+    gk_cnt = alloc<int>(gk_cnt_n);
+    FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * sizeof(int)));
+    gk_part = alloc<float>(gk_part_n);
     n_past.assign(lc.max_seqs, 0);
     last_tok.assign(lc.max_seqs, -1);
   }
@@ -808,7 +817,12 @@ struct Engine {
     }
   }
 
-  void gemv(const GemvArgs& a, int K, int epi) {
+  void gemv(const GemvArgs& a0, int K, int epi) {
+    GemvArgs a = a0;
+    a.kpart = gk_part;
+    a.kpart_n = gk_part_n;
+    a.kcnt = gk_cnt;
+    a.kcnt_n = gk_cnt_n;
     hipEvent_t ev;
     prof_begin(0, &ev);
     gemv_q8(a, K, epi, stream);

@@ -50,12 +50,15 @@ struct GemvArgs {
   const float* res; int64_t ldr;
   float* pval; int* pidx; int n_part;      // argmax partials [M][n_part]
   int M, O, rpw;
+  float* kpart; int64_t kpart_n;           // MFMA GEMM split-K workspace (floats) + arrival counters
+  int* kcnt; int64_t kcnt_n;               //   (counters zeroed once; re-armed by the combining block)
 };
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
 int gemv_rows_per_wave(int O);
 // argmax partials per token written by the lm_head launch for M tokens (GEMV for M <= 4, MFMA GEMM above)
 int lm_head_parts(int O, int M);
+int gemm_k_splits(int O, int M, int K);
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
                    int64_t seq_stride, hipStream_t s);

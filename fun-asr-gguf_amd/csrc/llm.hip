@@ -4,6 +4,7 @@
 //   integer dot is exact (v_dot4_i32_i8), scaled by f32(dw)*f32(dx) and summed in f32.
 // The decode GEMV streams every weight byte exactly once per step for the whole continuous batch
 // (HBM-bound: 633 MB/step for Qwen3-0.6B q8_0); one wave covers a K=1024 row with ONE 16 B/lane load.
+#include <algorithm>
 #include <type_traits>
 #include "common.h"
 #include "kernels.h"
@@ -324,89 +325,118 @@ static void launch_gemv_k(int K, const GemvArgs& a, hipStream_t s) {
 typedef int i32x16_t __attribute__((ext_vector_type(16)));
 
 template <int EPI>
-__global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K) {
-  constexpr int NG = EPI == 2 ? 4 : 8;  // q8_0 blocks per load group (gate+up: half, to stay in registers)
-  typedef typename std::conditional<NG == 8, uint4, uint2>::type ScaleVec;  // NG fp16 scales of one row
-  const int nb = K >> 5, nbw = nb >> 2;
+__global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS) {
+  constexpr int NG = 4;  // q8_0 blocks per load group
+  const int nb = K >> 5, nbk = nb / KS;  // blocks per K split
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
+  const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32, ks = blockIdx.z;
+  // SwiGLU: waves 0-1 take the gate matrix, 2-3 the up matrix (one accumulator set per wave);
+  // otherwise the 4 waves take K quarters
+  const bool upw = EPI == 2 && wave >= 2;
+  const int nbw = EPI == 2 ? nbk >> 1 : nbk >> 2;
+  const int bw0 = ks * nbk + (EPI == 2 ? (wave & 1) : wave) * nbw;
+  const int8_t* wq = upw ? a.wq2 : a.wq;
+  const __half* wd = upw ? a.wd2 : a.wd;
   const int o_a = min(o0 + r, a.O - 1);
   const int t_b = min(t0 + r, a.M - 1);
-  const int8_t* wa = a.wq + (int64_t)o_a * K + 16 * h;
-  const int8_t* wu = EPI == 2 ? a.wq2 + (int64_t)o_a * K + 16 * h : nullptr;
+  const int8_t* wa = wq + (int64_t)o_a * K + 16 * h;
   const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h;
   const float* xd = a.xd + (int64_t)t_b * nb;
-  int orow[16];
+  float acc[16];
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) orow[reg] = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
-  float acc[16], accu[16];
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) acc[reg] = accu[reg] = 0.f;
+  for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
   const i32x16_t zero = {};
-  for (int b0 = wave * nbw; b0 < (wave + 1) * nbw; b0 += NG) {
-    i32x4_t A[NG], U[NG], B[NG];
+  for (int b0 = bw0; b0 < bw0 + nbw; b0 += NG) {
+    i32x4_t A[NG], B[NG];
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
+#ifdef FA_GEMM_NT_LOADS
       A[j] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(wa + (b0 + j) * 32));
-      if (EPI == 2) U[j] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(wu + (b0 + j) * 32));
+#else
+      A[j] = *reinterpret_cast<const i32x4_t*>(wa + (b0 + j) * 32);
+#endif
       B[j] = *reinterpret_cast<const i32x4_t*>(xb + (b0 + j) * 32);
     }
-    ScaleVec dw[16], du[16];
+    uint2 dw[16];  // NG fp16 scales of each of this lane's 16 rows
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      dw[reg] = *reinterpret_cast<const ScaleVec*>(a.wd + (int64_t)orow[reg] * nb + b0);
-      if (EPI == 2) du[reg] = *reinterpret_cast<const ScaleVec*>(a.wd2 + (int64_t)orow[reg] * nb + b0);
+      const int row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
+      dw[reg] = *reinterpret_cast<const uint2*>(wd + (int64_t)row * nb + b0);
     }
-    float dx[NG];
-#pragma unroll
-    for (int j = 0; j < NG; j += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(xd + b0 + j);
-      dx[j] = v.x; dx[j + 1] = v.y; dx[j + 2] = v.z; dx[j + 3] = v.w;
-    }
+    const float4 dx4 = *reinterpret_cast<const float4*>(xd + b0);
+    const float dx[NG] = {dx4.x, dx4.y, dx4.z, dx4.w};
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
       const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
-      i32x16_t DU;
-      if (EPI == 2) DU = __builtin_amdgcn_mfma_i32_32x32x32_i8(U[j], B[j], zero, 0, 0, 0);
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const __half* hw = reinterpret_cast<const __half*>(&dw[reg]);
         acc[reg] += (float)D[reg] * (__half2float(hw[j]) * dx[j]);
-        if (EPI == 2) {
-          const __half* hu = reinterpret_cast<const __half*>(&du[reg]);
-          accu[reg] += (float)DU[reg] * (__half2float(hu[j]) * dx[j]);
-        }
       }
     }
   }
-  // fixed-order reduction of the 4 K-quarters; thread t finalises regs [4 (t>>6), +4) of lane t&63
-  constexpr int NS = EPI == 2 ? 2 : 1;
-  __shared__ float s_red[NS][4][16][64];
+  // fixed-order reduction over the waves; thread t finalises regs [4 (t>>6), +4) of lane t&63
+  __shared__ float s_red[4][16][64];
   __shared__ float s_out[32][33];  // EPI 3: [token][row] for the per-token argmax
+  __shared__ int s_last;
+  constexpr int NS = EPI == 2 ? 2 : 1;
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    s_red[0][wave][reg][lane] = acc[reg];
-    if (EPI == 2) s_red[NS - 1][wave][reg][lane] = accu[reg];
-  }
+  for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
   __syncthreads();
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  float y[4], y2[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int reg = 4 * g + q;
+    if (EPI == 2) {
+      y[q] = s_red[0][reg][l] + s_red[1][reg][l];
+      y2[q] = s_red[2][reg][l] + s_red[3][reg][l];
+    } else {
+      y[q] = ((s_red[0][reg][l] + s_red[1][reg][l]) + s_red[2][reg][l]) + s_red[3][reg][l];
+      y2[q] = 0.f;
+    }
+  }
+  if (KS > 1) {
+    // split-K: publish this split's tile (sc1), count arrivals; the last split sums all KS tiles in
+    // split order (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int SC1 = 16;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    float* base = a.kpart + (int64_t)tile * KS * (NS * 1024);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, KS * NS * 1024 * 4, 0x00020000);
+    const f4v v = {y[0], y[1], y[2], y[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4, 0, SC1);
+    if (EPI == 2) {
+      const f4v v2 = {y2[0], y2[1], y2[2], y2[3]};
+      __builtin_amdgcn_raw_buffer_store_b128(v2, rs, (ks * NS * 1024 + 1024 + threadIdx.x * 4) * 4, 0, SC1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(a.kcnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+    __syncthreads();
+    if (!s_last) return;
+    f4v sum = {0.f, 0.f, 0.f, 0.f}, sum2 = {0.f, 0.f, 0.f, 0.f};
+    for (int k2 = 0; k2 < KS; ++k2) {
+      sum += __builtin_amdgcn_raw_buffer_load_b128(rs, (k2 * NS * 1024 + threadIdx.x * 4) * 4, 0, SC1);
+      if (EPI == 2) sum2 += __builtin_amdgcn_raw_buffer_load_b128(rs, (k2 * NS * 1024 + 1024 + threadIdx.x * 4) * 4, 0, SC1);
+    }
+    y[0] = sum.x; y[1] = sum.y; y[2] = sum.z; y[3] = sum.w;
+    y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
+    if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int col = l & 31, tok = t0 + col;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int reg = 4 * g + q;
     const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
     const int row = o0 + rrow;
-    const float y = ((s_red[0][0][reg][l] + s_red[0][1][reg][l]) + s_red[0][2][reg][l]) + s_red[0][3][reg][l];
-    if (EPI == 3) s_out[col][rrow] = row < a.O ? y : -INFINITY;
+    if (EPI == 3) s_out[col][rrow] = row < a.O ? y[q] : -INFINITY;
     if (row < a.O && tok < a.M) {
       float* op = a.out + (int64_t)tok * a.ldo + row;
-      if (EPI == 0 || EPI == 3) *op = y;
-      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y;
-      else {
-        const float y2 =
-            ((s_red[NS - 1][0][reg][l] + s_red[NS - 1][1][reg][l]) + s_red[NS - 1][2][reg][l]) + s_red[NS - 1][3][reg][l];
-        *op = (y / (1.0f + expf(-y))) * y2;
-      }
+      if (EPI == 0 || EPI == 3) *op = y[q];
+      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y[q];
+      else *op = (y[q] / (1.0f + expf(-y[q]))) * y2[q];
     }
   }
   if (EPI == 3) {
@@ -419,6 +449,17 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K) {
       a.pidx[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bi;
     }
   }
+}
+
+// K splits for the MFMA GEMM: enough blocks to cover the chip when the tile count is small, keeping
+// (K/32)/KS/4 a multiple of the 4-block load group. Split-K needs the a.kpart/a.kcnt workspace.
+int gemm_k_splits(int O, int M, int K) {
+  const int tiles = cdiv(O, 32) * cdiv(M, 32);
+  const int nb = K / 32;
+  int ks = 1;
+  for (int c : {2, 3, 4, 6, 8})
+    if (tiles * ks < 256 && nb % (16 * c) == 0 && tiles * c <= 1024) ks = c;
+  return ks;
 }
 
 int gemv_rows_per_wave(int O) {
@@ -445,12 +486,17 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
-  dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32));
+  int KS = (a.kpart && a.kcnt && epi != 3) ? gemm_k_splits(a.O, a.M, K) : 1;
+  if (KS > 1)
+    FA_REQUIRE((int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) <= a.kcnt_n &&
+                   (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) * KS * (epi == 2 ? 2 : 1) * 1024 <= a.kpart_n,
+               "gemm_q8: split-K workspace too small");
+  dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
   switch (epi) {
-    case 0: hipLaunchKernelGGL(k_gemm_q8_mfma<0>, grid, dim3(256), 0, s, a, K); break;
-    case 1: hipLaunchKernelGGL(k_gemm_q8_mfma<1>, grid, dim3(256), 0, s, a, K); break;
-    case 2: hipLaunchKernelGGL(k_gemm_q8_mfma<2>, grid, dim3(256), 0, s, a, K); break;
-    case 3: hipLaunchKernelGGL(k_gemm_q8_mfma<3>, grid, dim3(256), 0, s, a, K); break;
+    case 0: hipLaunchKernelGGL(k_gemm_q8_mfma<0>, grid, dim3(256), 0, s, a, K, KS); break;
+    case 1: hipLaunchKernelGGL(k_gemm_q8_mfma<1>, grid, dim3(256), 0, s, a, K, KS); break;
+    case 2: hipLaunchKernelGGL(k_gemm_q8_mfma<2>, grid, dim3(256), 0, s, a, K, KS); break;
+    case 3: hipLaunchKernelGGL(k_gemm_q8_mfma<3>, grid, dim3(256), 0, s, a, K, KS); break;
   }
 }
 
@@ -705,7 +751,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
                                                          __half* __restrict__ vc, int H, int KV,
                                                          const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
                                                          int64_t seq_stride, float scale, float* __restrict__ out,
-                                                         int* __restrict__ counters, float* __restrict__ partials) {
+                                                         int* __restrict__ counters, float* __restrict__ partials,
+                                                         int nsplit) {
   constexpr int D = 128;
   STAMP(0);
   const int g = blockIdx.x % KV, sp = blockIdx.x / KV, m = blockIdx.y;
@@ -715,7 +762,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
   asm volatile("" ::"s"(pos), "s"(seq));  // issue both scalar loads together, ahead of the early-exit branch
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
-  const int gps = max(AMIN_G, (n_groups + ASPLIT - 1) / ASPLIT);  // groups per split
+  const int gps = max(AMIN_G, (n_groups + nsplit - 1) / nsplit);  // groups per split
   const int n_active = (n_groups + gps - 1) / gps;
   if (sp >= n_active) return;                                      // uniform over the block
   const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
@@ -875,8 +922,10 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
-  hipLaunchKernelGGL(k_attn_block, dim3(KV * ASPLIT, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos,
-                     rsin, kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out, wk.counters, wk.partials);
+  // key splits only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1, 4 at batch 32
+  const int nsplit = std::max(1, std::min(ASPLIT, 1024 / std::max(1, M * KV)));
+  hipLaunchKernelGGL(k_attn_block, dim3(KV * nsplit, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos,
+                     rsin, kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out, wk.counters, wk.partials, nsplit);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -86,5 +86,52 @@ int main() {
   { auto a = G(wemb, demb, V, x, nw, out, nullptr); a.ldx = E; a.pval = pval; a.pidx = pidx;
     a.n_part = (V + 4 * a.rpw - 1) / (4 * a.rpw) * 4;
     time_graph("lm_head 151936x1024 (argmax)", [&] { gemv_q8(a, E, 3, s); }, 50, (double)V * E * 34.0 / 32); }
+  // ---- continuous batch (M tokens, pre-quantised activations -> int8 MFMA GEMM) and prefill shapes
+  for (int M : {32, 204}) {
+    int8_t* xq = dalloc<int8_t>((size_t)M * F); float* xd = dalloc<float>((size_t)M * F / 32);
+    float* xs = dalloc<float>((size_t)M * F); launch_synth_fill(xs, (int64_t)M * F, 21, 1.f, 0.f, s);
+    float* ob = dalloc<float>((size_t)M * QKV);
+    prep_q8(xs, F, nullptr, 0.f, M, F, xq, xd, s);
+    CK(hipStreamSynchronize(s));
+    char nm[96];
+    snprintf(nm, sizeof nm, "M=%d prep_q8 K=1024 (norm)", M);
+    time_graph(nm, [&] { prep_q8(xs, E, nw, 1e-6f, M, E, xq, xd, s); });
+    int* kc_ = dalloc<int>(256); CK(hipMemset(kc_, 0, 1024));
+    float* kp_ = dalloc<float>(256 * 8 * 2 * 1024);
+    auto B = [&](const int8_t* q, const __half* d, int O) {
+      GemvArgs a{}; a.M = M; a.eps = 1e-6f; a.wq = q; a.wd = d; a.O = O; a.xq = xq; a.xd = xd; a.out = ob; a.ldo = O;
+      a.res = ob; a.ldr = O; a.kpart = kp_; a.kpart_n = 256 * 8 * 2 * 1024; a.kcnt = kc_; a.kcnt_n = 256; return a; };
+    double t = 0;
+    { auto a = B(wqkv, dqkv, QKV); snprintf(nm, sizeof nm, "M=%d gemm qkv 4096x1024", M);
+      t += time_graph(nm, [&] { gemv_q8(a, E, 0, s); }, 200, QKV * E * 34.0 / 32); }
+    { auto a = B(wo, dO, E); snprintf(nm, sizeof nm, "M=%d gemm o 1024x2048 (+res)", M);
+      t += time_graph(nm, [&] { gemv_q8(a, H * D, 1, s); }, 200, E * H * D * 34.0 / 32); }
+    { auto a = B(wg, dg, F); a.wq2 = wu; a.wd2 = du; snprintf(nm, sizeof nm, "M=%d gemm gate|up (swiglu)", M);
+      t += time_graph(nm, [&] { gemv_q8(a, E, 2, s); }, 200, 2.0 * F * E * 34.0 / 32); }
+    { auto a = B(wd, dd, E); snprintf(nm, sizeof nm, "M=%d gemm down 1024x3072 (+res)", M);
+      t += time_graph(nm, [&] { gemv_q8(a, F, 1, s); }, 200, E * F * 34.0 / 32); }
+    printf("%-34s %8.2f us\n", "  gemm sum", t);
+    { float* lg = dalloc<float>((size_t)M * V); float* pv = dalloc<float>((size_t)M * 4800); int* pi = dalloc<int>((size_t)M * 4800);
+      auto a = B(wemb, demb, V); a.out = lg; a.ldo = V; a.pval = pv; a.pidx = pi; a.n_part = lm_head_parts(V, M);
+      snprintf(nm, sizeof nm, "M=%d lm_head (argmax)", M);
+      time_graph(nm, [&] { gemv_q8(a, E, 3, s); }, 20, (double)V * E * 34.0 / 32);
+      CK(hipFree(lg)); CK(hipFree(pv)); CK(hipFree(pi)); }
+    CK(hipFree(xq)); CK(hipFree(xd)); CK(hipFree(xs)); CK(hipFree(ob));
+  }
+  {  // batch-32 decode attention: 32 sequences at n_past 330
+    const int M = 32;
+    AttnWork wb; wb.max_tokens = M; wb.max_kv = 8;
+    CK(hipMalloc(&wb.counters, M * 8 * 4)); CK(hipMemset(wb.counters, 0, M * 8 * 4));
+    CK(hipMalloc(&wb.partials, (size_t)M * 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
+    __half* kb = dalloc<__half>((size_t)M * NCTX * KV * D); __half* vb = dalloc<__half>((size_t)M * NCTX * KV * D);
+    CK(hipMemset(kb, 0, (size_t)M * NCTX * KV * D * 2)); CK(hipMemset(vb, 0, (size_t)M * NCTX * KV * D * 2));
+    float* qb = dalloc<float>((size_t)M * QKV); launch_synth_fill(qb, (int64_t)M * QKV, 22, 1.f, 0.f, s);
+    float* ab = dalloc<float>((size_t)M * H * D);
+    int hs[M], hp[M]; for (int i = 0; i < M; ++i) { hs[i] = i; hp[i] = 330; }
+    int* ds = dalloc<int>(M); int* dp = dalloc<int>(M);
+    CK(hipMemcpy(ds, hs, sizeof hs, hipMemcpyHostToDevice)); CK(hipMemcpy(dp, hp, sizeof hp, hipMemcpyHostToDevice));
+    time_graph("M=32 attn_block decode n_past=330", [&] {
+      attn_block(qb, 1, qn, qn, 1e-6f, rc, rs, kb, vb, M, H, KV, ds, dp, (int64_t)NCTX * KV * D, ab, wb, s); });
+  }
   return 0;
 }
