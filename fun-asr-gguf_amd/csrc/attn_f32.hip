@@ -2,44 +2,109 @@
 // per head, full-length (non-causal) with the reference's additive key mask (m-1)*1e4
 // (model_definition.py:68-78, 122-145). Exact-f32 MFMA (v_mfma_f32_32x32x2_f32), flash-style:
 //
-//   block = (32-query tile, head, clip); 4 waves split the key tiles (w, w+4, ...), each keeps its own
-//   online-softmax state; partial (m, l, O) are merged through LDS at the end.
-//   S^T = K . Q^T so the query index sits on the lane (col) and keys on the 16 accumulator registers:
-//   the per-query max/sum is an in-register reduction + one cross-half shuffle, and S^T is directly the
-//   B operand of O^T += V^T . P^T (key order permuted consistently on both operands).
-// Q/K fragments: lane (r=l&31, h=l>>5) holds row r, dims [h*D/2, h*D/2+D/2) — the dot-product index is
-// permuted identically on A and B, so each lane loads D/2 contiguous floats (float4s).
+//   block = (128-query tile, head, clip, key split); its 4 waves own 32 queries each and share the K/V
+//   stream: 32-key tiles are staged through LDS (double-buffered, one barrier per tile), so each K/V byte
+//   read from L2 feeds 128 queries. S^T = K . Q^T puts the query on the lane (col) and keys on the 16
+//   accumulator registers: the per-query max/sum is an in-register reduction + one cross-half swap, and
+//   P^T is directly the B operand of O^T += V^T . P^T.
+//   Q/K fragments: lane (r = l&31, h = l>>5) holds row r, dims [h*D/2, h*D/2 + D/2): the dot index is
+//   permuted identically on A and B.
+//   Key splits (single clip: too few (query tile, head) blocks to cover 256 CUs): each split stores its
+//   (m, l, O) with sc1 stores and counts arrivals; the last split merges them in split order
+//   (MI355X_MICROARCH.md hand-off table, row 1).
 #include "common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cmath>
 
 namespace fa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int AQ = 128;  // queries per block (4 waves x 32)
+constexpr int AK = 32;   // keys per tile
+
+template <int D>
+struct AttnLds {
+  static constexpr int S = D + 8;                    // row stride (floats): S % 16 == 8 -> conflict-free reads
+  static constexpr int TILE = AK * S;                // one K or V tile
+  static constexpr int BYTES_PIPE = 4 * TILE * 4;    // K, V x 2 stages
+  static constexpr int OS = D + 4;                   // output transpose stride
+  static constexpr int BYTES_OUT = AQ * OS * 4;
+  static constexpr int BYTES = (BYTES_PIPE > BYTES_OUT ? BYTES_PIPE : BYTES_OUT) + 2 * AQ * 4 + 16;
+};
+
+// global -> register staging of one K/V tile: float4 f = tid + 256 c -> key f / (D/4), dim4 f % (D/4)
+// (row-contiguous, coalesced); keys past the clip are clamped (masked to -inf in the scores)
+template <int D>
+__device__ __forceinline__ void attn_load_tile(const float* __restrict__ Kp, const float* __restrict__ V, int64_t ldk,
+                                               int64_t ldv, int64_t row_base, int head, int t_stride, int kt,
+                                               f4v (&pk)[AK * D / 1024], f4v (&pv)[AK * D / 1024]) {
+#pragma unroll
+  for (int c = 0; c < AK * D / 1024; ++c) {
+    const int f = threadIdx.x + 256 * c;
+    const int key = min(kt * AK + f / (D / 4), t_stride - 1);
+    const int d4 = f % (D / 4);
+    pk[c] = *reinterpret_cast<const f4v*>(Kp + (row_base + key) * ldk + head * D + 4 * d4);
+    pv[c] = *reinterpret_cast<const f4v*>(V + (row_base + key) * ldv + head * D + 4 * d4);
+  }
+}
+template <int D>
+__device__ __forceinline__ void attn_store_tile(float* lds, int stage, const f4v (&pk)[AK * D / 1024],
+                                                const f4v (&pv)[AK * D / 1024]) {
+  using L = AttnLds<D>;
+  float* ks_ = lds + stage * 2 * L::TILE;
+  float* vs_ = ks_ + L::TILE;
+#pragma unroll
+  for (int c = 0; c < AK * D / 1024; ++c) {
+    const int f = threadIdx.x + 256 * c;
+    const int key = f / (D / 4), d4 = f % (D / 4);
+    *reinterpret_cast<f4v*>(ks_ + key * L::S + 4 * d4) = pk[c];
+    *reinterpret_cast<f4v*>(vs_ + key * L::S + 4 * d4) = pv[c];
+  }
+}
 
 template <int D>
 __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
-                                                  const int* __restrict__ lens, float scale) {
-  constexpr int HD = D / 2;     // dims per lane half
-  constexpr int NDT = D / 32;   // output d-tiles
+                                                  const int* __restrict__ lens, float scale, int KS,
+                                                  float* __restrict__ part, int* __restrict__ cnt) {
+  using L = AttnLds<D>;
+  constexpr int HD = D / 2;    // dims per lane half
+  constexpr int NDT = D / 32;  // output d-tiles
+  constexpr int F4 = AK * D / 4 / 256;  // float4 per thread per tile (K or V)
   extern __shared__ float lds[];
-  const int qt = blockIdx.x, head = blockIdx.y, clip = blockIdx.z;
+  float* s_m = lds + (L::BYTES - 2 * AQ * 4 - 16) / 4;  // [AQ] merged row max / sum (split path)
+  float* s_l = s_m + AQ;
+  int* s_flag = reinterpret_cast<int*>(s_l + AQ);
+
+  const int n_qt = (t_stride + AQ - 1) / AQ;
+  // splits of one (query tile, head, clip) sit 8*k block ids apart: the dispatcher deals blocks round-robin
+  // over the 8 XCDs, so they usually share one XCD's L2 with the merging block (speed only: the sc1
+  // hand-off is correct at any placement). grid.x = KS * n_qt8, n_qt8 % 8 == 0
+  const int n_qt8 = (n_qt + 7) & ~7;
+  const int qt = blockIdx.x % n_qt8, ks = blockIdx.x / n_qt8, head = blockIdx.y, clip = blockIdx.z;
+  if (qt >= n_qt) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int64_t row_base = (int64_t)clip * t_stride;
   const int len = lens ? lens[clip] : t_stride;
-  const int q0 = qt * 32;
+  const int q0 = qt * AQ;
+  const int n_kt = (t_stride + AK - 1) / AK;
+  const int tpk = (n_kt + KS - 1) / KS;
+  const int kt0 = ks * tpk, kt1 = min(n_kt, kt0 + tpk);
 
+  // this wave's 32 queries, pre-scaled (python: q * d_k**-0.5 before the dot)
   float qreg[HD];
   {
-    int q = q0 + r;
+    const int q = min(q0 + wave * 32 + r, t_stride - 1);
     const float* p = Q + (row_base + q) * ldq + head * D + h * HD;
 #pragma unroll
     for (int s = 0; s < HD; s += 4) {
-      float4 v = q < t_stride ? *reinterpret_cast<const float4*>(p + s) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = *reinterpret_cast<const float4*>(p + s);
       qreg[s] = v.x * scale;
       qreg[s + 1] = v.y * scale;
       qreg[s + 2] = v.z * scale;
@@ -50,35 +115,33 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
 #pragma unroll
   for (int i = 0; i < NDT; ++i) o[i] = f32x16{};
   float m_run = -INFINITY, l_run = 0.f;
-
-  const int n_kt = (t_stride + 31) / 32;
-  for (int kt = wave; kt < n_kt; kt += 4) {
-    const int k0 = kt * 32;
+  f4v pk[F4], pv[F4];  // register staging of the next K/V tile
+  if (kt0 < kt1) {
+    attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt0, pk, pv);
+    attn_store_tile<D>(lds, 0, pk, pv);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int stage = (kt - kt0) & 1;
+    if (kt + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 1, pk, pv);  // in flight
+    const float* ks_ = lds + stage * 2 * L::TILE;
+    const float* vs_ = ks_ + L::TILE;
+    const int k0 = kt * AK;
+    // S^T[key][q] = sum_d K[key][d] Q[q][d]
     f32x16 s = {};
-    {
-      int key = k0 + r;
-      const float* p = Kp + (row_base + key) * ldk + head * D + h * HD;
-      bool ok = key < t_stride;
 #pragma unroll
-      for (int c = 0; c < HD; c += 16) {
-        float kr[16];
-#pragma unroll
-        for (int e = 0; e < 16; e += 4) {
-          float4 v = ok ? *reinterpret_cast<const float4*>(p + c + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-          kr[e] = v.x;
-          kr[e + 1] = v.y;
-          kr[e + 2] = v.z;
-          kr[e + 3] = v.w;
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[e], qreg[c + e], s, 0, 0, 0);
-      }
+    for (int c = 0; c < HD; c += 4) {
+      const float4 kv = *reinterpret_cast<const float4*>(ks_ + r * L::S + h * HD + c);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qreg[c], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qreg[c + 1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qreg[c + 2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qreg[c + 3], s, 0, 0, 0);
     }
-    // mask + online softmax (per query = per lane column)
+    // mask + online softmax (per query = per lane column; keys on registers and lane halves)
     float mt = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
+      const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
       float v = s[t];
       if (key >= t_stride) v = -INFINITY;
       else if (key >= len) v = v + -10000.0f;
@@ -86,12 +149,12 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
       mt = fmaxf(mt, v);
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    float m_new = fmaxf(m_run, mt);
-    float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
+      const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
       s[t] = p;
       ls += p;
     }
@@ -100,75 +163,135 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
     m_run = m_new;
 #pragma unroll
     for (int i = 0; i < NDT; ++i) o[i] *= alpha;
-    // O^T[d][q] += sum_key V[key][d] * P^T[key][q]
+    // O^T[d][q] += sum_key V[key][d] P^T[key][q]
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
-      const float* vp = V + (row_base + key) * ldv + head * D + r;
-      bool ok = key < t_stride;
+      const int kl = (t & 3) + 8 * (t >> 2) + 4 * h;
 #pragma unroll
-      for (int i = 0; i < NDT; ++i) {
-        float vv = ok ? vp[i * 32] : 0.f;
-        o[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(vv, s[t], o[i], 0, 0, 0);
-      }
+      for (int i = 0; i < NDT; ++i)
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(vs_[kl * L::S + i * 32 + r], s[t], o[i], 0, 0, 0);
     }
+    if (kt + 1 < kt1) attn_store_tile<D>(lds, stage ^ 1, pk, pv);
+    __syncthreads();
   }
-  // ---- merge the 4 waves' partial states through LDS
-  float* sm = lds;                   // [4][32]
-  float* sl = lds + 128;             // [4][32]
-  float* so = lds + 256;             // [4][D][32]
-  if (h == 0) {
-    sm[wave * 32 + r] = m_run;
-    sl[wave * 32 + r] = l_run;
-  }
+
+  // ---- O^T (d on registers, q on lanes) -> LDS [q][d] for row-contiguous stores
+  float* so = lds;
 #pragma unroll
   for (int i = 0; i < NDT; ++i)
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      int d = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h;
-      so[(wave * D + d) * 32 + r] = o[i][t];
+      const int d = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h;
+      so[(wave * 32 + r) * L::OS + d] = o[i][t];
     }
+  if (h == 0) {
+    s_m[wave * 32 + r] = m_run;
+    s_l[wave * 32 + r] = l_run;
+  }
   __syncthreads();
-  // 256 threads: thread -> query q = tid & 31, d group
-  const int q = threadIdx.x & 31;
-  float M = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 32 + q]);
-  float wsc[4], L = 0.f;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    float mw = sm[w * 32 + q];
-    wsc[w] = mw == -INFINITY ? 0.f : __expf(mw - M);
-    L += wsc[w] * sl[w * 32 + q];
-  }
-  const float inv = 1.0f / L;
-  const int qrow = q0 + q;
-  if (qrow < t_stride) {
-    float* op = O + (row_base + qrow) * ldo + head * D;
-    for (int d = threadIdx.x >> 5; d < D; d += 8) {
-      float acc = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) acc += wsc[w] * so[(w * D + d) * 32 + q];
-      op[d] = acc * inv;
+  constexpr int D4 = D / 4;
+  if (KS == 1) {
+    for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+      const int q = f / D4, d4 = f % D4;
+      if (q0 + q < t_stride) {
+        const float inv = 1.0f / s_l[q];
+        float4 v = *reinterpret_cast<const float4*>(so + q * L::OS + 4 * d4);
+        v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+        *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+      }
     }
+    return;
   }
+  // ---- key split: publish (m, l, O) of this split; the last split merges
+  constexpr int PSZ = AQ * D + 2 * AQ;  // floats per split partial
+  const int tile = (clip * gridDim.y + head) * n_qt + qt;
+  float* pbase = part + (int64_t)tile * KS * PSZ;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, KS * PSZ * 4);
+  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+    const int q = f / D4, d4 = f % D4;
+    const f4v v = *reinterpret_cast<const f4v*>(so + q * L::OS + 4 * d4);
+    st_sc1_f4(v, rs, (ks * PSZ + q * D + 4 * d4) * 4);
+  }
+  if (threadIdx.x < AQ / 2) {
+    const int q = threadIdx.x * 2;
+    const f4v v = {s_m[q], s_l[q], s_m[q + 1], s_l[q + 1]};
+    st_sc1_f4(v, rs, (ks * PSZ + AQ * D + 2 * q) * 4);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *s_flag = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+  __syncthreads();
+  if (!*s_flag) return;
+  // merged max / sum per query, then the weighted sum of the splits' O
+  if (threadIdx.x < AQ) {
+    const int q = threadIdx.x;
+    float mm = -INFINITY;
+    for (int k2 = 0; k2 < KS; ++k2) {
+      const f4v v = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
+      mm = fmaxf(mm, (q & 1) ? v.z : v.x);
+    }
+    float ll = 0.f;
+    for (int k2 = 0; k2 < KS; ++k2) {
+      const f4v v = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
+      const float mk = (q & 1) ? v.z : v.x, lk = (q & 1) ? v.w : v.y;
+      ll += mk == -INFINITY ? 0.f : __expf(mk - mm) * lk;
+    }
+    s_m[q] = mm;
+    s_l[q] = ll;
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+    const int q = f / D4, d4 = f % D4;
+    if (q0 + q >= t_stride) continue;
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k2 = 0; k2 < KS; ++k2) {
+      const f4v ml = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
+      const float mk = (q & 1) ? ml.z : ml.x;
+      const float w = mk == -INFINITY ? 0.f : __expf(mk - s_m[q]);
+      acc += w * ld_sc1_f4(rs, (k2 * PSZ + q * D + 4 * d4) * 4);
+    }
+    const float inv = 1.0f / s_l[q];
+    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) =
+        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
+
+int attn_f32_splits(int batch, int t_stride, int n_heads) {
+  if (g_attn_f32_force_splits > 0) return g_attn_f32_force_splits;
+  const int blocks = cdiv(t_stride, AQ) * n_heads * batch;
+  const int n_kt = cdiv(t_stride, AK);
+  int ks = 1;
+  while (blocks * ks * 2 <= 512 && ks * 2 <= 8 && n_kt >= ks * 2 * 2) ks *= 2;
+  return ks;
 }
 
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
-              int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens, hipStream_t s) {
-  dim3 grid(cdiv(t_stride, 32), n_heads, batch);
+              int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
+              const AttnF32Work& wk, hipStream_t s) {
+  const int KS = attn_f32_splits(batch, t_stride, n_heads);
+  const int n_tiles = cdiv(t_stride, AQ) * n_heads * batch;
+  if (KS > 1)
+    FA_REQUIRE(wk.part && wk.cnt && n_tiles <= wk.cnt_n &&
+                   (int64_t)n_tiles * KS * (AQ * head_dim + 2 * AQ) <= wk.part_n,
+               "attn_f32: split workspace too small");
+  dim3 grid(KS == 1 ? cdiv(t_stride, AQ) : ((cdiv(t_stride, AQ) + 7) & ~7) * KS, n_heads, batch);
   const float scale = (float)std::pow((double)head_dim, -0.5);  // python d_k ** -0.5 rounded to f32
-  size_t lds = (256 + 4 * head_dim * 32) * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 1024);
-    hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 1024);
+    hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<128>::BYTES);
+    hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<64>::BYTES);
     attr_set = true;
   }
   if (head_dim == 128) {
-    hipLaunchKernelGGL(k_attn_f32<128>, grid, dim3(256), lds, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale);
+    hipLaunchKernelGGL(k_attn_f32<128>, grid, dim3(256), AttnLds<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                       t_stride, lens, scale, KS, wk.part, wk.cnt);
   } else if (head_dim == 64) {
-    hipLaunchKernelGGL(k_attn_f32<64>, grid, dim3(256), lds, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale);
+    hipLaunchKernelGGL(k_attn_f32<64>, grid, dim3(256), AttnLds<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                       t_stride, lens, scale, KS, wk.part, wk.cnt);
   } else {
     FA_REQUIRE(false, "attn_f32: head_dim must be 64 or 128");
   }

@@ -88,6 +88,22 @@ __device__ __forceinline__ int wave_sum_i(int v) {
          (__builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48));
 }
 
+// 16-B loads/stores with the sc1 cache policy (bypass the CU's L1) through a raw buffer resource, for
+// cross-workgroup hand-offs (MI355X_MICROARCH.md hand-off table, row 1). The builtins traffic in int
+// vectors: always bit-cast explicitly (an implicit scalar*int-vector promotes the scalar to int).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x4v_t __attribute__((ext_vector_type(4)));
+constexpr int CPOL_SC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4_t ld_sc1_f4(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, CPOL_SC1));
+}
+__device__ __forceinline__ void st_sc1_f4(f32x4_t v, __amdgpu_buffer_rsrc_t rs, int byte_off) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v_t, v), rs, byte_off, 0, CPOL_SC1);
+}
+
 // (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).
 __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i) || (v != v)) {

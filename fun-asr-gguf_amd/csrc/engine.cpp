@@ -135,6 +135,7 @@ struct Engine {
   int hist_max = 0;
   std::vector<int> n_past, last_tok, logits_row;
   AttnWork attn_wk;
+  AttnF32Work enc_attn_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
   int* gk_cnt = nullptr;
   int64_t gk_part_n = 0, gk_cnt_n = 0;
@@ -472,6 +473,11 @@ struct Engine {
     xp = alloc<float>((size_t)max_batch * xp_stride_max);
     mean_part = alloc<float>((size_t)max_batch * 64);
     power = alloc<float>((size_t)max_batch * tm_max * 204);
+    enc_attn_wk.part_n = ATTN_F32_PART_FLOATS;
+    enc_attn_wk.part = alloc<float>(enc_attn_wk.part_n);
+    enc_attn_wk.cnt_n = ATTN_F32_COUNTERS;
+    enc_attn_wk.cnt = alloc<int>(enc_attn_wk.cnt_n);
+    FA_HIP(hipMemset(enc_attn_wk.cnt, 0, enc_attn_wk.cnt_n * sizeof(int)));
     mel = alloc<float>((size_t)max_batch * tm_max * ec.n_mels);
     const int wmax = std::max({ec.d_in, ec.d_llm, d});
     xa = alloc<float>((size_t)R * wmax);
@@ -595,7 +601,7 @@ struct Engine {
       hipEvent_t ev;
       prof_begin(2, &ev);
       attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.n_heads, d / ec.n_heads, lens,
-               stream);
+               enc_attn_wk, stream);
       prof_end(2, 0, 4.0 * rows * (double)ts * d);
     }
     if (first) {
@@ -620,7 +626,7 @@ struct Engine {
         hipEvent_t ev;
         prof_begin(2, &ev);
         attn_f32(qkv, qkv + d_out, qkv + 2 * d_out, 3 * d_out, 3 * d_out, 3 * d_out, att, d_out, rows / ts, ts, n_heads,
-                 d_out / n_heads, lens, stream);
+                 d_out / n_heads, lens, enc_attn_wk, stream);
         prof_end(2, 0, 4.0 * rows * (double)ts * d_out);
       }
       enc_lin(att, d_out, b.o_w, b.o_b, out, d_out, rows, d_out, d_out, 0, out, d_out);

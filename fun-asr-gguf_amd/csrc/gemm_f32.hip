@@ -14,7 +14,18 @@ namespace fa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 64, BN = 64, BK = 32, LDP = BM + 1;
+constexpr int BK = 32;
+
+// Block tile (64 WM) x (64 WN) x 32: 2x2 waves, each wave 32WM x 32WN = WM x WN accumulators of 32x32.
+// LDS is k-major with row stride BM + 32: the two lane halves (k parity) land 32 banks apart, so the
+// per-MFMA operand reads are conflict-free. Global loads cover 8 rows x 128 B per wave instruction.
+template <int WM, int WN>
+struct Tile {
+  static constexpr int BM = 64 * WM, BN = 64 * WN;
+  static constexpr int LDA = BM + 32, LDB = BN + 32;
+  static constexpr int NA = BM * BK / 4 / 256, NB = BN * BK / 4 / 256;  // float4 per thread
+  static constexpr int STAGE = BK * (LDA + LDB);                          // floats per LDS stage
+};
 
 struct ALoadPlain {
   const float* A;
@@ -45,47 +56,57 @@ struct ALoadFrames {
   }
 };
 
-template <class AL>
+__device__ __forceinline__ float4 load_w4(const float* __restrict__ W, int64_t ldw, int n, int k, int N, int K) {
+  if (n >= N) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* p = W + (int64_t)n * ldw + k;
+  if (k + 3 < K) return *reinterpret_cast<const float4*>(p);
+  float4 r;
+  r.x = k < K ? p[0] : 0.f;
+  r.y = k + 1 < K ? p[1] : 0.f;
+  r.z = k + 2 < K ? p[2] : 0.f;
+  r.w = k + 3 < K ? p[3] : 0.f;
+  return r;
+}
+
+template <int WM, int WN, class AL>
 __device__ __forceinline__ void load_tiles(const AL& al, const float* __restrict__ W, int64_t ldw, int m0, int n0,
-                                           int k0, int M, int N, int K, float4 (&ra)[2], float4 (&rb)[2]) {
-  int t = threadIdx.x;
+                                           int k0, int M, int N, int K, float4 (&ra)[Tile<WM, WN>::NA],
+                                           float4 (&rb)[Tile<WM, WN>::NB]) {
+  const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int idx = t + i * 256;           // 0..511 -> (row 0..63, k4 0..7)
-    int r = idx >> 3, k4 = idx & 7;
-    int k = k0 + 4 * k4;
-    ra[i] = al.load4(m0 + r, k, M, K);
-    int n = n0 + r;
-    if (n < N) {
-      const float* p = W + (int64_t)n * ldw + k;
-      if (k + 3 < K) {
-        rb[i] = *reinterpret_cast<const float4*>(p);
-      } else {
-        rb[i].x = k < K ? p[0] : 0.f;
-        rb[i].y = k + 1 < K ? p[1] : 0.f;
-        rb[i].z = k + 2 < K ? p[2] : 0.f;
-        rb[i].w = k + 3 < K ? p[3] : 0.f;
-      }
-    } else {
-      rb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int i = 0; i < Tile<WM, WN>::NA; ++i) {
+    const int idx = t + i * 256;  // (row idx >> 3, k4 idx & 7)
+    ra[i] = al.load4(m0 + (idx >> 3), k0 + 4 * (idx & 7), M, K);
+  }
+#pragma unroll
+  for (int i = 0; i < Tile<WM, WN>::NB; ++i) {
+    const int idx = t + i * 256;
+    rb[i] = load_w4(W, ldw, n0 + (idx >> 3), k0 + 4 * (idx & 7), N, K);
   }
 }
 
-__device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (&ra)[2], const float4 (&rb)[2]) {
-  int t = threadIdx.x;
+template <int WM, int WN>
+__device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (&ra)[Tile<WM, WN>::NA],
+                                            const float4 (&rb)[Tile<WM, WN>::NB]) {
+  using T = Tile<WM, WN>;
+  const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    int idx = t + i * 256;
-    int r = idx >> 3, k = 4 * (idx & 7);
-    As[(k + 0) * LDP + r] = ra[i].x;
-    As[(k + 1) * LDP + r] = ra[i].y;
-    As[(k + 2) * LDP + r] = ra[i].z;
-    As[(k + 3) * LDP + r] = ra[i].w;
-    Bs[(k + 0) * LDP + r] = rb[i].x;
-    Bs[(k + 1) * LDP + r] = rb[i].y;
-    Bs[(k + 2) * LDP + r] = rb[i].z;
-    Bs[(k + 3) * LDP + r] = rb[i].w;
+  for (int i = 0; i < T::NA; ++i) {
+    const int idx = t + i * 256;
+    const int r = idx >> 3, k = 4 * (idx & 7);
+    As[(k + 0) * T::LDA + r] = ra[i].x;
+    As[(k + 1) * T::LDA + r] = ra[i].y;
+    As[(k + 2) * T::LDA + r] = ra[i].z;
+    As[(k + 3) * T::LDA + r] = ra[i].w;
+  }
+#pragma unroll
+  for (int i = 0; i < T::NB; ++i) {
+    const int idx = t + i * 256;
+    const int r = idx >> 3, k = 4 * (idx & 7);
+    Bs[(k + 0) * T::LDB + r] = rb[i].x;
+    Bs[(k + 1) * T::LDB + r] = rb[i].y;
+    Bs[(k + 2) * T::LDB + r] = rb[i].z;
+    Bs[(k + 3) * T::LDB + r] = rb[i].w;
   }
 }
 
@@ -197,43 +218,73 @@ struct EpiArgmax {
   }
 };
 
-template <class AL, class EPI>
+template <class AL, class EPI, int WM, int WN>
 __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
                                                   EPI epi) {
-  __shared__ float smem[2 * 2 * BK * LDP];
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  using T = Tile<WM, WN>;
+  extern __shared__ float smem[];  // 2 stages x (A [BK][LDA], B [BK][LDB])
+  const int m0 = blockIdx.y * T::BM, n0 = blockIdx.x * T::BN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 31, h = lane >> 5;
-  f32x16 acc = {};
-  float4 ra[2], rb[2];
-  load_tiles(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
-  store_tiles(smem, smem + BK * LDP, ra, rb);
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  float4 ra[T::NA], rb[T::NB];
+  load_tiles<WM, WN>(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
+  store_tiles<WM, WN>(smem, smem + BK * T::LDA, ra, rb);
   __syncthreads();
   const int nk = (K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
-    const float* a = smem + cur * 2 * BK * LDP + wr * 32 + r;
-    const float* b = smem + cur * 2 * BK * LDP + BK * LDP + wc * 32 + r;
+    if (kt + 1 < nk) load_tiles<WM, WN>(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
+    const float* a = smem + cur * T::STAGE + wr * 32 * WM + r;
+    const float* b = smem + cur * T::STAGE + BK * T::LDA + wc * 32 * WN + r;
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
-      float av = a[(2 * kk + h) * LDP];
-      float bv = b[(2 * kk + h) * LDP];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      float av[WM], bv[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) av[i] = a[(2 * kk + h) * T::LDA + 32 * i];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) bv[j] = b[(2 * kk + h) * T::LDB + 32 * j];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) {
-      store_tiles(smem + (cur ^ 1) * 2 * BK * LDP, smem + (cur ^ 1) * 2 * BK * LDP + BK * LDP, ra, rb);
-    }
+    if (kt + 1 < nk) store_tiles<WM, WN>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + BK * T::LDA, ra, rb);
     __syncthreads();
   }
-  epi.apply(acc, m0 + wr * 32, n0 + wc * 32, M, N, smem);
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
 }
 
+template <class AL, class EPI, int WM, int WN>
+static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
+  using T = Tile<WM, WN>;
+  dim3 grid(cdiv(N, T::BN), cdiv(M, T::BM));
+  const size_t lds = 2 * T::STAGE * sizeof(float);
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi);
+}
+
+// 128x128 blocks (4 MFMA accumulators per wave: half the LDS reads per MFMA) when they still give every CU
+// at least two blocks (batched encoder, C3); 64x64 blocks otherwise (single clip: fill the 256 CUs).
 template <class AL, class EPI>
-static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
-  dim3 grid(cdiv(N, BN), cdiv(M, BM));
-  hipLaunchKernelGGL((k_gemm_f32<AL, EPI>), grid, dim3(256), 0, s, al, W, ldw, M, N, K, epi);
+static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
+                     bool allow_big = true) {
+  if (allow_big && (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512)
+    launch_gemm<AL, EPI, 2, 2>(al, W, ldw, M, N, K, epi, s);
+  else
+    launch_gemm<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);
 }
 
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
@@ -277,10 +328,10 @@ __global__ void k_argmax_final(const float* __restrict__ pval, const int* __rest
 
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
                      int* pidx, int* out, hipStream_t s) {
-  int n_tiles = cdiv(N, BN);
+  int n_tiles = cdiv(N, 64);
   ALoadPlain al{A, lda};
   EpiArgmax epi{bias, pval, pidx, n_tiles};
-  run_gemm(al, W, K, M, N, K, epi, s);
+  run_gemm(al, W, K, M, N, K, epi, s, false);  // the argmax epilogue reduces 64-column blocks
   hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
 }
 

@@ -25,8 +25,21 @@ void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* b
                      int* pidx, int* out, hipStream_t s);
 
 // attn_f32.hip
+// Key-split workspace of the encoder attention (used only while (query tile, head, clip) blocks leave the
+// chip idle): splits x tiles <= 512, so 512 partials of 128 x (128 + 2) floats and 512 arrival counters
+// (zeroed once; re-armed by the merging block) always suffice.
+struct AttnF32Work {
+  float* part = nullptr;
+  int64_t part_n = 0;
+  int* cnt = nullptr;
+  int64_t cnt_n = 0;
+};
+constexpr int64_t ATTN_F32_PART_FLOATS = (int64_t)512 * (128 * 128 + 2 * 128);
+constexpr int64_t ATTN_F32_COUNTERS = 512;
+int attn_f32_splits(int batch, int t_stride, int n_heads);
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
-              int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens, hipStream_t s);
+              int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
+              const AttnF32Work& wk, hipStream_t s);
 
 // enc_misc.hip
 void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,

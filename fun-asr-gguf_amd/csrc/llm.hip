@@ -400,15 +400,14 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
     // split-K: publish this split's tile (sc1), count arrivals; the last split sums all KS tiles in
     // split order (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1)
     typedef float f4v __attribute__((ext_vector_type(4)));
-    constexpr int SC1 = 16;
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+      const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     float* base = a.kpart + (int64_t)tile * KS * (NS * 1024);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, KS * NS * 1024 * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * NS * 1024 * 4);
     const f4v v = {y[0], y[1], y[2], y[3]};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4, 0, SC1);
+    st_sc1_f4(v, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4);
     if (EPI == 2) {
       const f4v v2 = {y2[0], y2[1], y2[2], y2[3]};
-      __builtin_amdgcn_raw_buffer_store_b128(v2, rs, (ks * NS * 1024 + 1024 + threadIdx.x * 4) * 4, 0, SC1);
+      st_sc1_f4(v2, rs, (ks * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -418,8 +417,8 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
     if (!s_last) return;
     f4v sum = {0.f, 0.f, 0.f, 0.f}, sum2 = {0.f, 0.f, 0.f, 0.f};
     for (int k2 = 0; k2 < KS; ++k2) {
-      sum += __builtin_amdgcn_raw_buffer_load_b128(rs, (k2 * NS * 1024 + threadIdx.x * 4) * 4, 0, SC1);
-      if (EPI == 2) sum2 += __builtin_amdgcn_raw_buffer_load_b128(rs, (k2 * NS * 1024 + 1024 + threadIdx.x * 4) * 4, 0, SC1);
+      sum += ld_sc1_f4(rs, (k2 * NS * 1024 + threadIdx.x * 4) * 4);
+      if (EPI == 2) sum2 += ld_sc1_f4(rs, (k2 * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
     }
     y[0] = sum.x; y[1] = sum.y; y[2] = sum.z; y[3] = sum.w;
     y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
@@ -874,14 +873,13 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
   // split partial -> global (sc1: bypass L1, the combiner reads it from another CU)
   typedef float f4v __attribute__((ext_vector_type(4)));
   float* pbase = partials + ((int64_t)m * KV + g) * ASPLIT * APART;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pbase, 0, ASPLIT * APART * 4, 0x00020000);
-  constexpr int SC1 = 16;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, ASPLIT * APART * 4);
   const f4v ov = {o.x, o.y, o.z, o.w};
-  __builtin_amdgcn_raw_buffer_store_b128(ov, rs, (sp * APART + j * D + d0) * 4, 0, SC1);
+  st_sc1_f4(ov, rs, (sp * APART + j * D + d0) * 4);
   const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
   if (lane == 0) {
     const f4v ml = {M, L, M1, L1};
-    __builtin_amdgcn_raw_buffer_store_b128(ml, rs, (sp * APART + GQ * D) * 4, 0, SC1);
+    st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int last = 0;
@@ -894,8 +892,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict
 #pragma unroll
   for (int t = 0; t < ASPLIT; ++t) {
     const int tt = min(t, n_active - 1);
-    pml[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tt * APART + GQ * D) * 4, 0, SC1);
-    po[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tt * APART + j * D + d0) * 4, 0, SC1);
+    pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
+    po[t] = ld_sc1_f4(rs, (tt * APART + j * D + d0) * 4);
   }
   float MM = -INFINITY;
 #pragma unroll

@@ -1,0 +1,142 @@
+// attn_f32 (encoder attention) vs a CPU double reference over split / partial-tile / masked cases.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include "../../fun-asr-gguf_amd/csrc/kernels.h"
+namespace fa {
+extern int g_attn_f32_force_splits;
+void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
+void log(int, const std::string&) {}
+}
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using namespace fa;
+static float frand(uint32_t& s) { s = s * 1664525u + 1013904223u; return ((s >> 8) * (1.0f / 16777216.0f)) * 2.f - 1.f; }
+int main() {
+  hipStream_t st; CK(hipStreamCreate(&st));
+  AttnF32Work wk; wk.part_n = ATTN_F32_PART_FLOATS; wk.cnt_n = ATTN_F32_COUNTERS;
+  CK(hipMalloc(&wk.part, wk.part_n * 4)); CK(hipMalloc(&wk.cnt, wk.cnt_n * 4)); CK(hipMemset(wk.cnt, 0, wk.cnt_n * 4));
+  struct Case { int B, T, H, Dh; int len0; };
+  const Case cases[] = {{1, 50, 4, 128, 50}, {1, 167, 4, 128, 167}, {1, 1001, 4, 128, 1001}, {1, 167, 8, 64, 167},
+                        {2, 167, 4, 128, 120}, {1, 300, 8, 128, 300}, {3, 90, 8, 64, 77}};
+  int bad = 0;
+  {  // split-partial dump: T=64, 1 head, D=128, 2 splits of one 32-key tile each
+    const int T = 64, H = 1, Dh = 128, d = 128;
+    std::vector<float> qkv((size_t)T * 3 * d);
+    uint32_t seed = 99;
+    for (auto& v : qkv) v = frand(seed);
+    float *dq, *dout; CK(hipMalloc(&dq, qkv.size() * 4)); CK(hipMalloc(&dout, T * d * 4));
+    CK(hipMemcpy(dq, qkv.data(), qkv.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(wk.part, 0, 2 * (128 * 128 + 256) * 4));
+    g_attn_f32_force_splits = 2;
+    attn_f32(dq, dq + d, dq + 2 * d, 3 * d, 3 * d, 3 * d, dout, d, 1, T, H, Dh, nullptr, wk, st);
+    g_attn_f32_force_splits = 0;
+    CK(hipStreamSynchronize(st));
+    std::vector<float> part(2 * (128 * 128 + 256));
+    CK(hipMemcpy(part.data(), wk.part, part.size() * 4, hipMemcpyDeviceToHost));
+    const double scale = 1.0 / std::sqrt(128.0);
+    for (int sp = 0; sp < 2; ++sp) {
+      double em = 0, el = 0, eo = 0;
+      for (int q = 0; q < T; ++q) {
+        double sc[32], mx = -1e300;
+        for (int k = 0; k < 32; ++k) {
+          double sum = 0;
+          for (int e = 0; e < Dh; ++e) sum += (double)qkv[q * 3 * d + e] * scale * qkv[(sp * 32 + k) * 3 * d + d + e];
+          sc[k] = sum; mx = std::max(mx, sum);
+        }
+        double L = 0; for (int k = 0; k < 32; ++k) { sc[k] = std::exp(sc[k] - mx); L += sc[k]; }
+        const float* P = &part[sp * (128 * 128 + 256)];
+        em = std::max(em, std::fabs(P[128 * 128 + 2 * q] - mx));
+        el = std::max(el, std::fabs(P[128 * 128 + 2 * q + 1] - L));
+        for (int e = 0; e < Dh; ++e) {
+          double o = 0; for (int k = 0; k < 32; ++k) o += sc[k] * qkv[(sp * 32 + k) * 3 * d + 2 * d + e];
+          eo = std::max(eo, std::fabs(P[q * 128 + e] - o));
+        }
+      }
+      printf("split %d partial: max|dm| %.3g  max|dl| %.3g  max|dO| %.3g\n", sp, em, el, eo);
+    }
+    std::vector<float> out(T * d);
+    CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
+    int shown = 0;
+    for (int q = 0; q < T; ++q) {
+      double sc[64], mx = -1e300, L = 0, err = 0;
+      for (int k = 0; k < T; ++k) {
+        double sum = 0;
+        for (int e = 0; e < Dh; ++e) sum += (double)qkv[q * 3 * d + e] * scale * qkv[k * 3 * d + d + e];
+        sc[k] = sum; mx = std::max(mx, sum);
+      }
+      for (int k = 0; k < T; ++k) { sc[k] = std::exp(sc[k] - mx); L += sc[k]; }
+      int worst = 0;
+      for (int e = 0; e < Dh; ++e) {
+        double o = 0; for (int k = 0; k < T; ++k) o += sc[k] * qkv[k * 3 * d + 2 * d + e];
+        o /= L;
+        if (std::fabs(out[q * d + e] - o) > err) { err = std::fabs(out[q * d + e] - o); worst = e; }
+      }
+      if (err > 1e-4 && shown++ < 6) printf("  merged row q=%d max err %.3g at e=%d (got %.4f)\n", q, err, worst, out[q * d + worst]);
+    }
+    printf("merged: %d rows wrong of %d\n", shown, T);
+    {  // CPU merge of the dumped partials, q = 0
+      const int q = 0;
+      const float* P0 = &part[0]; const float* P1 = &part[128 * 128 + 256];
+      const double m0 = P0[128 * 128 + 2 * q], l0 = P0[128 * 128 + 2 * q + 1];
+      const double m1 = P1[128 * 128 + 2 * q], l1 = P1[128 * 128 + 2 * q + 1];
+      const double M = std::max(m0, m1), w0 = std::exp(m0 - M), w1 = std::exp(m1 - M), Ls = w0 * l0 + w1 * l1;
+      for (int e : {0, 55, 83}) {
+        const double o = (w0 * P0[q * 128 + e] + w1 * P1[q * 128 + e]) / Ls;
+        printf("  q=0 e=%d cpu-merge %.5f gpu %.5f | O0/l0 %.5f O1/l1 %.5f (m0 %.4f l0 %.4f m1 %.4f l1 %.4f)\n", e, o,
+               out[q * d + e], P0[q * 128 + e] / l0, P1[q * 128 + e] / l1, m0, l0, m1, l1);
+      }
+    }
+    CK(hipFree(dq)); CK(hipFree(dout));
+  }
+  for (const Case& c : cases) {
+    const int d = c.H * c.Dh, rows = c.B * c.T;
+    std::vector<float> qkv((size_t)rows * 3 * d), out((size_t)rows * d);
+    uint32_t seed = 1234 + c.T;
+    for (auto& v : qkv) v = frand(seed) * 2.f;
+    std::vector<int> lens(c.B);
+    for (int b = 0; b < c.B; ++b) lens[b] = b == 0 ? c.len0 : c.T;
+    float *dq, *dout; int* dl;
+    CK(hipMalloc(&dq, qkv.size() * 4)); CK(hipMalloc(&dout, out.size() * 4)); CK(hipMalloc(&dl, c.B * 4));
+    CK(hipMemcpy(dq, qkv.data(), qkv.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dl, lens.data(), c.B * 4, hipMemcpyHostToDevice));
+    for (int rep = 0; rep < 2; ++rep)
+      attn_f32(dq, dq + d, dq + 2 * d, 3 * d, 3 * d, 3 * d, dout, d, c.B, c.T, c.H, c.Dh, dl, wk, st);
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
+    double maxerr = 0, maxref = 0;
+    const double scale = std::pow((double)c.Dh, -0.5);
+    std::vector<double> sc(c.T);
+    for (int b = 0; b < c.B; ++b)
+      for (int h = 0; h < c.H; ++h)
+        for (int q = 0; q < c.T; ++q) {
+          const float* qp = &qkv[((size_t)b * c.T + q) * 3 * d + h * c.Dh];
+          double mx = -1e300;
+          for (int k = 0; k < c.T; ++k) {
+            const float* kp = &qkv[((size_t)b * c.T + k) * 3 * d + d + h * c.Dh];
+            double s = 0;
+            for (int e = 0; e < c.Dh; ++e) s += (double)qp[e] * scale * kp[e];
+            if (k >= lens[b]) s += -10000.0;
+            sc[k] = s;
+            mx = std::max(mx, s);
+          }
+          double L = 0;
+          for (int k = 0; k < c.T; ++k) { sc[k] = std::exp(sc[k] - mx); L += sc[k]; }
+          for (int e = 0; e < c.Dh; ++e) {
+            double o = 0;
+            for (int k = 0; k < c.T; ++k) o += sc[k] * qkv[((size_t)b * c.T + k) * 3 * d + 2 * d + h * c.Dh + e];
+            o /= L;
+            const double g = out[((size_t)b * c.T + q) * d + h * c.Dh + e];
+            maxerr = std::max(maxerr, std::fabs(g - o));
+            maxref = std::max(maxref, std::fabs(o));
+          }
+        }
+    const bool ok = maxerr < 1e-4 * std::max(1.0, maxref);
+    bad += !ok;
+    printf("B=%d T=%4d H=%d D=%3d len0=%4d splits=%d  max|err|=%.3g (max|ref| %.3g) %s\n", c.B, c.T, c.H, c.Dh, c.len0,
+           attn_f32_splits(c.B, c.T, c.H), maxerr, maxref, ok ? "ok" : "FAIL");
+    CK(hipFree(dq)); CK(hipFree(dout)); CK(hipFree(dl));
+  }
+  return bad != 0;
+}
