@@ -145,7 +145,7 @@ struct Engine {
   struct ProfCls {
     double ms = 0, bytes = 0, flops = 0;
     int64_t launches = 0;
-  } pcls[4];
+  } pcls[5];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool, graph_events;
   struct Pending {
     int cls;
@@ -830,10 +830,11 @@ struct Engine {
     a.kcnt = gk_cnt;
     a.kcnt_n = gk_cnt_n;
     hipEvent_t ev;
-    prof_begin(0, &ev);
+    const int cls = epi == 3 ? 4 : 0;  // LM head (fused argmax) is its own class: it is not layer-sampled
+    prof_begin(cls, &ev);
     gemv_q8(a, K, epi, stream);
     const double wbytes = (double)a.O * K * (epi == 2 ? 2.0 : 1.0) * 34.0 / 32.0;
-    prof_end(0, wbytes, 2.0 * a.M * a.O * K * (epi == 2 ? 2.0 : 1.0));
+    prof_end(cls, wbytes, 2.0 * a.M * a.O * K * (epi == 2 ? 2.0 : 1.0));
   }
 
   void sample(int M, const fa_sampling* s, const int* step_ctr, int* tok_out, int* hist) {
@@ -1226,7 +1227,7 @@ int fa_profile_enable(fa_engine* h, int32_t on) {
 int fa_profile_read(fa_engine* h, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops) {
   FA_API_BEGIN
   Engine* e = h->e;
-  FA_REQUIRE(cls >= 0 && cls < 4, "class");
+  FA_REQUIRE(cls >= 0 && cls < 5, "class");
   e->prof_collect();
   if (ms) *ms = e->pcls[cls].ms;
   if (launches) *launches = e->pcls[cls].launches;

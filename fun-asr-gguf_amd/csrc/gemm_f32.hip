@@ -2,8 +2,7 @@
 //
 // v_mfma_f32_32x32x2_f32 (exact f32 fma chain, 157 TF/s dense peak on MI355X): lane l holds
 // A[i=l&31][k=l>>5], B[k=l>>5][j=l&31]; accumulator reg r -> row (r&3)+8(r>>2)+4(l>>5), col l&31.
-// Block tile 64x64x32, 4 waves (2x2 of 32x32), LDS k-major [BK][BM+1] double-buffered: global loads are
-// 8 rows x 128 B per wave instruction, LDS writes/reads are bank-conflict free with the +1 pad.
+// Block tiles 64x64 or 128x128 (x32 in k), 4 waves, row-major LDS double-buffered (see Tile below).
 // Used for every encoder/adaptor/CTC projection, the STFT-as-DFT-GEMM (F2) with a
 // power epilogue (F3), the mel projection with a log epilogue, and the CTC projection with a fused
 // row-argmax epilogue (C1) so the [T, 60515] logits never reach HBM.
@@ -17,14 +16,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int BK = 32;
 
 // Block tile (64 WM) x (64 WN) x 32: 2x2 waves, each wave 32WM x 32WN = WM x WN accumulators of 32x32.
-// LDS is k-major with row stride BM + 32: the two lane halves (k parity) land 32 banks apart, so the
-// per-MFMA operand reads are conflict-free. Global loads cover 8 rows x 128 B per wave instruction.
+// LDS is row-major [row][k] with row stride 34 floats: the MFMA operand read of lane (r, h) hits bank
+// (34 r + 2 kk + h) mod 64 = 2 (17 r mod 32) + h -> 64 distinct banks (17 is odd); each thread stores its
+// 16-B global chunk as two aligned 8-B writes. Global loads cover 8 rows x 128 B per wave instruction.
+constexpr int LDK = BK + 2;
 template <int WM, int WN>
 struct Tile {
   static constexpr int BM = 64 * WM, BN = 64 * WN;
-  static constexpr int LDA = BM + 32, LDB = BN + 32;
   static constexpr int NA = BM * BK / 4 / 256, NB = BN * BK / 4 / 256;  // float4 per thread
-  static constexpr int STAGE = BK * (LDA + LDB);                          // floats per LDS stage
+  static constexpr int STAGE = (BM + BN) * LDK;                         // floats per LDS stage
 };
 
 struct ALoadPlain {
@@ -93,20 +93,16 @@ __device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
-    const int r = idx >> 3, k = 4 * (idx & 7);
-    As[(k + 0) * T::LDA + r] = ra[i].x;
-    As[(k + 1) * T::LDA + r] = ra[i].y;
-    As[(k + 2) * T::LDA + r] = ra[i].z;
-    As[(k + 3) * T::LDA + r] = ra[i].w;
+    float* d = As + (idx >> 3) * LDK + 4 * (idx & 7);
+    reinterpret_cast<float2*>(d)[0] = make_float2(ra[i].x, ra[i].y);
+    reinterpret_cast<float2*>(d)[1] = make_float2(ra[i].z, ra[i].w);
   }
 #pragma unroll
   for (int i = 0; i < T::NB; ++i) {
     const int idx = t + i * 256;
-    const int r = idx >> 3, k = 4 * (idx & 7);
-    Bs[(k + 0) * T::LDB + r] = rb[i].x;
-    Bs[(k + 1) * T::LDB + r] = rb[i].y;
-    Bs[(k + 2) * T::LDB + r] = rb[i].z;
-    Bs[(k + 3) * T::LDB + r] = rb[i].w;
+    float* d = Bs + (idx >> 3) * LDK + 4 * (idx & 7);
+    reinterpret_cast<float2*>(d)[0] = make_float2(rb[i].x, rb[i].y);
+    reinterpret_cast<float2*>(d)[1] = make_float2(rb[i].z, rb[i].w);
   }
 }
 
@@ -222,7 +218,7 @@ template <class AL, class EPI, int WM, int WN>
 __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
                                                   EPI epi) {
   using T = Tile<WM, WN>;
-  extern __shared__ float smem[];  // 2 stages x (A [BK][LDA], B [BK][LDB])
+  extern __shared__ float smem[];  // 2 stages x (A [BM][LDK], B [BN][LDK])
   const int m0 = blockIdx.y * T::BM, n0 = blockIdx.x * T::BN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
@@ -234,27 +230,27 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
   float4 ra[T::NA], rb[T::NB];
   load_tiles<WM, WN>(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
-  store_tiles<WM, WN>(smem, smem + BK * T::LDA, ra, rb);
+  store_tiles<WM, WN>(smem, smem + T::BM * LDK, ra, rb);
   __syncthreads();
   const int nk = (K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_tiles<WM, WN>(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
-    const float* a = smem + cur * T::STAGE + wr * 32 * WM + r;
-    const float* b = smem + cur * T::STAGE + BK * T::LDA + wc * 32 * WN + r;
+    const float* a = smem + cur * T::STAGE + (wr * 32 * WM + r) * LDK + h;
+    const float* b = smem + cur * T::STAGE + T::BM * LDK + (wc * 32 * WN + r) * LDK + h;
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       float av[WM], bv[WN];
 #pragma unroll
-      for (int i = 0; i < WM; ++i) av[i] = a[(2 * kk + h) * T::LDA + 32 * i];
+      for (int i = 0; i < WM; ++i) av[i] = a[32 * i * LDK + 2 * kk];
 #pragma unroll
-      for (int j = 0; j < WN; ++j) bv[j] = b[(2 * kk + h) * T::LDB + 32 * j];
+      for (int j = 0; j < WN; ++j) bv[j] = b[32 * j * LDK + 2 * kk];
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles<WM, WN>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + BK * T::LDA, ra, rb);
+    if (kt + 1 < nk) store_tiles<WM, WN>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
     __syncthreads();
   }
 #pragma unroll
@@ -278,10 +274,13 @@ static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N,
 
 // 128x128 blocks (4 MFMA accumulators per wave: half the LDS reads per MFMA) when they still give every CU
 // at least two blocks (batched encoder, C3); 64x64 blocks otherwise (single clip: fill the 256 CUs).
+int g_gemm_f32_force = 0;  // microbenchmark hook: 1 = 64x64 blocks, 2 = 128x128 blocks
+
 template <class AL, class EPI>
 static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
                      bool allow_big = true) {
-  if (allow_big && (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512)
+  const bool big = g_gemm_f32_force ? g_gemm_f32_force == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
+  if (allow_big && big)
     launch_gemm<AL, EPI, 2, 2>(al, W, ldw, M, N, K, epi, s);
   else
     launch_gemm<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);

@@ -743,26 +743,30 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
 // to the (m, g) counter (agent scope); the block whose add comes last combines the partials with sc1
 // loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1: no fences needed).
 // Prefill mode (decode_mode = 0): q is already normed/roped (qk_rope_store) and K/V[pos] are in the cache.
-__global__ __launch_bounds__(AWV * 64) void k_attn_block(const float* __restrict__ qsrc, int decode_mode,
+// (parameter order = kernarg layout: everything the prologue needs sits in the first 64-B line)
+__global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+                                                         int lg_nsplit, int decode_mode, int H, int KV,
+                                                         int64_t seq_stride, __half* __restrict__ kc,
+                                                         __half* __restrict__ vc, const float* __restrict__ qsrc,
                                                          const float* __restrict__ qn, const float* __restrict__ kn,
-                                                         float eps, const float* __restrict__ rcos,
-                                                         const float* __restrict__ rsin, __half* __restrict__ kc,
-                                                         __half* __restrict__ vc, int H, int KV,
-                                                         const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
-                                                         int64_t seq_stride, float scale, float* __restrict__ out,
-                                                         int* __restrict__ counters, float* __restrict__ partials,
-                                                         int nsplit) {
+                                                         const float* __restrict__ rcos, const float* __restrict__ rsin,
+                                                         float eps, float scale, float* __restrict__ out,
+                                                         int* __restrict__ counters, float* __restrict__ partials) {
   constexpr int D = 128;
   STAMP(0);
-  const int g = blockIdx.x % KV, sp = blockIdx.x / KV, m = blockIdx.y;
+  const int g = blockIdx.x, sp = blockIdx.y, m = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int pos = tok_pos[m];
+  int pos = tok_pos[m];
   const int seq = tok_seq[m];
-  asm volatile("" ::"s"(pos), "s"(seq));  // issue both scalar loads together, ahead of the early-exit branch
+  // pos "depends" on seq and on the pointer arguments: the two index loads and every kernarg line are
+  // fetched together, before the first use (otherwise each is a serial scalar-load latency)
+  asm volatile("" : "+s"(pos) : "s"(seq), "s"(qsrc), "s"(kc), "s"(vc), "s"(rcos), "s"(rsin), "s"(qn), "s"(kn),
+               "s"(seq_stride), "s"(out), "s"(partials));
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
-  const int gps = max(AMIN_G, (n_groups + nsplit - 1) / nsplit);  // groups per split
-  const int n_active = (n_groups + gps - 1) / gps;
+  const int gps = max(AMIN_G, (n_groups + (1 << lg_nsplit) - 1) >> lg_nsplit);  // groups per split
+  // n_active = ceil(n_groups / gps) without an integer-division sequence (gps <= n_groups < 2^24: exact)
+  int n_active = (int)ceilf((float)n_groups / (float)gps);
   if (sp >= n_active) return;                                      // uniform over the block
   const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
   STAMP(1);
@@ -920,10 +924,12 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
-  // key splits only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1, 4 at batch 32
-  const int nsplit = std::max(1, std::min(ASPLIT, 1024 / std::max(1, M * KV)));
-  hipLaunchKernelGGL(k_attn_block, dim3(KV * nsplit, M), dim3(AWV * 64), 0, s, qsrc, decode_mode, qn, kn, eps, rcos,
-                     rsin, kc, vc, H, KV, tok_seq, tok_pos, seq_stride, scale, out, wk.counters, wk.partials, nsplit);
+  // key splits (a power of two) only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1,
+  // 4 at batch 32, 1 for prefill
+  int lg = 0;
+  while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= 1024) ++lg;
+  hipLaunchKernelGGL(k_attn_block, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode, H, KV,
+                     seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -133,7 +133,9 @@ int fa_align_timestamps(const int32_t* ctc_keys, const double* ctc_starts, int32
 
 /* ---- timing hooks for bench.py roofline (HIP events on the engine's stream) */
 /* Enable per-kernel-class event timing; fa_profile_read returns accumulated ms and launch counts for
- * class ids: 0 q8 GEMV (decode), 1 f32 GEMM (encoder), 2 encoder attention, 3 decode attention. */
+ * class ids: 0 q8 GEMV/GEMM of the decoder layers, 1 f32 GEMM (encoder), 2 encoder attention,
+ * 3 decoder attention, 4 LM head. Classes 0 and 3 are sampled on layer 0 only (identical shapes in every
+ * layer): multiply their ms by n_layer for the device time of all layers. */
 int fa_profile_enable(fa_engine* e, int32_t on);
 int fa_profile_read(fa_engine* e, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops);
 int fa_synchronize(fa_engine* e);

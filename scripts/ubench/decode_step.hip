@@ -22,9 +22,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048, L = 28;
   float* tmp = dalloc<float>((size_t)V * E);
+  // "arena": all q8_0 weights carved from ONE allocation (TLB experiment), else one hipMalloc per tensor
+  const bool arena = argc > 1 && !strcmp(argv[1], "arena");
+  char* arena_p = nullptr; size_t arena_off = 0;
+  if (arena) CK(hipMalloc(&arena_p, (size_t)700 << 20));
+  auto take = [&](size_t bytes) -> void* {
+    if (!arena) { void* p; CK(hipMalloc(&p, bytes)); return p; }
+    void* p = arena_p + arena_off; arena_off += (bytes + 4095) & ~(size_t)4095; return p; };
   auto q8 = [&](int64_t rows, int64_t cols, uint32_t key, int8_t** q, __half** d) {
     launch_synth_fill(tmp, rows * cols, key, 0.05f, 0.f, s);
-    *q = dalloc<int8_t>(rows * cols); *d = dalloc<__half>(rows * cols / 32);
+    *q = (int8_t*)take(rows * cols); *d = (__half*)take(rows * cols / 32 * 2);
     launch_quant_q8_0(tmp, rows * cols, *q, *d, s);
   };
   struct LW { int8_t *qkv, *o, *g, *u, *d; __half *dqkv, *dO, *dg, *du, *dd; };
@@ -67,6 +74,7 @@ int main(int argc, char** argv) {
     if (mask & 32) gemv_q8(h, E, 3, s);
   };
   const bool eager = argc > 1 && !strcmp(argv[1], "eager");
+  printf("weights: %s\n", arena ? "one arena allocation" : "one hipMalloc per tensor");
   const int n = argc > 2 ? atoi(argv[2]) : 3;
   if (eager) { for (int i = 0; i < n; ++i) step(); CK(hipStreamSynchronize(s)); printf("eager %d steps done\n", n); return 0; }
   const double bytes = (double)L * (QKV * E + E * H * D + 2.0 * F * E + E * F) * 34 / 32 + (double)V * E * 34 / 32;

@@ -1,0 +1,70 @@
+// Encoder f32 GEMM (gemm_linear) per shape and tile variant, graph-timed; plus a CPU spot check.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+#include "../../fun-asr-gguf_amd/csrc/kernels.h"
+namespace fa {
+extern int g_gemm_f32_force;
+void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
+void log(int, const std::string&) {}
+}
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using namespace fa;
+static hipStream_t s;
+static double time_graph(std::function<void()> f, int reps) {
+  hipGraph_t g; hipGraphExec_t ex;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipStreamEndCapture(s, &g)); CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  CK(hipGraphLaunch(ex, s)); CK(hipStreamSynchronize(s));
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  CK(hipEventRecord(a, s)); for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
+  CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
+  return ms * 1e3 / (3.0 * reps);
+}
+int main() {
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int Mmax = 32032, Kmax = 2048, Nmax = 2048;
+  float *A, *W, *bias, *C;
+  CK(hipMalloc(&A, (size_t)Mmax * Kmax * 4)); CK(hipMalloc(&W, (size_t)Nmax * Kmax * 4));
+  CK(hipMalloc(&bias, Nmax * 4)); CK(hipMalloc(&C, (size_t)Mmax * Nmax * 4));
+  launch_synth_fill(A, (int64_t)Mmax * Kmax, 1, 1.f, 0.f, s); launch_synth_fill(W, (int64_t)Nmax * Kmax, 2, 0.05f, 0.f, s);
+  launch_synth_fill(bias, Nmax, 3, 0.1f, 0.f, s);
+  CK(hipStreamSynchronize(s));
+  {  // spot check: M=100 N=96 K=72 (partial tiles) against the CPU
+    const int M = 100, N = 96, K = 72;
+    for (int v : {1, 2}) {
+      g_gemm_f32_force = v;
+      gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s);
+      CK(hipStreamSynchronize(s));
+      std::vector<float> a((size_t)M * K), w((size_t)N * K), b(N), c((size_t)M * N);
+      CK(hipMemcpy(a.data(), A, a.size() * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(w.data(), W, w.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), bias, N * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(c.data(), C, c.size() * 4, hipMemcpyDeviceToHost));
+      double err = 0;
+      for (int i = 0; i < M; ++i) for (int j = 0; j < N; ++j) {
+        double r = b[j]; for (int k = 0; k < K; ++k) r += (double)a[i * K + k] * w[j * K + k];
+        err = std::max(err, std::fabs(r - c[i * N + j]));
+      }
+      printf("check variant %d: max|err| %.3g %s\n", v, err, err < 1e-4 ? "ok" : "FAIL");
+    }
+  }
+  struct Sh { const char* name; int N, K; };
+  const Sh shapes[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
+  for (int M : {1001, 32032}) {
+    for (const Sh& sh : shapes) {
+      printf("M=%5d %-9s N=%4d K=%4d:", M, sh.name, sh.N, sh.K);
+      for (int v : {1, 2}) {
+        g_gemm_f32_force = v;
+        const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s); },
+                                     M > 2000 ? 10 : 50);
+        printf("  %s %8.1f us %6.1f TF/s", v == 1 ? "64x64" : "128x128", us, 2.0 * M * sh.N * sh.K / us / 1e6);
+      }
+      printf("\n");
+    }
+  }
+  return 0;
+}
