@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    *s_flag = __hip_atomic_fetch_add(cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+    *s_flag = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
   __syncthreads();
   if (!*s_flag) return;
   // merged max / sum per query, then the weighted sum of the splits' O
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
     *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) =
         make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)

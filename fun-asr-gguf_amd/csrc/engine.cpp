@@ -476,8 +476,8 @@ struct Engine {
     enc_attn_wk.part_n = ATTN_F32_PART_FLOATS;
     enc_attn_wk.part = alloc<float>(enc_attn_wk.part_n);
     enc_attn_wk.cnt_n = ATTN_F32_COUNTERS;
-    enc_attn_wk.cnt = alloc<int>(enc_attn_wk.cnt_n);
-    FA_HIP(hipMemset(enc_attn_wk.cnt, 0, enc_attn_wk.cnt_n * sizeof(int)));
+    enc_attn_wk.cnt = alloc<int>(enc_attn_wk.cnt_n * CNT_LINE);
+    FA_HIP(hipMemset(enc_attn_wk.cnt, 0, enc_attn_wk.cnt_n * CNT_LINE * sizeof(int)));
     mel = alloc<float>((size_t)max_batch * tm_max * ec.n_mels);
     const int wmax = std::max({ec.d_in, ec.d_llm, d});
     xa = alloc<float>((size_t)R * wmax);
@@ -530,14 +530,14 @@ struct Engine {
     d_ids = alloc<int>(m_max);
     attn_wk.max_tokens = m_max;
     attn_wk.max_kv = KV;
-    attn_wk.counters = alloc<int>((size_t)m_max * KV);
-    FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * sizeof(int)));
+    attn_wk.counters = alloc<int>((size_t)m_max * KV * CNT_LINE);
+    FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * CNT_LINE * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
     // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)
     gk_cnt_n = 256;
     gk_part_n = (int64_t)256 * 8 * 2 * 1024;
-    gk_cnt = alloc<int>(gk_cnt_n);
-    FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * sizeof(int)));
+    gk_cnt = alloc<int>(gk_cnt_n * CNT_LINE);
+    FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * CNT_LINE * sizeof(int)));
     gk_part = alloc<float>(gk_part_n);
     n_past.assign(lc.max_seqs, 0);
     last_tok.assign(lc.max_seqs, -1);

@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-      s_last = __hip_atomic_fetch_add(a.kcnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+      s_last = __hip_atomic_fetch_add(a.kcnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
     __syncthreads();
     if (!s_last) return;
     f4v sum = {0.f, 0.f, 0.f, 0.f}, sum2 = {0.f, 0.f, 0.f, 0.f};
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
     }
     y[0] = sum.x; y[1] = sum.y; y[2] = sum.z; y[3] = sum.w;
     y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
-    if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const int col = l & 31, tok = t0 + col;
 #pragma unroll
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int last = 0;
-  if (lane == 0) last = __hip_atomic_fetch_add(counters + m * KV + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) last = __hip_atomic_fetch_add(counters + (m * KV + g) * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   last = __builtin_amdgcn_readfirstlane(last);
   if (last != n_active - 1) return;
   STAMP(9);
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     }
   }
   *reinterpret_cast<float4*>(op) = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
-  if (lane == 0) __hip_atomic_store(counters + m * KV + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(counters + (m * KV + g) * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,

@@ -14,5 +14,6 @@ timeout -k 10 900 python bench.py --steps $STEPS --warmup 2 ${BENCH_ARGS} > gpur
 cat gpurun_out/bench.json
 if [ -n "$PROFILE" ]; then
   FUNASR_GRAPHS=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/prof.log; exit 1; }
-  python scripts/prof_summary.py gpurun_out/prof/run_results.db 22
+  python scripts/prof_summary.py gpurun_out/prof/run_results.db 40 > gpurun_out/prof_summary.txt && cat gpurun_out/prof_summary.txt
+  rm -rf gpurun_out/prof
 fi

@@ -14,7 +14,7 @@ template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T)
 int main() {
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
-  CK(hipMalloc(&wk.counters, 64)); CK(hipMemset(wk.counters, 0, 64));
+  CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int H = 16, KV = 8, D = 128, NCTX = 2048, QKV = 4096;
   float* qkv = dalloc<float>(QKV); launch_synth_fill(qkv, QKV, 9, 1.f, 0.f, s);

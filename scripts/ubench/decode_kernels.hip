@@ -31,7 +31,7 @@ static double time_graph(const char* name, std::function<void()> f, int reps = 2
 int main() {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
-  CK(hipMalloc(&wk.counters, 64)); CK(hipMemset(wk.counters, 0, 64));
+  CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048;
   auto q8 = [&](int64_t rows, int64_t cols, uint32_t key, int8_t** q, __half** d) {

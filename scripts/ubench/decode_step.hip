@@ -18,7 +18,7 @@ template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T)
 int main(int argc, char** argv) {
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
-  CK(hipMalloc(&wk.counters, 64)); CK(hipMemset(wk.counters, 0, 64));
+  CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048, L = 28;
   float* tmp = dalloc<float>((size_t)V * E);
