@@ -186,9 +186,11 @@ struct Engine {
   void prof_begin(int cls, hipEvent_t* a) {
     if (!prof || !prof_sample) return;
     if (ev_next >= ev_pool.size()) {
+      // timing-only events: no system-scope fence (cache writeback + invalidate) at each record, which would
+      // otherwise be charged to the bracketed kernel
       hipEvent_t x, y;
-      FA_HIP(hipEventCreate(&x));
-      FA_HIP(hipEventCreate(&y));
+      FA_HIP(hipEventCreateWithFlags(&x, hipEventDisableSystemFence));
+      FA_HIP(hipEventCreateWithFlags(&y, hipEventDisableSystemFence));
       ev_pool.push_back({x, y});
     }
     *a = ev_pool[ev_next].first;
@@ -774,10 +776,15 @@ struct Engine {
 
   // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
   void decode_step(int n, const fa_sampling* s) {
-    embed_rows(tok_embd.q, tok_embd.d, d_tok_cur, n, lc.n_embd, 0, lx, stream);
+    // profiled (eager) steps: give the host a head start so the sampled event pairs time back-to-back kernels,
+    // not host launch gaps
+    if (prof) gpu_delay_us(1500, stream);
     llm_forward(n, true, 0);
-    sample(n, s, d_step, d_tok_cur, d_tok_hist);
-    advance_positions(d_tok_pos, d_step, n, stream);
+    // sample, then the next step's input row + position advance in the same launch (the first step's row is
+    // embedded by fa_llm_generate before the steps)
+    EmbedNext en;
+    en.qs = tok_embd.q; en.d = tok_embd.d; en.E = lc.n_embd; en.x = lx; en.tok_pos = d_tok_pos;
+    sample(n, s, d_step, d_tok_cur, d_tok_hist, &en);
   }
 
   // hipGraph of one decode step (all per-step state lives in device memory, grids are n_past-independent).
@@ -837,10 +844,10 @@ struct Engine {
     prof_end(cls, wbytes, 2.0 * a.M * a.O * K * (epi == 2 ? 2.0 : 1.0));
   }
 
-  void sample(int M, const fa_sampling* s, const int* step_ctr, int* tok_out, int* hist) {
+  void sample(int M, const fa_sampling* s, int* step_ctr, int* tok_out, int* hist, const EmbedNext* en = nullptr) {
     const float temp = s ? s->temperature : 0.f;
     sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, M, temp, s ? s->top_k : 1, s ? s->top_p : 1.f,
-                  s ? s->seed : 0u, step_ctr, tok_out, hist, hist_max, stream);
+                  s ? s->seed : 0u, step_ctr, tok_out, hist, hist_max, en, stream);
   }
 };
 
@@ -896,6 +903,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_HIP(hipSetDevice(device));
     FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();
     e->build_encoder();
@@ -1175,6 +1183,8 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_cur, cur.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
+  // input row of the first step (later steps get theirs from the sampler launch)
+  fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_tok_cur, n_seqs, e->lc.n_embd, 0, e->lx, e->stream);
   // sampling parameters are baked into a captured graph: graphs only for the greedy path.
   // With profiling on, the last step of the call replays the profiled graph variant (sampled timing).
   // (event nodes inside graphs do not time individual nodes on ROCm 7.2: profiling runs eager)

@@ -77,6 +77,7 @@ int gemv_rows_per_wave(int O);
 // argmax partials per token written by the lm_head launch for M tokens (GEMV for M <= 4, MFMA GEMM above)
 int lm_head_parts(int O, int M);
 int gemm_k_splits(int O, int M, int K);
+extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
                    int64_t seq_stride, hipStream_t s);
@@ -95,9 +96,19 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
                 int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
+// Decode-step tail fused into the sampler: embedding row of the sampled token -> x (the next step's input), and
+// tok_pos / step_ctr advanced by one (x == nullptr: sample only, e.g. after prefill)
+struct EmbedNext {
+  const int8_t* qs = nullptr;
+  const __half* d = nullptr;
+  int E = 0;
+  float* x = nullptr;
+  int* tok_pos = nullptr;
+};
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   float temperature, int top_k, float top_p, uint32_t seed, const int* step_ctr, int* tok_out,
-                   int* tok_hist, int hist_stride, hipStream_t s);
+                   float temperature, int top_k, float top_p, uint32_t seed, int* step_ctr, int* tok_out,
+                   int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s);
 void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s);
+void gpu_delay_us(int us, hipStream_t s);
 
 }  // namespace fa

@@ -450,8 +450,108 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
   }
 }
 
+// Same GEMM with K split over the 8 waves of ONE block instead of over blocks: no cross-block split-K hop (on this
+// chip an in-launch hand-off costs about a kernel boundary: scripts/ubench/edge_chain.hip), and every wave issues
+// ALL its loads (NBW q8_0 blocks of weights and activations, their scales) before its MFMAs, so a tile costs one
+// memory round trip. Waves are reduced in LDS in fixed order (deterministic). SwiGLU: waves 0-3 gate, 4-7 up.
+constexpr int KW_WAVES = 8;
+template <int EPI, int NBW>
+__global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
+  static_assert(NBW % 4 == 0 && EPI != 3, "k_gemm_q8_kw: 4-block scale groups, no lm_head epilogue");
+  constexpr int NWM = EPI == 2 ? KW_WAVES / 2 : KW_WAVES;  // waves per weight matrix
+  const int nb = K >> 5;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
+  const bool upw = EPI == 2 && wave >= NWM;
+  const int b0 = (EPI == 2 ? wave % NWM : wave) * NBW;  // this wave's q8_0 blocks [b0, b0 + NBW) (host: NBW*NWM == nb)
+  const int8_t* wq = upw ? a.wq2 : a.wq;
+  const __half* wd = upw ? a.wd2 : a.wd;
+  const int8_t* wa = wq + (int64_t)min(o0 + r, a.O - 1) * K + 16 * h + b0 * 32;
+  const int t_b = min(t0 + r, a.M - 1);
+  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + b0 * 32;
+  i32x4_t A[NBW], B[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
+    B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
+  }
+  uint2 dw[16][NBW / 4];  // fp16 scales of each of this lane's 16 rows, 4 blocks per uint2
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
+#pragma unroll
+    for (int q = 0; q < NBW / 4; ++q) dw[reg][q] = *reinterpret_cast<const uint2*>(wd + (int64_t)row * nb + b0 + 4 * q);
+  }
+  float4 dx4[NBW / 4];
+#pragma unroll
+  for (int q = 0; q < NBW / 4; ++q) dx4[q] = *reinterpret_cast<const float4*>(a.xd + (int64_t)t_b * nb + b0 + 4 * q);
+  float acc[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
+  const i32x16_t zero = {};
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
+    const float4& d4 = dx4[j >> 2];
+    const float dx = (j & 3) == 0 ? d4.x : (j & 3) == 1 ? d4.y : (j & 3) == 2 ? d4.z : d4.w;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 2]);
+      acc[reg] += (float)D[reg] * (__half2float(hw[j & 3]) * dx);
+    }
+  }
+  // fixed-order reduction over the waves of each matrix; thread t finalises regs [2 (t>>6), +2) of lane t&63
+  __shared__ float s_red[KW_WAVES][16][64];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
+  __syncthreads();
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = l & 31, tok = t0 + col;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int reg = 2 * g + q;
+    float y = 0.f, y2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWM; ++w) y += s_red[w][reg][l];
+    if (EPI == 2) {
+#pragma unroll
+      for (int w = NWM; w < KW_WAVES; ++w) y2 += s_red[w][reg][l];
+    }
+    const int row = o0 + (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
+    if (row < a.O && tok < a.M) {
+      float* op = a.out + (int64_t)tok * a.ldo + row;
+      if (EPI == 0) *op = y;
+      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y;
+      else *op = (y / (1.0f + expf(-y))) * y2;
+    }
+  }
+}
+
+template <int EPI, int NBW>
+static void launch_gemm_kw(const GemvArgs& a, int K, hipStream_t s) {
+  hipLaunchKernelGGL((k_gemm_q8_kw<EPI, NBW>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)), dim3(KW_WAVES * 64), 0, s, a, K);
+}
+
+// K-in-block GEMM for the shapes it is instantiated for (q8_0 blocks per wave NBW = 4, 8, 12); false otherwise
+static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
+  const int nbw = (K / 32) * (epi == 2 ? 2 : 1) / KW_WAVES;
+  if (epi == 3 || (K / 32) * (epi == 2 ? 2 : 1) != nbw * KW_WAVES) return false;
+  switch (epi * 100 + nbw) {
+    case 4: launch_gemm_kw<0, 4>(a, K, s); return true;
+    case 8: launch_gemm_kw<0, 8>(a, K, s); return true;
+    case 12: launch_gemm_kw<0, 12>(a, K, s); return true;
+    case 104: launch_gemm_kw<1, 4>(a, K, s); return true;
+    case 108: launch_gemm_kw<1, 8>(a, K, s); return true;
+    case 112: launch_gemm_kw<1, 12>(a, K, s); return true;
+    case 208: launch_gemm_kw<2, 8>(a, K, s); return true;
+    default: return false;
+  }
+}
+
 // K splits for the MFMA GEMM: enough blocks to cover the chip when the tile count is small, keeping
 // (K/32)/KS/4 a multiple of the 4-block load group. Split-K needs the a.kpart/a.kcnt workspace.
+int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0)
+
 int gemm_k_splits(int O, int M, int K) {
   const int tiles = cdiv(O, 32) * cdiv(M, 32);
   const int nb = K / 32;
@@ -484,6 +584,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
+  if (g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
   int KS = (a.kpart && a.kcnt && epi != 3) ? gemm_k_splits(a.O, a.M, K) : 1;
   if (KS > 1)
@@ -964,8 +1065,8 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
 __global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logits, int64_t ldl, int V,
                                                  const float* __restrict__ pval, const int* __restrict__ pidx, int n_part,
                                                  float temperature, int top_k, float top_p, uint32_t seed,
-                                                 const int* __restrict__ step_ctr, int* __restrict__ tok_out,
-                                                 int* __restrict__ tok_hist, int hist_stride) {
+                                                 int* __restrict__ step_ctr, int* __restrict__ tok_out,
+                                                 int* __restrict__ tok_hist, int hist_stride, EmbedNext en) {
   const int m = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ float sv[16];
@@ -1047,21 +1148,39 @@ __global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logit
     __syncthreads();
     tok = si[0];
   }
+  if (en.x) {
+    // decode step tail: the next step's input row (D0, f32 token_embd row) and the position advance ride along,
+    // so a step is forward + this launch (the row was consumed by the lm_head launch before this one)
+    const int64_t row = tok;
+    for (int i = threadIdx.x; i < en.E; i += 1024)
+      en.x[(int64_t)m * en.E + i] = __half2float(en.d[row * (en.E / 32) + i / 32]) * (float)en.qs[row * en.E + i];
+  }
   if (threadIdx.x == 0) {
     tok_out[m] = tok;
-    if (tok_hist) {
-      const int c = step_ctr ? step_ctr[m] : 0;
-      tok_hist[(int64_t)m * hist_stride + c] = tok;
+    const int c = step_ctr ? step_ctr[m] : 0;
+    if (tok_hist) tok_hist[(int64_t)m * hist_stride + c] = tok;
+    if (en.x) {
+      en.tok_pos[m] += 1;
+      step_ctr[m] = c + 1;
     }
   }
 }
 
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   float temperature, int top_k, float top_p, uint32_t seed, const int* step_ctr, int* tok_out,
-                   int* tok_hist, int hist_stride, hipStream_t s) {
+                   float temperature, int top_k, float top_p, uint32_t seed, int* step_ctr, int* tok_out,
+                   int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s) {
+  FA_REQUIRE(!en || (step_ctr && en->tok_pos && en->qs && en->d && en->E % 32 == 0), "sample_tokens: embed-next args");
   hipLaunchKernelGGL(k_sample, dim3(M), dim3(1024), 0, s, logits, ldl, V, pval, pidx, n_part, temperature, top_k, top_p,
-                     seed, step_ctr, tok_out, tok_hist, hist_stride);
+                     seed, step_ctr, tok_out, tok_hist, hist_stride, en ? *en : EmbedNext{});
 }
+
+// Profiling aid: one wave spins for `us` microseconds (100 MHz reference clock), so an eager host that
+// enqueues a profiled decode step gets ahead of the GPU and the event pairs bracket back-to-back kernels.
+__global__ void k_delay(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+void gpu_delay_us(int us, hipStream_t s) { hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (uint64_t)us * 100); }
 
 // advance per-token positions / counters after a decode step
 __global__ void k_advance(int* __restrict__ tok_pos, int* __restrict__ step_ctr, int M) {
