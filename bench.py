@@ -217,6 +217,26 @@ def main():
     out = {}
     if rank == 0:
         out = headline(args, world, dt, dt_prof, prof, stage)
+    # ---- C5 leg (configs[4] on one GPU): the same clip with the fp16 encoder graph (02-Quantize-ONNX.py) and the
+    # 73-token prefix; the 8-GPU segment-parallel part is the driver's scaling run of the same entry point
+    m.engine.set_encoder_fp16(True)
+    step()
+    m.engine.synchronize()
+    barrier()
+    t5 = time.perf_counter()
+    st5 = np.zeros(6)
+    for _ in range(args.steps):
+        tm = step().timings
+        st5 += [tm.encode, tm.ctc, tm.prepare, tm.inject, tm.llm_generate, tm.align]
+    m.engine.synchronize()
+    dt5 = time.perf_counter() - t5
+    m.engine.set_encoder_fp16(False)
+    if rank == 0:
+        out["c5"] = {"workload": "configs[4] on 1 GPU: single 60 s clip, fp16 encoder graph + q8_0 LLM, 73-token prefix",
+                     "value": round(CLIP_S * args.steps / dt5, 3), "unit": "audio_s/s",
+                     "ms_per_step": round(dt5 / args.steps * 1e3, 3),
+                     "stage_ms": {k: round(v / args.steps * 1e3, 3) for k, v in zip(
+                         ["encode", "ctc", "prompt", "prefill", "generate", "align"], st5)}}
     eng.cleanup()
     if args.c3_batch > 0:
         try:

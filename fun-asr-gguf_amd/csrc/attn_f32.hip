@@ -20,6 +20,12 @@
 
 namespace fa {
 
+// fp16 encoder mode (C5): the attention output (an fp16 tensor in the float16 graph) rounded to fp16
+__device__ __forceinline__ float4 round_f16x4(float4 v) {
+  return make_float4(__half2float(__float2half_rn(v.x)), __half2float(__float2half_rn(v.y)),
+                     __half2float(__float2half_rn(v.z)), __half2float(__float2half_rn(v.w)));
+}
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -70,7 +76,7 @@ template <int D>
 __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
-                                                  const int* __restrict__ lens, float scale, int KS,
+                                                  const int* __restrict__ lens, float scale, int KS, int r16,
                                                   float* __restrict__ part, int* __restrict__ cnt) {
   using L = AttnLds<D>;
   constexpr int HD = D / 2;    // dims per lane half
@@ -197,6 +203,7 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
         const float inv = 1.0f / s_l[q];
         float4 v = *reinterpret_cast<const float4*>(so + q * L::OS + 4 * d4);
         v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+        if (r16) v = round_f16x4(v);
         *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
       }
     }
@@ -252,8 +259,9 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
       acc += w * ld_sc1_f4(rs, (k2 * PSZ + q * D + 4 * d4) * 4);
     }
     const float inv = 1.0f / s_l[q];
-    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) =
-        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (r16) v = round_f16x4(v);
+    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -271,7 +279,7 @@ int attn_f32_splits(int batch, int t_stride, int n_heads) {
 
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s) {
+              const AttnF32Work& wk, hipStream_t s, int r16) {
   const int KS = attn_f32_splits(batch, t_stride, n_heads);
   const int n_tiles = cdiv(t_stride, AQ) * n_heads * batch;
   if (KS > 1)
@@ -288,10 +296,10 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
   }
   if (head_dim == 128) {
     hipLaunchKernelGGL(k_attn_f32<128>, grid, dim3(256), AttnLds<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, r16, wk.part, wk.cnt);
   } else if (head_dim == 64) {
     hipLaunchKernelGGL(k_attn_f32<64>, grid, dim3(256), AttnLds<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, r16, wk.part, wk.cnt);
   } else {
     FA_REQUIRE(false, "attn_f32: head_dim must be 64 or 128");
   }

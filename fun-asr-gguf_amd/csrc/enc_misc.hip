@@ -5,18 +5,21 @@
 
 namespace fa {
 
+// fp16 encoder mode (C5): op outputs are fp16 values, held in f32
+__device__ __forceinline__ float r16e(float v, int r16) { return r16 ? __half2float(__float2half_rn(v)) : v; }
+
 // ---------------- F1: mean over valid samples (model_definition.py:277-278), partial sums per block
 constexpr int MEAN_PARTS = 64;
 
 __global__ void k_mean_partial(const float* __restrict__ pcm, int64_t stride, const int64_t* __restrict__ n_samples,
-                               float* __restrict__ partial) {
+                               float* __restrict__ partial, int r16) {
   const int b = blockIdx.y, p = blockIdx.x;
   const int64_t n = n_samples[b];
   const int64_t chunk = (n + MEAN_PARTS - 1) / MEAN_PARTS;
   const int64_t lo = p * chunk, hi = min(n, lo + chunk);
   const float* x = pcm + b * stride;
   float acc = 0.f;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += x[i];
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc += r16e(x[i], r16);
   __shared__ float red[4];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -26,13 +29,13 @@ __global__ void k_mean_partial(const float* __restrict__ pcm, int64_t stride, co
 
 // pre-emphasis into the 200/200 zero-padded STFT input xp[b][0 .. xp_stride) (model_definition.py:279-282, 255)
 __global__ void k_preemph_pad(const float* __restrict__ pcm, int64_t stride, const int64_t* __restrict__ n_samples,
-                              const float* __restrict__ partial, float* __restrict__ xp, int64_t xp_stride) {
+                              const float* __restrict__ partial, float* __restrict__ xp, int64_t xp_stride, int r16) {
   const int b = blockIdx.y;
   __shared__ float s_mean;
   if (threadIdx.x < 64) {
     float v = threadIdx.x < MEAN_PARTS ? partial[b * MEAN_PARTS + threadIdx.x] : 0.f;
     v = wave_sum(v);
-    if (threadIdx.x == 0) s_mean = v / (float)n_samples[b];
+    if (threadIdx.x == 0) s_mean = r16e(v / (float)n_samples[b], r16);
   }
   __syncthreads();
   const float mean = s_mean;
@@ -42,25 +45,25 @@ __global__ void k_preemph_pad(const float* __restrict__ pcm, int64_t stride, con
     int64_t t = i - 200;
     float v = 0.f;
     if (t >= 0 && t < n) {
-      float a = x[t] - mean;
-      v = t == 0 ? a : a - 0.97f * (x[t - 1] - mean);
+      const float a = r16e(r16e(x[t], r16) - mean, r16);
+      v = t == 0 ? a : r16e(a - r16e(0.97f * r16e(r16e(x[t - 1], r16) - mean, r16), r16), r16);
     }
     xp[b * xp_stride + i] = v;
   }
 }
 
 void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,
-                      float* xp, int64_t xp_stride, hipStream_t s) {
-  hipLaunchKernelGGL(k_mean_partial, dim3(MEAN_PARTS, batch), dim3(256), 0, s, pcm, stride, d_n_samples, partial);
+                      float* xp, int64_t xp_stride, hipStream_t s, int r16) {
+  hipLaunchKernelGGL(k_mean_partial, dim3(MEAN_PARTS, batch), dim3(256), 0, s, pcm, stride, d_n_samples, partial, r16);
   hipLaunchKernelGGL(k_preemph_pad, dim3(cdiv(xp_stride, 256 * 8), batch), dim3(256), 0, s, pcm, stride, d_n_samples,
-                     partial, xp, xp_stride);
+                     partial, xp, xp_stride, r16);
 }
 
 // ---------------- F4: LFR (m=7, n=6) with replicate padding, mask, x*sqrt(512) + PE (model_definition.py:290-311, 206)
 // x[b, i, j*80 + c] = mel[b, clamp(6i + j - 3, 0, t_mel_valid-1), c] for i < t_lfr_valid else 0; then *22.627417 + pe[i].
 __global__ void k_lfr_pe(const float* __restrict__ mel, int mel_stride, const int* __restrict__ t_mel_valid,
                          const int* __restrict__ t_lfr_valid, const float* __restrict__ pe, float* __restrict__ x,
-                         int t_stride, int n_mels, int lfr_m, int lfr_n) {
+                         int t_stride, int n_mels, int lfr_m, int lfr_n, int r16) {
   const int b = blockIdx.y;
   const int d_in = n_mels * lfr_m;
   const int64_t total = (int64_t)t_stride * d_in;
@@ -75,22 +78,23 @@ __global__ void k_lfr_pe(const float* __restrict__ mel, int mel_stride, const in
       p = p < 0 ? 0 : (p > tmv - 1 ? tmv - 1 : p);
       v = mel[((int64_t)b * mel_stride + p) * n_mels + c];
     }
-    x[((int64_t)b * t_stride + i) * d_in + jc] = v * sq + pe[(int64_t)i * d_in + jc];
+    x[((int64_t)b * t_stride + i) * d_in + jc] =
+        r16e(r16e(v * r16e(sq, r16), r16) + r16e(pe[(int64_t)i * d_in + jc], r16), r16);
   }
 }
 
 void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, const int* t_lfr_valid, const float* pe,
-                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s) {
+                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s, int r16) {
   int64_t total = (int64_t)t_stride * n_mels * lfr_m;
   hipLaunchKernelGGL(k_lfr_pe, dim3(std::min(cdiv(total, 256), 4096), batch), dim3(256), 0, s, mel, mel_stride,
-                     t_mel_valid, t_lfr_valid, pe, x, t_stride, n_mels, lfr_m, lfr_n);
+                     t_mel_valid, t_lfr_valid, pe, x, t_stride, n_mels, lfr_m, lfr_n, r16);
 }
 
 // ---------------- E1: LayerNorm, one wave per row, optional row-mask sweep (model_definition.py:209-213)
 template <int PER>
 __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
                             const float* __restrict__ w, const float* __restrict__ bb, int rows, int D, float eps,
-                            const int* __restrict__ lens, int t_stride) {
+                            const int* __restrict__ lens, int t_stride, int r16) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -121,22 +125,22 @@ __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __r
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     int c = lane + i * 64;
-    if (c < D) yr[c] = ((v[i] - mean) * rstd * w[c] + bb[c]) * mk;
+    if (c < D) yr[c] = r16e((v[i] - mean) * rstd * w[c] + bb[c], r16) * mk;
   }
 }
 
 void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
-               float eps, const int* lens, int t_stride, hipStream_t s) {
+               float eps, const int* lens, int t_stride, hipStream_t s, int r16) {
   dim3 grid(cdiv(rows, 4));
-  if (D <= 512) hipLaunchKernelGGL(k_layernorm<8>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
-  else if (D <= 640) hipLaunchKernelGGL(k_layernorm<10>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
-  else if (D <= 1024) hipLaunchKernelGGL(k_layernorm<16>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride);
+  if (D <= 512) hipLaunchKernelGGL(k_layernorm<8>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
+  else if (D <= 640) hipLaunchKernelGGL(k_layernorm<10>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
+  else if (D <= 1024) hipLaunchKernelGGL(k_layernorm<16>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
   else FA_REQUIRE(false, "layernorm: D > 1024");
 }
 
 // ---------------- E4: FSMN memory = depthwise conv_k(v*m) (zero pad (k-1)/2) + v*m (model_definition.py:60-66)
 __global__ void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w, float* __restrict__ out,
-                       int64_t ldo, int rows, int C, int ksize, const int* __restrict__ lens, int t_stride) {
+                       int64_t ldo, int rows, int C, int ksize, const int* __restrict__ lens, int t_stride, int r16) {
   const int64_t total = (int64_t)rows * C;
   const int lp = (ksize - 1) / 2;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -147,18 +151,18 @@ __global__ void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __
     for (int j = 0; j < ksize; ++j) {
       int tt = t + j - lp;
       float xv = (tt >= 0 && tt < len && tt < t_stride) ? v[((int64_t)b * t_stride + tt) * ldv + c] : 0.f;
-      acc += w[c * ksize + j] * xv;
+      acc += r16e(w[c * ksize + j], r16) * xv;
     }
     float self = t < len ? v[(int64_t)row * ldv + c] : 0.f;
-    out[(int64_t)row * ldo + c] = acc + self;
+    out[(int64_t)row * ldo + c] = r16e(r16e(acc, r16) + self, r16);
   }
 }
 
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
-          const int* lens, int t_stride, hipStream_t s) {
+          const int* lens, int t_stride, hipStream_t s, int r16) {
   int64_t total = (int64_t)rows * C;
   hipLaunchKernelGGL(k_fsmn, dim3(std::min(cdiv(total, 256), 8192)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
-                     ksize, lens, t_stride);
+                     ksize, lens, t_stride, r16);
 }
 
 // ---------------- C2: CTC greedy collapse (nano_ctc.py:65-104): keep frame i iff id != blank and

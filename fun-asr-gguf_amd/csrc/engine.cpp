@@ -253,7 +253,46 @@ struct Engine {
   void lin(const std::string& p, int n_in, int n_out, float* w, float* b) {
     add_f32(p + ".weight", (int64_t)n_in * n_out, lin_scale(n_in), 0.f, w);
     if (b) add_f32(p + ".bias", n_out, 0.02f, 0.f, b);
+    gemm_w.push_back({w, (int64_t)n_in * n_out});
   }
+
+  // ---- fp16 encoder mode (C5: the reference's float16 ONNX graphs, 02-Quantize-ONNX.py:13-27). Every GEMM weight
+  // gets an fp16 copy in one arena, in registration order (the adaptor's q|k|v sub-matrices stay contiguous), built
+  // on the first fp16 encode after weights change.
+  struct WRegion {
+    const float* w;
+    int64_t n;
+  };
+  std::vector<WRegion> gemm_w;
+  bool enc_fp16 = false, w16_stale = true;
+  __half* w16_arena = nullptr;
+  std::unordered_map<const float*, const __half*> w16;
+  float *basis16 = nullptr, *fbank16 = nullptr;  // frontend initializers as fp16 values (held in f32)
+
+  void prepare_fp16() {
+    if (!w16_stale) return;
+    int64_t total = 0;
+    for (const WRegion& r : gemm_w) total += r.n;
+    if (!w16_arena) w16_arena = alloc<__half>((size_t)total);
+    int64_t off = 0;
+    for (const WRegion& r : gemm_w) {
+      launch_f2h_initializer(r.w, w16_arena + off, nullptr, r.n, stream);
+      w16[r.w] = w16_arena + off;
+      off += r.n;
+    }
+    if (!basis16) basis16 = alloc<float>((size_t)402 * 400);
+    if (!fbank16) fbank16 = alloc<float>((size_t)80 * 204);
+    launch_f2h_initializer(basis, nullptr, basis16, (int64_t)402 * 400, stream);
+    launch_f2h_initializer(fbank, nullptr, fbank16, (int64_t)80 * 204, stream);
+    w16_stale = false;
+  }
+  const __half* W16(const float* W) const {
+    if (!enc_fp16) return nullptr;
+    auto it = w16.find(W);
+    FA_REQUIRE(it != w16.end(), "fp16 encoder: GEMM weight without an fp16 copy");
+    return it->second;
+  }
+  int r16() const { return enc_fp16 ? 1 : 0; }
 
   EncBlockW sanm_block(const std::string& p, int d_in) {
     const int d = ec.d_model, f = ec.d_ffn, k = ec.fsmn_k;
@@ -587,7 +626,7 @@ struct Engine {
                int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0) {
     hipEvent_t ev;
     prof_begin(1, &ev);
-    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream);
+    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W));
     prof_end(1, 0, 2.0 * M * N * K);
   }
 
@@ -596,14 +635,14 @@ struct Engine {
     const float* xin = first ? hbuf : xa;  // block0 input = PE'd LFR features (hbuf holds them)
     float* x = xa;
     // LN1
-    layernorm(first ? xin : x, w.d_in, att, w.d_in, w.ln1_w, w.ln1_b, rows, w.d_in, 1e-5f, nullptr, ts, stream);
+    layernorm(first ? xin : x, w.d_in, att, w.d_in, w.ln1_w, w.ln1_b, rows, w.d_in, 1e-5f, nullptr, ts, stream, r16());
     enc_lin(att, w.d_in, w.qkv_w, w.qkv_b, qkv, 3 * d, rows, 3 * d, w.d_in);
-    fsmn(qkv + 2 * d, 3 * d, w.fsmn_w, mem, d, rows, d, ec.fsmn_k, lens, ts, stream);
+    fsmn(qkv + 2 * d, 3 * d, w.fsmn_w, mem, d, rows, d, ec.fsmn_k, lens, ts, stream, r16());
     {
       hipEvent_t ev;
       prof_begin(2, &ev);
       attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.n_heads, d / ec.n_heads, lens,
-               enc_attn_wk, stream);
+               enc_attn_wk, stream, r16());
       prof_end(2, 0, 4.0 * rows * (double)ts * d);
     }
     if (first) {
@@ -611,7 +650,7 @@ struct Engine {
       return;
     }
     enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, x, d, mem, d);
-    layernorm(x, d, hbuf, d, w.ln2_w, w.ln2_b, rows, d, 1e-5f, nullptr, ts, stream);
+    layernorm(x, d, hbuf, d, w.ln2_w, w.ln2_b, rows, d, 1e-5f, nullptr, ts, stream, r16());
     enc_lin(hbuf, d, w.w1, w.b1, ffn, ec.d_ffn, rows, ec.d_ffn, d, 1);
     enc_lin(ffn, ec.d_ffn, w.w2, w.b2, x, d, rows, d, ec.d_ffn, 0, x, d);
   }
@@ -622,17 +661,17 @@ struct Engine {
     enc_lin(in, d_enc, a.l1_w, a.l1_b, ffn, d_ffn, rows, d_ffn, d_enc, 1);
     enc_lin(ffn, d_ffn, a.l2_w, a.l2_b, out, d_out, rows, d_out, d_ffn);
     for (const AdBlockW& b : a.blocks) {
-      layernorm(out, d_out, hbuf, d_out, b.ln1_w, b.ln1_b, rows, d_out, 1e-12f, nullptr, ts, stream);
+      layernorm(out, d_out, hbuf, d_out, b.ln1_w, b.ln1_b, rows, d_out, 1e-12f, nullptr, ts, stream, r16());
       enc_lin(hbuf, d_out, b.qkv_w, b.qkv_b, qkv, 3 * d_out, rows, 3 * d_out, d_out);
       {
         hipEvent_t ev;
         prof_begin(2, &ev);
         attn_f32(qkv, qkv + d_out, qkv + 2 * d_out, 3 * d_out, 3 * d_out, 3 * d_out, att, d_out, rows / ts, ts, n_heads,
-                 d_out / n_heads, lens, enc_attn_wk, stream);
+                 d_out / n_heads, lens, enc_attn_wk, stream, r16());
         prof_end(2, 0, 4.0 * rows * (double)ts * d_out);
       }
       enc_lin(att, d_out, b.o_w, b.o_b, out, d_out, rows, d_out, d_out, 0, out, d_out);
-      layernorm(out, d_out, hbuf, d_out, b.ln2_w, b.ln2_b, rows, d_out, 1e-12f, nullptr, ts, stream);
+      layernorm(out, d_out, hbuf, d_out, b.ln2_w, b.ln2_b, rows, d_out, 1e-12f, nullptr, ts, stream, r16());
       enc_lin(hbuf, d_out, b.w1, b.b1, ffn, d_out / 4, rows, d_out / 4, d_out, 1);
       enc_lin(ffn, d_out / 4, b.w2, b.b2, out, d_out, rows, d_out, d_out / 4, 0, out, d_out);
     }
@@ -669,15 +708,16 @@ struct Engine {
     FA_HIP(hipMemcpyAsync(d_tgt, h_tgt.data(), batch * 4, hipMemcpyHostToDevice, stream));
     FA_HIP(hipMemcpyAsync(d_ctclen, h_ctclen.data(), batch * 4, hipMemcpyHostToDevice, stream));
     // F1-F4
-    frontend_preemph(pcm, stride, d_nsamp, batch, mean_part, xp, xps, stream);
+    if (enc_fp16) prepare_fp16();
+    frontend_preemph(pcm, stride, d_nsamp, batch, mean_part, xp, xps, stream, r16());
     {
       hipEvent_t ev;
       prof_begin(1, &ev);
-      gemm_stft_power(xp, xps, tm_stride, batch * tm_stride, basis, power, 204, stream);
+      gemm_stft_power(xp, xps, tm_stride, batch * tm_stride, enc_fp16 ? basis16 : basis, power, 204, stream, r16());
       prof_end(1, 0, 2.0 * batch * tm_stride * 402.0 * 400.0);
     }
-    gemm_mel_log(power, 204, fbank, 204, mel, batch * tm_stride, ec.n_mels, 201, stream);
-    frontend_lfr(mel, tm_stride, d_tmel, d_tlfr, pe, hbuf, batch, ts, ec.n_mels, ec.lfr_m, ec.lfr_n, stream);
+    gemm_mel_log(power, 204, enc_fp16 ? fbank16 : fbank, 204, mel, batch * tm_stride, ec.n_mels, 201, stream, r16());
+    frontend_lfr(mel, tm_stride, d_tmel, d_tlfr, pe, hbuf, batch, ts, ec.n_mels, ec.lfr_m, ec.lfr_n, stream, r16());
     if (debug_flags & 1) {
       if (!tap_lfr) tap_lfr = alloc<float>((size_t)tl_max * ec.d_in);
       // LFR features before the x*sqrt(512)+PE embed are not materialised; the tap holds the embedded rows
@@ -687,12 +727,13 @@ struct Engine {
     const int d = ec.d_model;
     for (size_t i = 0; i < enc_blocks.size(); ++i) {
       if ((int)i == ec.n_blocks) {
-        layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream);
+        layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream, r16());
       }
       sanm(enc_blocks[i], rows, ts, d_tlfr, i == 0);
     }
-    if ((int)enc_blocks.size() == ec.n_blocks) layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream);
-    layernorm(xa, d, enc, d, tp_w, tp_b, rows, d, 1e-5f, d_tlfr, ts, stream);
+    if ((int)enc_blocks.size() == ec.n_blocks)
+      layernorm(xa, d, xa, d, after_w, after_b, rows, d, 1e-5f, d_tlfr, ts, stream, r16());
+    layernorm(xa, d, enc, d, tp_w, tp_b, rows, d, 1e-5f, d_tlfr, ts, stream, r16());
     // adaptor (key mask = valid frames) -> ad [rows][d_llm]
     run_adaptor(adaptor, enc, d, ec.d_llm, ec.adaptor_ffn, ec.adaptor_heads, ad, rows, ts, d_tlfr);
     // CTC head (reference: unmasked over the clip's own frames -> key length = ctc_len)
@@ -700,7 +741,7 @@ struct Engine {
     {
       hipEvent_t ev;
       prof_begin(1, &ev);
-      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, rows, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream);
+      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, rows, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w));
       prof_end(1, 0, 2.0 * rows * (double)ec.ctc_vocab * d);
     }
   }
@@ -927,6 +968,7 @@ int fa_engine_destroy(fa_engine* h) {
 int fa_weights_synthetic(fa_engine* h, uint32_t seed) {
   FA_API_BEGIN
   h->e->synthetic(seed);
+  h->e->w16_stale = true;
   FA_API_END
 }
 
@@ -937,6 +979,7 @@ int fa_set_tensor_f32(fa_engine* h, const char* name, const float* host, int64_t
   FA_REQUIRE(n == s.n, std::string("size mismatch for ") + name);
   if (s.kind == 0) {
     FA_HIP(hipMemcpyAsync(s.f, host, n * 4, hipMemcpyHostToDevice, e->stream));
+    e->w16_stale = true;
   } else {
     float* tmp = nullptr;
     FA_HIP(hipMalloc(&tmp, n * 4));
@@ -1098,6 +1141,12 @@ int fa_ctc_collapse(fa_engine* h, int32_t blank_id, int32_t* ids_out, int32_t* f
     n_out[b] = n[b];
   }
   FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_set_encoder_fp16(fa_engine* h, int32_t on) {
+  FA_API_BEGIN
+  h->e->enc_fp16 = on != 0;
   FA_API_END
 }
 

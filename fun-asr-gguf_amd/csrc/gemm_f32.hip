@@ -6,12 +6,16 @@
 // Used for every encoder/adaptor/CTC projection, the STFT-as-DFT-GEMM (F2) with a
 // power epilogue (F3), the mel projection with a log epilogue, and the CTC projection with a fused
 // row-argmax epilogue (C1) so the [T, 60515] logits never reach HBM.
+#include <algorithm>
 #include "common.h"
 #include "kernels.h"
 
 namespace fa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// fp16 encoder mode (C5, the reference's float16 ONNX graphs): every op's output is an fp16 value; held in f32
+__device__ __forceinline__ float r16v(float v, int r16) { return r16 ? __half2float(__float2half_rn(v)) : v; }
 
 constexpr int BK = 32;
 
@@ -117,19 +121,20 @@ struct EpiLinear {
   const float* add2;  // e.g. FSMN memory (added before the residual, model_definition.py:90,109)
   int64_t ld2;
   int relu;
+  int r16;            // fp16 mode: Gemm (+bias) output, then each Add, rounded to fp16
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
     if (col >= N) return;
-    float b = bias ? bias[col] : 0.f;
+    float b = bias ? r16v(bias[col], r16) : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (row < M) {
-        float v = acc[r] + b;
+        float v = r16v(acc[r] + b, r16);
         if (relu) v = fmaxf(v, 0.f);
-        if (add2) v = v + add2[(int64_t)row * ld2 + col];
-        if (add1) v = add1[(int64_t)row * ld1 + col] + v;
+        if (add2) v = r16v(v + add2[(int64_t)row * ld2 + col], r16);
+        if (add1) v = r16v(add1[(int64_t)row * ld1 + col] + v, r16);
         C[(int64_t)row * ldc + col] = v;
       }
     }
@@ -140,6 +145,7 @@ struct EpiLinear {
 struct EpiPower {
   float* P;
   int64_t ldp;
+  int r16;
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
@@ -148,7 +154,10 @@ struct EpiPower {
       float v = acc[r];
       float o = __shfl_xor(v, 1, 64);
       int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (!(lane & 1) && row < M && col < N) P[(int64_t)row * ldp + (col >> 1)] = v * v + o * o;
+      if (!(lane & 1) && row < M && col < N) {
+        const float re = r16v(v, r16), im = r16v(o, r16);
+        P[(int64_t)row * ldp + (col >> 1)] = r16v(r16v(re * re, r16) + r16v(im * im, r16), r16);
+      }
     }
   }
 };
@@ -157,6 +166,7 @@ struct EpiPower {
 struct EpiLog {
   float* C;
   int64_t ldc;
+  int r16;
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
@@ -164,7 +174,7 @@ struct EpiLog {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < M) C[(int64_t)row * ldc + col] = logf(acc[r] + 1e-7f);
+      if (row < M) C[(int64_t)row * ldc + col] = r16v(logf(r16v(r16v(acc[r], r16) + r16v(1e-7f, r16), r16)), r16);
     }
   }
 };
@@ -175,16 +185,17 @@ struct EpiArgmax {
   float* pval;   // [M][n_tiles]
   int* pidx;
   int n_tiles;
+  int r16;  // fp16 mode: argmax over fp16 logits (ties resolve to the first index, as on the rounded values)
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int col = col0 + (lane & 31);
-    float b = col < N ? bias[col] : 0.f;
+    float b = col < N ? r16v(bias[col], r16) : 0.f;
     float* sv = lds;                              // [64 rows][2]
     int* si = reinterpret_cast<int*>(lds + 128);  // [64][2]
     int wr = wave >> 1, wc = wave & 1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float v = col < N ? acc[r] + b : -INFINITY;
+      float v = col < N ? r16v(acc[r] + b, r16) : -INFINITY;
       int i = col < N ? col : 0x7fffffff;
 #pragma unroll
       for (int o = 16; o >= 1; o >>= 1) {
@@ -286,25 +297,142 @@ static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, in
     launch_gemm<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp16 encoder GEMM (C5): v_mfma_f32_32x32x16_f16, f16 x f16 products exact in the f32 accumulator. A comes from
+// the f32 activation buffers (fp16 values in fp16 mode) and is converted while staged; W is the fp16 copy of the
+// weight. Lane l holds A[i = l&31][k = 8 (l>>5) + 0..7] (one 16-B LDS read), B likewise; the accumulator layout is
+// that of the f32 kernel, so the same epilogues apply. LDS rows of 40 halves (80 B): the 16 rows a 16-lane group
+// reads start in 16 distinct 4-bank groups (20 r mod 64), conflict-free.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int LDKH = BK + 8;
+template <int WM, int WN>
+struct Tile16 {
+  static constexpr int BM = 64 * WM, BN = 64 * WN;
+  static constexpr int NA = BM * BK / 4 / 256;    // float4 of A per thread
+  static constexpr int NB = BN * BK / 8 / 256;    // 8 halves of W per thread
+  static constexpr int STAGE = (BM + BN) * LDKH;  // halves per LDS stage
+};
+
+template <class AL, int WM, int WN>
+__device__ __forceinline__ void load16(const AL& al, const __half* __restrict__ W, int64_t ldw, int m0, int n0, int k0,
+                                       int M, int N, int K, float4 (&ra)[Tile16<WM, WN>::NA],
+                                       uint4 (&rb)[Tile16<WM, WN>::NB]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < Tile16<WM, WN>::NA; ++i) {
+    const int idx = t + i * 256;  // (row idx >> 3, k4 idx & 7)
+    ra[i] = al.load4(m0 + (idx >> 3), k0 + 4 * (idx & 7), M, K);
+  }
+#pragma unroll
+  for (int i = 0; i < Tile16<WM, WN>::NB; ++i) {
+    const int idx = t + i * 256;  // (row idx >> 2, k8 idx & 3); K % 8 == 0
+    const int n = n0 + (idx >> 2), k = k0 + 8 * (idx & 3);
+    rb[i] = (n < N && k < K) ? *reinterpret_cast<const uint4*>(W + (int64_t)n * ldw + k) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int WM, int WN>
+__device__ __forceinline__ void store16(_Float16* As, _Float16* Bs, const float4 (&ra)[Tile16<WM, WN>::NA],
+                                        const uint4 (&rb)[Tile16<WM, WN>::NB]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < Tile16<WM, WN>::NA; ++i) {
+    const int idx = t + i * 256;
+    const f16x4 v = {(_Float16)ra[i].x, (_Float16)ra[i].y, (_Float16)ra[i].z, (_Float16)ra[i].w};
+    *reinterpret_cast<f16x4*>(As + (idx >> 3) * LDKH + 4 * (idx & 7)) = v;
+  }
+#pragma unroll
+  for (int i = 0; i < Tile16<WM, WN>::NB; ++i) {
+    const int idx = t + i * 256;
+    *reinterpret_cast<uint4*>(Bs + (idx >> 2) * LDKH + 8 * (idx & 3)) = rb[i];
+  }
+}
+
+template <class AL, class EPI, int WM, int WN>
+__global__ __launch_bounds__(256) void k_gemm_f16(AL al, const __half* __restrict__ W, int64_t ldw, int M, int N, int K,
+                                                  EPI epi) {
+  using T = Tile16<WM, WN>;
+  extern __shared__ float smem[];  // 2 stages x (A [BM][LDKH], W [BN][LDKH]) halves; the epilogue reuses it
+  _Float16* sh = reinterpret_cast<_Float16*>(smem);
+  const int m0 = blockIdx.y * T::BM, n0 = blockIdx.x * T::BN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  float4 ra[T::NA];
+  uint4 rb[T::NB];
+  load16<AL, WM, WN>(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
+  store16<WM, WN>(sh, sh + T::BM * LDKH, ra, rb);
+  __syncthreads();
+  const int nk = (K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load16<AL, WM, WN>(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
+    const _Float16* a = sh + cur * T::STAGE + (wr * 32 * WM + r) * LDKH + 8 * h;
+    const _Float16* b = sh + cur * T::STAGE + T::BM * LDKH + (wc * 32 * WN + r) * LDKH + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      f16x8 av[WM], bv[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) av[i] = *reinterpret_cast<const f16x8*>(a + 32 * i * LDKH + 16 * kk);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) bv[j] = *reinterpret_cast<const f16x8*>(b + 32 * j * LDKH + 16 * kk);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store16<WM, WN>(sh + (cur ^ 1) * T::STAGE, sh + (cur ^ 1) * T::STAGE + T::BM * LDKH, ra, rb);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+}
+
+template <class AL, class EPI, int WM, int WN>
+static void launch_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N, int K, const EPI& epi,
+                          hipStream_t s) {
+  using T = Tile16<WM, WN>;
+  FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_f16: K and ldw must be multiples of 8");
+  dim3 grid(cdiv(N, T::BN), cdiv(M, T::BM));
+  const size_t lds = std::max<size_t>(2 * T::STAGE * sizeof(_Float16), 1024);  // >= EpiArgmax scratch
+  hipLaunchKernelGGL((k_gemm_f16<AL, EPI, WM, WN>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi);
+}
+
+template <class AL, class EPI>
+static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
+  // 128x128 blocks once they still give every CU two; 64x64 otherwise
+  if ((int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512) launch_gemm16<AL, EPI, 2, 2>(al, W, ldw, M, N, K, epi, s);
+  else launch_gemm16<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);
+}
+
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s) {
+                 hipStream_t s, const __half* W16) {
   ALoadPlain al{A, lda};
-  EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu};
-  run_gemm(al, W, ldw, M, N, K, epi, s);
+  EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
+  if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
+  else run_gemm(al, W, ldw, M, N, K, epi, s);
 }
 
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
-                     int64_t ldp, hipStream_t s) {
+                     int64_t ldp, hipStream_t s, int r16) {
   ALoadFrames al{xp, xp_stride, t_stride, 160};
-  EpiPower epi{power, ldp};
+  EpiPower epi{power, ldp, r16};
   run_gemm(al, basis, 400, M, 402, 400, epi, s);
 }
 
 void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
-                  int n_freq, hipStream_t s) {
+                  int n_freq, hipStream_t s, int r16) {
   ALoadPlain al{power, ldp};
-  EpiLog epi{mel, n_mels};
+  EpiLog epi{mel, n_mels, r16};
   run_gemm(al, fbank, ldf, M, n_mels, n_freq, epi, s);
 }
 
@@ -326,11 +454,13 @@ __global__ void k_argmax_final(const float* __restrict__ pval, const int* __rest
 }
 
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
-                     int* pidx, int* out, hipStream_t s) {
+                     int* pidx, int* out, hipStream_t s, const __half* W16) {
   int n_tiles = cdiv(N, 64);
   ALoadPlain al{A, lda};
-  EpiArgmax epi{bias, pval, pidx, n_tiles};
-  run_gemm(al, W, K, M, N, K, epi, s, false);  // the argmax epilogue reduces 64-column blocks
+  EpiArgmax epi{bias, pval, pidx, n_tiles, W16 ? 1 : 0};
+  // the argmax epilogue reduces 64-column blocks
+  if (W16) launch_gemm16<ALoadPlain, EpiArgmax, 1, 1>(al, W16, K, M, N, K, epi, s);
+  else run_gemm(al, W, K, M, N, K, epi, s, false);
   hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
 }
 

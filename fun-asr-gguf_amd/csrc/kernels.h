@@ -17,17 +17,20 @@ void launch_quant_q8_0(const float* x, int64_t n, int8_t* qs, __half* d, hipStre
 void launch_unpack_q8_0(const uint8_t* blocks, int64_t n_blocks, int8_t* qs, __half* d, hipStream_t s);
 void launch_pack_q8_0(const int8_t* qs, const __half* d, int64_t n_blocks, uint8_t* blocks, hipStream_t s);
 void launch_h2f(const __half* a, float* b, int64_t n, hipStream_t s);
+// float16-ONNX initializer conversion (clamp to [1e-7, 65504] magnitude, RN): f16 copy b and/or its f32 value b32
+void launch_f2h_initializer(const float* a, __half* b, float* b32, int64_t n, hipStream_t s);
 
 // gemm_f32.hip
+// W16 != nullptr: fp16 mode (C5) on the f16 MFMA kernel with the fp16 weight copy W16, every op output rounded to fp16
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s);
+                 hipStream_t s, const __half* W16 = nullptr);
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
-                     int64_t ldp, hipStream_t s);
+                     int64_t ldp, hipStream_t s, int r16 = 0);
 void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
-                  int n_freq, hipStream_t s);
+                  int n_freq, hipStream_t s, int r16 = 0);
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
-                     int* pidx, int* out, hipStream_t s);
+                     int* pidx, int* out, hipStream_t s, const __half* W16 = nullptr);
 
 // attn_f32.hip
 // Key-split workspace of the encoder attention (used only while (query tile, head, clip) blocks leave the
@@ -44,17 +47,17 @@ constexpr int64_t ATTN_F32_COUNTERS = 512;
 int attn_f32_splits(int batch, int t_stride, int n_heads);
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s);
+              const AttnF32Work& wk, hipStream_t s, int r16 = 0);
 
 // enc_misc.hip
 void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,
-                      float* xp, int64_t xp_stride, hipStream_t s);
+                      float* xp, int64_t xp_stride, hipStream_t s, int r16 = 0);
 void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, const int* t_lfr_valid, const float* pe,
-                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s);
+                  float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s, int r16 = 0);
 void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
-               float eps, const int* lens, int t_stride, hipStream_t s);
+               float eps, const int* lens, int t_stride, hipStream_t s, int r16 = 0);
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
-          const int* lens, int t_stride, hipStream_t s);
+          const int* lens, int t_stride, hipStream_t s, int r16 = 0);
 void ctc_collapse(const int* ids, int64_t ids_stride, const int* lens, int batch, int blank, int* out_ids,
                   int* out_frames, int64_t out_stride, int* n_out, hipStream_t s);
 

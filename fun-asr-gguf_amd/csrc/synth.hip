@@ -105,4 +105,22 @@ void launch_h2f(const __half* a, float* b, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_h2f, dim3(cdiv(n, 256)), dim3(256), 0, s, a, b, n);
 }
 
+// f32 -> f16 as the float16 ONNX converter does for initializers (onnxruntime.transformers.float16,
+// 02-Quantize-ONNX.py:21-27: min_positive_val 1e-7, max_finite_val 65504): nonzero magnitudes below 1e-7 become
+// +-1e-7, magnitudes above 65504 become +-65504, then round to nearest even. round_only: plain RN (activations).
+__global__ void k_f2h(const float* __restrict__ a, __half* __restrict__ b, float* __restrict__ b32, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = a[i];
+  const float m = fabsf(v);
+  if (m > 0.f && m < 1e-7f) v = copysignf(1e-7f, v);
+  if (m > 65504.f) v = copysignf(65504.f, v);
+  const __half h = __float2half_rn(v);
+  if (b) b[i] = h;
+  if (b32) b32[i] = __half2float(h);
+}
+void launch_f2h_initializer(const float* a, __half* b, float* b32, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_f2h, dim3(cdiv(n, 256)), dim3(256), 0, s, a, b, b32, n);
+}
+
 }  // namespace fa

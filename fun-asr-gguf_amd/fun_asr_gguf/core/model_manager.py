@@ -79,6 +79,7 @@ class ModelManager:
             self.engine = _native.Engine(self.enc_cfg, self.llm_cfg, max_batch=max(1, c.max_batch),
                                          max_samples=c.sample_rate * 64, device=c.device)
             self.engine.synthetic_weights(c.synthetic_seed)
+            self.engine.set_encoder_fp16(c.encoder_fp16())
             if not _is_synthetic(c.encoder_onnx_path):
                 if str(c.encoder_onnx_path).endswith(".onnx"):
                     raise NotImplementedError("ONNX initializer ingestion is not implemented; pass model.pt")

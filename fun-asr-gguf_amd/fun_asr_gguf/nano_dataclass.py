@@ -5,6 +5,7 @@ Field names, defaults and semantics mirror /root/reference/fun_asr_gguf/nano_dat
 ASREngineConfig :132-165, CTCResult :170-184, Statistics :189-221, DecodeResult :224-249,
 LLMDecodeResult :252-268). Additive fields only (marked "MI355X").
 """
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
@@ -90,6 +91,16 @@ class ASREngineConfig:
     model: str = "full"            # "full" (Fun-ASR-Nano dims) or "tiny" (test dims)
     synthetic_seed: int = 0
     ignore_eos: bool = False       # benchmark protocol: pin the decode length (no stop tokens, no breaker)
+    # encoder graph precision: "auto" follows the reference's file naming (*.fp16.onnx -> the float16 graph of
+    # 02-Quantize-ONNX.py; anything else fp32), or "fp32" / "fp16" explicitly
+    encoder_precision: str = "auto"
+
+    def encoder_fp16(self) -> bool:
+        if self.encoder_precision in ("fp16", "fp32"):
+            return self.encoder_precision == "fp16"
+        if self.encoder_precision != "auto":
+            raise ValueError(f"encoder_precision must be auto, fp32 or fp16, not {self.encoder_precision!r}")
+        return ".fp16." in os.path.basename(str(self.encoder_onnx_path))
 
 
 @dataclass

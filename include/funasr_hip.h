@@ -99,6 +99,10 @@ int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* f
                     int32_t* n_out);
 /* Debug hooks (tests): flags bit 0 keeps clip 0's embedded LFR features (x*sqrt(512)+PE, [T, d_in]) of
  * the next fa_encode; fa_encode_tap(e, 0, out, n) copies them out. */
+/* Encoder precision: 0 = fp32 graph (Fun-ASR-Nano-Encoder-Adaptor.fp32.onnx / CTC.fp32.onnx), 1 = the float16
+ * graphs of 02-Quantize-ONNX.py:13-27 (fp16 weights and op outputs, LayerNorm in fp32, fp16 input audio;
+ * replaces the dtype switch of nano_onnx.py:84,101). The fp16 weight copies are built on the next encode. */
+int fa_set_encoder_fp16(fa_engine* e, int32_t on);
 int fa_set_debug(fa_engine* e, int32_t flags);
 int fa_encode_tap(fa_engine* e, int32_t which, float* out, int64_t n);
 

@@ -103,6 +103,37 @@ def test_encoder_padded_batch_equals_unpadded(tiny_engine, enc_w_tiny):
         assert ((out["ctc_ids"][i] != r["ctc_ids"]) & nontie).sum() == 0, i
 
 
+# fp16 encoder graph (C5): GPU vs oracle/encoder_fp16 (same fp16 rounding points; differences are f32
+# accumulation order, i.e. occasional 1-ulp fp16 flips), and loosely vs the fp32 reference golden.
+FP16_REL, FP16_COS = 1e-2, 0.99995
+
+
+def test_encoder_fp16_graph_vs_oracle(tiny_engine, enc_w_tiny):
+    from oracle import encoder_fp16 as oe16
+    g = np.load(os.path.join(GOLDEN, "encoder_tiny_3s.npz"))
+    valid = int(g["valid"])
+    audio = g["audio"][:valid]
+    tiny_engine.set_encoder_fp16(True)
+    try:
+        out = tiny_engine.encode([audio], want_enc=True)
+    finally:
+        tiny_engine.set_encoder_fp16(False)
+    r = oe16.encode(audio, enc_w_tiny, synth.ENC_TINY)
+    T = int(g["t_lfr_valid"])
+    enc, emb = out["enc"][0][:T], out["audio_embd"][0]
+    assert (emb.astype(np.float16).astype(np.float32) == emb).all()  # fp16 values
+    assert _rel(enc, r["enc"][:T]) < FP16_REL and _cos(enc, r["enc"][:T]) > FP16_COS
+    assert _rel(emb, r["audio_embd"]) < FP16_REL and _cos(emb, r["audio_embd"]) > FP16_COS
+    assert _cos(emb, g["adaptor"]) > 0.9995  # fp32 reference, fp16 accuracy
+    lg = r["ctc_logits"][:T]
+    top2 = np.sort(lg, -1)[:, -2:]
+    nontie = (top2[:, 1] - top2[:, 0]) > 0.05
+    assert ((out["ctc_ids"][0][:T] != r["ctc_ids"][:T]) & nontie).sum() == 0
+    # the engine is back on the fp32 graph: bit-for-bit the result it gave before the switch
+    out32 = tiny_engine.encode([audio], want_enc=True)
+    assert _rel(out32["audio_embd"][0], g["adaptor"]) < ENC_ATOL_TINY
+
+
 def test_ctc_collapse_matches_reference_rule(tiny_engine):
     from fun_asr_gguf.synthetic import synth_audio
     clips = [synth_audio(30000, 5), synth_audio(20000, 6)]

@@ -86,3 +86,20 @@ def test_qwen3_q8_noise_floor():
     b = m.forward(p + (rng.standard_normal(p.shape) * 1e-6).astype(np.float32), 0)
     cos = float(a @ b / np.linalg.norm(a) / np.linalg.norm(b))
     assert 0.9995 < cos < 1.0 and np.abs(a - b).max() > 1e-3
+
+
+def test_fp16_graph_oracle_tracks_fp32_reference():
+    """oracle/encoder_fp16 (the float16 ONNX graph restated: fp16 initializers and op outputs, LayerNorm in f32)
+    stays within fp16 accuracy of the reference's fp32 result (golden from model_definition.py). The fp16 graph
+    itself is parity-unpinned (no onnxruntime here); this bounds the restatement."""
+    from oracle import encoder_fp16 as e16
+    cfg = synth.ENC_TINY
+    g = np.load(os.path.join(GOLDEN, "encoder_tiny_3s.npz"))
+    W = synth.make_weights(synth.encoder_tensors(cfg))
+    r = e16.encode(g["audio"], W, cfg, valid=int(g["valid"]))
+    T = int(g["t_lfr_valid"])
+    assert _cos(r["enc"][:T], g["enc"][:T]) > 0.9995
+    assert _cos(r["audio_embd"], g["adaptor"]) > 0.9995
+    assert np.abs(r["audio_embd"] - g["adaptor"]).max() < 3e-2 * np.abs(g["adaptor"]).max()
+    # every output is an fp16 value
+    assert (r["audio_embd"].astype(np.float16).astype(np.float32) == r["audio_embd"]).all()
