@@ -126,8 +126,8 @@ struct Engine {
   int64_t seq_stride = 0, layer_stride = 0;
   int m_max = 0, n_part = 0, n_part_cur = 0;  // partial stride allocated / written by the last lm_head
   float *lx = nullptr, *lqkv = nullptr, *lq = nullptr, *latt = nullptr, *lact = nullptr, *logits = nullptr;
-  int8_t* lxq = nullptr;
-  float* lxd = nullptr;
+  int8_t *lxq = nullptr, *lxq2 = nullptr;
+  float *lxd = nullptr, *lxd2 = nullptr;
   float* pval = nullptr;
   int* pidx = nullptr;
   int *d_tok_seq = nullptr, *d_tok_pos = nullptr, *d_step = nullptr, *d_tok_cur = nullptr, *d_tok_hist = nullptr,
@@ -557,6 +557,8 @@ struct Engine {
     const int kmax = std::max({E, H * D, lc.n_ff});
     lxq = alloc<int8_t>((size_t)m_max * kmax);
     lxd = alloc<float>((size_t)m_max * kmax / 32);
+    lxq2 = alloc<int8_t>((size_t)m_max * kmax);  // q8_0 rows produced by epilogues (attention out, SwiGLU act)
+    lxd2 = alloc<float>((size_t)m_max * kmax / 32);
     logits = alloc<float>((size_t)lc.max_seqs * lc.n_vocab);
     n_part = std::max(lm_head_parts(lc.n_vocab, 1), lm_head_parts(lc.n_vocab, lc.max_seqs));
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
@@ -775,8 +777,10 @@ struct Engine {
         if (!decode)
           qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
                         seq_stride, stream);
+        // M > 4: the attention also leaves its rows as q8_0 blocks for the o GEMM (no prep launch)
         attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
-                   d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream);
+                   d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream, small ? nullptr : lxq2,
+                   small ? nullptr : lxd2);
         prof_end(3, 0, 0);
       }
       // x += Wo . attn
@@ -784,21 +788,25 @@ struct Engine {
       o.M = M; o.eps = lc.rms_eps; o.wq = w.o.q; o.wd = w.o.d; o.O = E; o.rpw = gemv_rows_per_wave(E);
       o.out = lx; o.ldo = E; o.res = lx; o.ldr = E;
       if (small) { o.x = latt; o.ldx = H * D; }
-      else { prep_q8(latt, H * D, nullptr, 0.f, M, H * D, lxq, lxd, stream); o.xq = lxq; o.xd = lxd; }
+      else { o.xq = lxq2; o.xd = lxd2; }
       gemv(o, H * D, 1);
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
       GemvArgs g{};
       g.M = M; g.eps = lc.rms_eps; g.wq = w.gate.q; g.wd = w.gate.d; g.wq2 = w.up.q; g.wd2 = w.up.d; g.O = F;
       g.rpw = gemv_rows_per_wave(F); g.out = lact; g.ldo = F;
       if (small) { g.x = lx; g.ldx = E; g.norm_w = w.ffn_norm; }
-      else { prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream); g.xq = lxq; g.xd = lxd; }
+      else {
+        prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream);
+        g.xq = lxq; g.xd = lxd;
+        g.qout = lxq2; g.dout = lxd2;  // SwiGLU epilogue quantises act for the down GEMM (no prep launch)
+      }
       gemv(g, E, 2);
       // x += Wdown . act
       GemvArgs dn{};
       dn.M = M; dn.eps = lc.rms_eps; dn.wq = w.down.q; dn.wd = w.down.d; dn.O = E; dn.rpw = gemv_rows_per_wave(E);
       dn.out = lx; dn.ldo = E; dn.res = lx; dn.ldr = E;
       if (small) { dn.x = lact; dn.ldx = F; }
-      else { prep_q8(lact, F, nullptr, 0.f, M, F, lxq, lxd, stream); dn.xq = lxq; dn.xd = lxd; }
+      else { dn.xq = lxq2; dn.xd = lxd2; }
       gemv(dn, F, 1);
     }
     prof_sample = true;

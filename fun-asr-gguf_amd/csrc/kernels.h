@@ -73,6 +73,7 @@ struct GemvArgs {
   int M, O, rpw;
   float* kpart; int64_t kpart_n;           // MFMA GEMM split-K workspace (floats) + arrival counters
   int* kcnt; int64_t kcnt_n;               //   (counters zeroed once; re-armed by the combining block)
+  int8_t* qout; float* dout;               // MFMA GEMM SwiGLU epilogue: also the q8_0 rows of out (next GEMM's input)
 };
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
@@ -94,9 +95,11 @@ struct AttnWork {
   float* partials = nullptr;  // [max_tokens][max_kv][ATTN_SPLITS][ATTN_PART_FLOATS]
   int max_tokens = 0, max_kv = 0;
 };
+// qout/dout (optional): the output rows also as q8_0 blocks (the o GEMM's pre-quantised input, no prep launch)
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s);
+                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout = nullptr,
+                float* dout = nullptr);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 // Decode-step tail fused into the sampler: embedding row of the sampled token -> x (the next step's input), and

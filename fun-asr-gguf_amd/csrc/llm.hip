@@ -502,6 +502,7 @@ __global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K)
   }
   // fixed-order reduction over the waves of each matrix; thread t finalises regs [2 (t>>6), +2) of lane t&63
   __shared__ float s_red[KW_WAVES][16][64];
+  __shared__ float s_act[EPI == 2 ? 32 : 1][33];  // SwiGLU tile [token][row] for the q8_0 epilogue
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
   __syncthreads();
@@ -517,12 +518,42 @@ __global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K)
 #pragma unroll
       for (int w = NWM; w < KW_WAVES; ++w) y2 += s_red[w][reg][l];
     }
-    const int row = o0 + (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
+    const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5), row = o0 + rrow;
+    float v = 0.f;
     if (row < a.O && tok < a.M) {
       float* op = a.out + (int64_t)tok * a.ldo + row;
       if (EPI == 0) *op = y;
       else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y;
-      else *op = (y / (1.0f + expf(-y))) * y2;
+      else *op = v = (y / (1.0f + expf(-y))) * y2;
+    }
+    if (EPI == 2) s_act[col][rrow] = v;
+  }
+  if (EPI == 2 && a.qout) {
+    // the tile's 32 rows of a token are one q8_0 block of the down projection's input: quantise it here, exactly
+    // as norm_quant_row does (no prep launch); thread t < 64: token t & 31, rows [16 (t >> 5), +16)
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int tk = threadIdx.x & 31, hh = threadIdx.x >> 5;
+      float vv[16], am = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        vv[i] = s_act[tk][16 * hh + i];
+        am = fmaxf(am, fabsf(vv[i]));
+      }
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const float d = am / 127.0f;
+      const float id = d != 0.0f ? 1.0f / d : 0.0f;
+      int32_t pk[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b0 = (int)roundf(__fmul_rn(vv[4 * j], id)) & 0xFF, b1 = (int)roundf(__fmul_rn(vv[4 * j + 1], id)) & 0xFF;
+        const int b2 = (int)roundf(__fmul_rn(vv[4 * j + 2], id)) & 0xFF, b3 = (int)roundf(__fmul_rn(vv[4 * j + 3], id)) & 0xFF;
+        pk[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      }
+      if (t0 + tk < a.M) {
+        *reinterpret_cast<int4*>(a.qout + (int64_t)(t0 + tk) * a.ldo + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+        if (hh == 0) a.dout[(int64_t)(t0 + tk) * (a.ldo / 32) + o0 / 32] = __half2float(__float2half_rn(d));
+      }
     }
   }
 }
@@ -598,6 +629,8 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     case 2: hipLaunchKernelGGL(k_gemm_q8_mfma<2>, grid, dim3(256), 0, s, a, K, KS); break;
     case 3: hipLaunchKernelGGL(k_gemm_q8_mfma<3>, grid, dim3(256), 0, s, a, K, KS); break;
   }
+  // this kernel has no quantising epilogue: produce the requested q8_0 rows of out with a prep launch
+  if (a.qout) prep_q8(a.out, a.ldo, nullptr, 0.f, a.M, a.O, a.qout, a.dout, s);
 }
 
 int lm_head_parts(int O, int M) { return M <= 4 ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
@@ -837,6 +870,19 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
   }
 }
 
+// q8_0 quantisation of an attention output row held 4 dims per lane (lanes 8b..8b+7 = one 32-dim block): the
+// o projection's input, with the arithmetic of norm_quant_row (no prep launch). e = element index of v.x.
+__device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* __restrict__ dout, int64_t e, int lane,
+                                              float4 v) {
+  const float a = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  const float d = a / 127.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  const int b0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, b1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
+  const int b2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, b3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
+  *reinterpret_cast<int32_t*>(qout + e) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  if ((lane & 7) == 0) dout[e / 32] = __half2float(__float2half_rn(d));
+}
+
 // Decode / causal attention for one (kv head g, token m, key split sp): GQ = 2 query heads share the
 // K/V stream. Keys [0, pos] are cut into n_active contiguous splits of >= AMIN_G groups each (one block
 // per split, so a long context is fetched by up to ASPLIT CUs instead of one). A single active split writes
@@ -852,7 +898,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
                                                          const float* __restrict__ qn, const float* __restrict__ kn,
                                                          const float* __restrict__ rcos, const float* __restrict__ rsin,
                                                          float eps, float scale, float* __restrict__ out,
-                                                         int* __restrict__ counters, float* __restrict__ partials) {
+                                                         int* __restrict__ counters, float* __restrict__ partials,
+                                                         int8_t* __restrict__ qout, float* __restrict__ dout) {
   constexpr int D = 128;
   STAMP(0);
   const int g = blockIdx.x, sp = blockIdx.y, m = blockIdx.z;
@@ -971,7 +1018,9 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   }
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;
   if (n_active == 1) {
-    *reinterpret_cast<float4*>(op) = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+    const float4 r = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+    *reinterpret_cast<float4*>(op) = r;
+    if (qout) store_q8_row4(qout, dout, (int64_t)m * H * D + (g * GQ + j) * D + d0, lane, r);
     STAMP(9);
     return;
   }
@@ -1015,13 +1064,15 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
       oo += wt * po[t];
     }
   }
-  *reinterpret_cast<float4*>(op) = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
+  const float4 r = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
+  *reinterpret_cast<float4*>(op) = r;
+  if (qout) store_q8_row4(qout, dout, (int64_t)m * H * D + (g * GQ + j) * D + d0, lane, r);
   if (lane == 0) __hip_atomic_store(counters + (m * KV + g) * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s) {
+                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout, float* dout) {
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
@@ -1030,7 +1081,8 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   int lg = 0;
   while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= 1024) ++lg;
   hipLaunchKernelGGL(k_attn_block, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode, H, KV,
-                     seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials);
+                     seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials, qout,
+                     dout);
 }
 
 // ------------------------------------------------------------------------------------------------

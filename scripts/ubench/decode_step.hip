@@ -24,6 +24,9 @@ int main(int argc, char** argv) {
   float* tmp = dalloc<float>((size_t)V * E);
   // "arena": all q8_0 weights carved from ONE allocation (TLB experiment), else one hipMalloc per tensor
   const bool arena = argc > 1 && !strcmp(argv[1], "arena");
+  // "mall": layers reuse 6 distinct weight sets (~100 MB < 256 MB Infinity Cache): the step reads MALL-resident
+  // weights (what a run-ahead prefetcher could at best achieve)
+  const int n_distinct = (argc > 1 && !strcmp(argv[1], "mall")) ? 6 : 28;
   char* arena_p = nullptr; size_t arena_off = 0;
   if (arena) CK(hipMalloc(&arena_p, (size_t)700 << 20));
   auto take = [&](size_t bytes) -> void* {
@@ -60,7 +63,7 @@ int main(int argc, char** argv) {
   int mask = 63;  // 1 qkv, 2 attn, 4 o, 8 gate/up, 16 down, 32 lm_head (ablation: time a subset of the chain)
   auto step = [&]() {
     for (int l = 0; l < L; ++l) {
-      auto& w = lw[l];
+      auto& w = lw[l % n_distinct];
       if (mask & 1) gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
       if (mask & 2) attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV,
                  seq, pos, (int64_t)NCTX * KV * D, att, wk, s);
@@ -74,7 +77,7 @@ int main(int argc, char** argv) {
     if (mask & 32) gemv_q8(h, E, 3, s);
   };
   const bool eager = argc > 1 && !strcmp(argv[1], "eager");
-  printf("weights: %s\n", arena ? "one arena allocation" : "one hipMalloc per tensor");
+  printf("weights: %s, %d distinct layers\n", arena ? "one arena allocation" : "one hipMalloc per tensor", n_distinct);
   const int n = argc > 2 ? atoi(argv[2]) : 3;
   if (eager) { for (int i = 0; i < n; ++i) step(); CK(hipStreamSynchronize(s)); printf("eager %d steps done\n", n); return 0; }
   const double bytes = (double)L * (QKV * E + E * H * D + 2.0 * F * E + E * F) * 34 / 32 + (double)V * E * 34 / 32;
