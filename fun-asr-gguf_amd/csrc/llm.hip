@@ -450,15 +450,16 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
   }
 }
 
-// Same GEMM with K split over the 8 waves of ONE block instead of over blocks: no cross-block split-K hop (on this
-// chip an in-launch hand-off costs about a kernel boundary: scripts/ubench/edge_chain.hip), and every wave issues
-// ALL its loads (NBW q8_0 blocks of weights and activations, their scales) before its MFMAs, so a tile costs one
-// memory round trip. Waves are reduced in LDS in fixed order (deterministic). SwiGLU: waves 0-3 gate, 4-7 up.
-constexpr int KW_WAVES = 8;
-template <int EPI, int NBW>
-__global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
-  static_assert(NBW % 4 == 0 && EPI != 3, "k_gemm_q8_kw: 4-block scale groups, no lm_head epilogue");
-  constexpr int NWM = EPI == 2 ? KW_WAVES / 2 : KW_WAVES;  // waves per weight matrix
+// Same GEMM with K split over the NW waves of ONE block instead of over blocks: no cross-block split-K hop (on
+// this chip an in-launch hand-off costs about a kernel boundary: scripts/ubench/edge_chain.hip), and every wave
+// issues ALL its loads (NBW q8_0 blocks of weights and activations, their scales) before its MFMAs, so a tile
+// costs one memory round trip. Waves are reduced in LDS in fixed order (deterministic). SwiGLU: the first half
+// of the waves take the gate matrix, the second half the up matrix. NW = 16 (1024 threads) for the few-tile
+// shapes (o and down at batch 32: 32 tiles) so each CU keeps twice the loads in flight.
+template <int EPI, int NW, int NBW>
+__global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
+  static_assert(NBW % 2 == 0 && EPI != 3 && (NW == 8 || (NW == 16 && EPI != 2)), "k_gemm_q8_kw: shapes");
+  constexpr int NWM = EPI == 2 ? NW / 2 : NW;  // waves per weight matrix
   const int nb = K >> 5;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32;
@@ -475,16 +476,16 @@ __global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K)
     A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
     B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
   }
-  uint2 dw[16][NBW / 4];  // fp16 scales of each of this lane's 16 rows, 4 blocks per uint2
+  uint32_t dw[16][NBW / 2];  // fp16 scales of each of this lane's 16 rows, 2 blocks per dword
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) {
     const int row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
 #pragma unroll
-    for (int q = 0; q < NBW / 4; ++q) dw[reg][q] = *reinterpret_cast<const uint2*>(wd + (int64_t)row * nb + b0 + 4 * q);
+    for (int q = 0; q < NBW / 2; ++q) dw[reg][q] = *reinterpret_cast<const uint32_t*>(wd + (int64_t)row * nb + b0 + 2 * q);
   }
-  float4 dx4[NBW / 4];
+  float2 dx2[NBW / 2];
 #pragma unroll
-  for (int q = 0; q < NBW / 4; ++q) dx4[q] = *reinterpret_cast<const float4*>(a.xd + (int64_t)t_b * nb + b0 + 4 * q);
+  for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + b0 + 2 * q);
   float acc[16];
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
@@ -492,31 +493,48 @@ __global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K)
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
-    const float4& d4 = dx4[j >> 2];
-    const float dx = (j & 3) == 0 ? d4.x : (j & 3) == 1 ? d4.y : (j & 3) == 2 ? d4.z : d4.w;
+    const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 2]);
-      acc[reg] += (float)D[reg] * (__half2float(hw[j & 3]) * dx);
+      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 1]);
+      acc[reg] += (float)D[reg] * (__half2float(hw[j & 1]) * dx);
     }
   }
-  // fixed-order reduction over the waves of each matrix; thread t finalises regs [2 (t>>6), +2) of lane t&63
-  __shared__ float s_red[KW_WAVES][16][64];
+  // fixed-order reduction over the waves of each matrix (NW = 16: waves w and w + 8 first pair up); thread t then
+  // finalises regs [RPT (t>>6), +RPT) of lane t&63
+  constexpr int NR = NW == 16 ? 8 : NW;  // partial tiles left for the final sum
+  constexpr int NRM = EPI == 2 ? NR / 2 : NR;
+  constexpr int RPT = 16 / NW;
+  __shared__ float s_red[NR][16][64];
   __shared__ float s_act[EPI == 2 ? 32 : 1][33];  // SwiGLU tile [token][row] for the q8_0 epilogue
+  if (NW == 16) {
+    if (wave >= 8) {
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
+      for (int reg = 0; reg < 16; ++reg) s_red[wave - 8][reg][lane] = acc[reg];
+    }
+    __syncthreads();
+    if (wave < 8) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) acc[reg] += s_red[wave][reg][lane];
+    }
+    __syncthreads();
+  }
+  if (wave < NR) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
+  }
   __syncthreads();
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int col = l & 31, tok = t0 + col;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int reg = 2 * g + q;
+  for (int q = 0; q < RPT; ++q) {
+    const int reg = RPT * g + q;
     float y = 0.f, y2 = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWM; ++w) y += s_red[w][reg][l];
+    for (int w = 0; w < NRM; ++w) y += s_red[w][reg][l];
     if (EPI == 2) {
 #pragma unroll
-      for (int w = NWM; w < KW_WAVES; ++w) y2 += s_red[w][reg][l];
+      for (int w = NRM; w < NR; ++w) y2 += s_red[w][reg][l];
     }
     const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5), row = o0 + rrow;
     float v = 0.f;
@@ -558,29 +576,31 @@ __global__ __launch_bounds__(KW_WAVES * 64) void k_gemm_q8_kw(GemvArgs a, int K)
   }
 }
 
-template <int EPI, int NBW>
+template <int EPI, int NW, int NBW>
 static void launch_gemm_kw(const GemvArgs& a, int K, hipStream_t s) {
-  hipLaunchKernelGGL((k_gemm_q8_kw<EPI, NBW>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)), dim3(KW_WAVES * 64), 0, s, a, K);
+  hipLaunchKernelGGL((k_gemm_q8_kw<EPI, NW, NBW>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)), dim3(NW * 64), 0, s, a, K);
 }
 
-// K-in-block GEMM for the shapes it is instantiated for (q8_0 blocks per wave NBW = 4, 8, 12); false otherwise
+// K-in-block GEMM for the shapes it is instantiated for; false otherwise. 8 waves (16 measured slower on the
+// few-tile o / down shapes at batch 32: 10.2 / 18.3 vs 8.8 / 14.6 us, register-capped at 128 VGPRs);
+// q8_0 blocks per wave NBW = blocks of K per wave.
 static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
-  const int nbw = (K / 32) * (epi == 2 ? 2 : 1) / KW_WAVES;
-  if (epi == 3 || (K / 32) * (epi == 2 ? 2 : 1) != nbw * KW_WAVES) return false;
-  switch (epi * 100 + nbw) {
-    case 4: launch_gemm_kw<0, 4>(a, K, s); return true;
-    case 8: launch_gemm_kw<0, 8>(a, K, s); return true;
-    case 12: launch_gemm_kw<0, 12>(a, K, s); return true;
-    case 104: launch_gemm_kw<1, 4>(a, K, s); return true;
-    case 108: launch_gemm_kw<1, 8>(a, K, s); return true;
-    case 112: launch_gemm_kw<1, 12>(a, K, s); return true;
-    case 208: launch_gemm_kw<2, 8>(a, K, s); return true;
+  constexpr int nw = 8;
+  if (epi == 3) return false;
+  const int nb = (K / 32) * (epi == 2 ? 2 : 1);
+  if (nb % nw) return false;
+  switch (epi * 100 + nb / nw) {
+    case 4: launch_gemm_kw<0, nw, 4>(a, K, s); return true;
+    case 8: launch_gemm_kw<0, nw, 8>(a, K, s); return true;
+    case 12: launch_gemm_kw<0, nw, 12>(a, K, s); return true;
+    case 104: launch_gemm_kw<1, nw, 4>(a, K, s); return true;
+    case 108: launch_gemm_kw<1, nw, 8>(a, K, s); return true;
+    case 112: launch_gemm_kw<1, nw, 12>(a, K, s); return true;
+    case 208: launch_gemm_kw<2, nw, 8>(a, K, s); return true;
     default: return false;
   }
 }
 
-// K splits for the MFMA GEMM: enough blocks to cover the chip when the tile count is small, keeping
-// (K/32)/KS/4 a multiple of the 4-block load group. Split-K needs the a.kpart/a.kcnt workspace.
 int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0)
 
 int gemm_k_splits(int O, int M, int K) {
