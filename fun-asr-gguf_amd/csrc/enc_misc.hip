@@ -139,30 +139,46 @@ void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* 
 }
 
 // ---------------- E4: FSMN memory = depthwise conv_k(v*m) (zero pad (k-1)/2) + v*m (model_definition.py:60-66)
-__global__ void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w, float* __restrict__ out,
-                       int64_t ldo, int rows, int C, int ksize, const int* __restrict__ lens, int t_stride, int r16) {
-  const int64_t total = (int64_t)rows * C;
-  const int lp = (ksize - 1) / 2;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int row = (int)(e / C), c = (int)(e - (int64_t)row * C);
-    int b = row / t_stride, t = row - b * t_stride;
-    int len = lens ? lens[b] : t_stride;
+// A lane owns one channel for FR consecutive rows: the FR + K - 1 input rows it needs are loaded once into
+// registers (a wave reads 64 consecutive channels = 256 B per row), the K taps stay in registers, and each output
+// row sums only inputs of its own clip that are inside the clip's valid length (the v*m mask + per-clip zero pad).
+constexpr int FSMN_K = 11, FSMN_R = 32;
+__global__ __launch_bounds__(256) void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w,
+                                              float* __restrict__ out, int64_t ldo, int rows, int C,
+                                              const int* __restrict__ lens, int t_stride, int r16) {
+  constexpr int LP = (FSMN_K - 1) / 2, NW = FSMN_R + FSMN_K - 1;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * FSMN_R;
+  if (c >= C || r0 >= rows) return;
+  float wk[FSMN_K], win[NW];
+#pragma unroll
+  for (int j = 0; j < FSMN_K; ++j) wk[j] = r16e(w[c * FSMN_K + j], r16);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int q = min(max(r0 - LP + i, 0), rows - 1);  // clamped address; out-of-clip taps are skipped below
+    win[i] = v[(int64_t)q * ldv + c];
+  }
+#pragma unroll
+  for (int i = 0; i < FSMN_R; ++i) {
+    const int r = r0 + i;
+    if (r >= rows) break;
+    const int b = r / t_stride, lo = b * t_stride, hi = lo + (lens ? lens[b] : t_stride);
     float acc = 0.f;
-    for (int j = 0; j < ksize; ++j) {
-      int tt = t + j - lp;
-      float xv = (tt >= 0 && tt < len && tt < t_stride) ? v[((int64_t)b * t_stride + tt) * ldv + c] : 0.f;
-      acc += r16e(w[c * ksize + j], r16) * xv;
+#pragma unroll
+    for (int j = 0; j < FSMN_K; ++j) {
+      const int q = r - LP + j;
+      acc = fmaf(wk[j], (q >= lo && q < hi) ? win[i + j] : 0.f, acc);
     }
-    float self = t < len ? v[(int64_t)row * ldv + c] : 0.f;
-    out[(int64_t)row * ldo + c] = r16e(r16e(acc, r16) + self, r16);
+    const float self = r < hi ? win[i + LP] : 0.f;
+    out[(int64_t)r * ldo + c] = r16e(r16e(acc, r16) + self, r16);
   }
 }
 
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
           const int* lens, int t_stride, hipStream_t s, int r16) {
-  int64_t total = (int64_t)rows * C;
-  hipLaunchKernelGGL(k_fsmn, dim3(std::min(cdiv(total, 256), 8192)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
-                     ksize, lens, t_stride, r16);
+  FA_REQUIRE(ksize == FSMN_K, "fsmn: kernel size 11 (SenseVoiceSmall sanm_shfit 0, kernel_size 11)");
+  dim3 grid(cdiv(C, 64), cdiv(rows, 4 * FSMN_R));
+  hipLaunchKernelGGL(k_fsmn, grid, dim3(256), 0, s, v, ldv, w, out, ldo, rows, C, lens, t_stride, r16);
 }
 
 // ---------------- C2: CTC greedy collapse (nano_ctc.py:65-104): keep frame i iff id != blank and
