@@ -274,6 +274,13 @@ def headline(args, world, dt, dt_prof, prof, stage):
     roof.update(kernel=names[dom], avg_launch_us=round(avg_s * 1e6, 2), launches_timed=p["launches"],
                 per_launch=("q8_0 weight bytes" if dom in (0, 4) else "algorithmic FLOPs"),
                 est_device_ms_per_step={names[c]: round(est_ms[c] / args.steps, 2) for c in prof})
+    # the encoder's MFMA classes against the f32 matrix peak (secondary: the clip's 705 GFLOP of contractions)
+    for c, key in ((1, "encoder_gemm_f32"), (2, "encoder_attention_f32")):
+        e = prof[c]
+        if e["launches"] and e["ms"] > 0:
+            tfs = e["flops"] / (e["ms"] / 1e3) / 1e12
+            roof[key] = {"achieved_TFs": round(tfs, 2), "peak_TFs": FP32_MFMA_PEAK_TFS,
+                         "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4), "avg_launch_us": round(e["ms"] * 1e3 / e["launches"], 2)}
     lm = prof[4]
     if lm["launches"]:
         lm_s = lm["ms"] / lm["launches"] / 1e3

@@ -134,6 +134,26 @@ def test_encoder_fp16_graph_vs_oracle(tiny_engine, enc_w_tiny):
     assert _rel(out32["audio_embd"][0], g["adaptor"]) < ENC_ATOL_TINY
 
 
+def test_encoder_fp16_graph_padded_batch(tiny_engine, enc_w_tiny):
+    """fp16 graph on a ragged batch (incl. a < 1 s clip): each clip equals its own unpadded fp16-oracle run."""
+    from fun_asr_gguf.synthetic import synth_audio
+    from oracle import encoder_fp16 as oe16
+    lens = [16000 * 2 + 321, 9000]
+    clips = [synth_audio(n, 40 + i) for i, n in enumerate(lens)]
+    tiny_engine.set_encoder_fp16(True)
+    try:
+        out = tiny_engine.encode(clips, want_enc=True)
+    finally:
+        tiny_engine.set_encoder_fp16(False)
+    for i, c in enumerate(clips):
+        n = len(c)
+        a = np.zeros(max(n, 16000), np.float32)
+        a[:n] = c
+        r = oe16.encode(a, enc_w_tiny, synth.ENC_TINY, valid=n)
+        assert _rel(out["enc"][i], r["enc"]) < FP16_REL and _cos(out["enc"][i], r["enc"]) > FP16_COS, i
+        assert _rel(out["audio_embd"][i], r["audio_embd"]) < FP16_REL, i
+
+
 def test_ctc_collapse_matches_reference_rule(tiny_engine):
     from fun_asr_gguf.synthetic import synth_audio
     clips = [synth_audio(30000, 5), synth_audio(20000, 6)]
