@@ -125,6 +125,63 @@ __device__ __forceinline__ void norm_quant_row_block(const float* __restrict__ x
   if ((t % TPB) == 0) d_out[t / TPB] = __half2float(__float2half_rn(d));
 }
 
+// The same two prologues from values already in registers (the GEMV issues its activation loads before its
+// weight stream: vmcnt retires in issue order, so activation loads issued after the weights would wait for them).
+// Arithmetic identical to norm_quant_row_block / norm_quant_row.
+template <int PER>
+__device__ __forceinline__ void norm_quant_block_regs(float (&v)[PER], const float (&wv)[PER], bool has_w, float eps,
+                                                      int K, int8_t* __restrict__ q_out, float* __restrict__ d_out,
+                                                      float* __restrict__ s_red) {
+  constexpr int TPB = 32 / PER;
+  const int t = threadIdx.x;
+  if (has_w) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) ss += v[j] * v[j];
+    ss = wave_sum(ss);
+    if ((t & 63) == 0) s_red[t >> 6] = ss;
+    __syncthreads();
+    ss = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    const float scale = 1.0f / sqrtf(ss / (float)K + eps);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) v[j] = (v[j] * scale) * wv[j];
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) a = fmaxf(a, fabsf(v[j]));
+  a = group_max<TPB>(a);
+  const float d = a / 127.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  int8_t qv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) qv[j] = (int8_t)roundf(__fmul_rn(v[j], id));
+  if (PER == 4) *reinterpret_cast<int32_t*>(q_out + t * PER) = *reinterpret_cast<int32_t*>(qv);
+  else *reinterpret_cast<int2*>(q_out + t * PER) = *reinterpret_cast<int2*>(qv);
+  if ((t % TPB) == 0) d_out[t / TPB] = __half2float(__float2half_rn(d));
+}
+
+// one 1024-chunk per wave, no norm (norm_quant_row<1> with w = nullptr): lane holds x[lane*16 .. +16)
+__device__ __forceinline__ void quant_chunk_regs(const float (&v)[16], int lane, int8_t* __restrict__ q_out,
+                                                 float* __restrict__ d_out) {
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a = fmaxf(a, fabsf(v[j]));
+  a = group_max<2>(a);
+  const float d = a / 127.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  int32_t packed[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int b0 = (int)roundf(__fmul_rn(v[4 * j], id)) & 0xFF;
+    int b1 = (int)roundf(__fmul_rn(v[4 * j + 1], id)) & 0xFF;
+    int b2 = (int)roundf(__fmul_rn(v[4 * j + 2], id)) & 0xFF;
+    int b3 = (int)roundf(__fmul_rn(v[4 * j + 3], id)) & 0xFF;
+    packed[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  }
+  *reinterpret_cast<int4*>(q_out + lane * 16) = make_int4(packed[0], packed[1], packed[2], packed[3]);
+  if (!(lane & 1)) d_out[lane >> 1] = __half2float(__float2half_rn(d));
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void k_prep_q8(const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                  float eps, int M, int8_t* __restrict__ xq, float* __restrict__ xd) {
@@ -240,8 +297,21 @@ __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, i
   }
 }
 
+// FA_GEMV_STAMPS (microbenchmark builds only): per-block s_memrealtime stamps (100 MHz, chip-wide) of the
+// decode GEMV: [start, prologue done, rows done, end] -> g_gstamps[block]
+#ifdef FA_GEMV_STAMPS
+__device__ unsigned long long g_gstamps[4096][4];
+#define GSTAMP(i) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_gstamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+void gemv_stamps_read(unsigned long long* host, int n) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gstamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define GSTAMP(i) do { } while (0)
+#endif
+
 template <int NCH, int MT, bool FUSED, int EPI>
 __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
+  GSTAMP(0);
   constexpr int K = NCH * 1024, NB = K / 32;
   __shared__ int8_t s_q[MT * K];
   __shared__ float s_d[MT * NB];
@@ -249,17 +319,51 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   const int m0 = blockIdx.y * MT;
   const int mt = min(MT, a.M - m0);
   const int row_base = (blockIdx.x * 4 + wave) * a.rpw;
-  // weights do not depend on the activations: issue the first row group before the prologue
+  // ---- activation loads first (a few KB that the whole block waits on; vmcnt retires in issue order, so
+  // behind the weight stream they would arrive only with it), then the first weight row group, then the
+  // prologue math: the weights stream in while the activations are normalised and quantised
+  // (branch-free: a branch here makes the wait-count pass drain the loads at the join, before the weight stream)
+  constexpr int PERB = NCH * 4;  // block-cooperative prologue: values per thread
+  const bool pro_blk = FUSED && mt == 1 && NCH < 3;
+  const bool pro_chunk = FUSED && mt == 1 && NCH == 3 && !a.norm_w;  // K = 3072, no norm (down projection)
+  float xv[NCH < 3 ? PERB : 16], xw[PERB];
+  if constexpr (FUSED && NCH < 3) {
+    const float* xr = a.x + (int64_t)m0 * a.ldx + threadIdx.x * PERB;
+    const float* wr = (a.norm_w ? a.norm_w : a.x) + threadIdx.x * PERB;  // no norm: a valid dummy row, unused
+#pragma unroll
+    for (int j = 0; j < PERB; j += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(xr + j);
+      xv[j] = f.x; xv[j + 1] = f.y; xv[j + 2] = f.z; xv[j + 3] = f.w;
+      const float4 g = *reinterpret_cast<const float4*>(wr + j);
+      xw[j] = g.x; xw[j + 1] = g.y; xw[j + 2] = g.z; xw[j + 3] = g.w;
+    }
+  } else if constexpr (FUSED && NCH == 3) {
+    const float* xr = a.x + (int64_t)m0 * a.ldx + min(wave, 2) * 1024 + lane * 16;  // wave 3: a duplicate, unused
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(xr + j);
+      xv[j] = f.x; xv[j + 1] = f.y; xv[j + 2] = f.z; xv[j + 3] = f.w;
+    }
+  }
   RowGroup<NCH, EPI> G0, G1;
   load_group<NCH, EPI>(a, row_base, 0, lane, G0);
+  // keep the prologue math below the weight loads: otherwise the scheduler hoists it and waits for the
+  // activations (vmcnt(0)) before the weight stream is even issued
+  __builtin_amdgcn_sched_barrier(0);
   // ---- prologue: activation tile -> LDS (int8 q + f32 d)
-  if (FUSED && mt == 1 && NCH < 3) {
+  if (pro_blk) {
     __shared__ float s_red[4];
-    norm_quant_row_block<NCH>(a.x + (int64_t)m0 * a.ldx, a.norm_w, a.eps, s_q, s_d, s_red);
-  } else if (FUSED && mt == 1 && !a.norm_w) {
-    // K = 3072 without norm (down proj): waves 0..2 quantise one 1024-chunk each
-    if (wave < NCH) norm_quant_row<1>(a.x + (int64_t)m0 * a.ldx + wave * 1024, nullptr, 0.f, lane, s_q + wave * 1024,
-                                      s_d + wave * 32);
+    float v[PERB];
+#pragma unroll
+    for (int j = 0; j < PERB; ++j) v[j] = xv[j];
+    norm_quant_block_regs<PERB>(v, xw, a.norm_w != nullptr, a.eps, NCH * 1024, s_q, s_d, s_red);
+  } else if (pro_chunk) {
+    if (wave < NCH) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = xv[j];
+      quant_chunk_regs(v, lane, s_q + wave * 1024, s_d + wave * 32);
+    }
   } else if (FUSED) {
     for (int m = wave; m < mt; m += 4)
       norm_quant_row<NCH>(a.x + (int64_t)(m0 + m) * a.ldx, a.norm_w, a.eps, lane, s_q + m * K, s_d + m * NB);
@@ -270,6 +374,7 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
     for (int i = threadIdx.x; i < mt * NB; i += 256) s_d[i] = a.xd[(int64_t)m0 * NB + i];
   }
   __syncthreads();
+  GSTAMP(1);
   float best_v[MT];
   int best_i[MT];
 #pragma unroll
@@ -285,6 +390,7 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
     if (r0 + 8 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 8, lane, G0);
     compute_group<NCH, MT, EPI>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i);
   }
+  GSTAMP(2);
   if (EPI == 3 && lane == 0) {
     const int part = blockIdx.x * 4 + wave;
 #pragma unroll

@@ -4,3 +4,5 @@ set -e
 B=fun-asr-gguf_amd/build; U=scripts/ubench; F="-O3 -std=c++17 --offload-arch=gfx950 -Iinclude"
 hipcc $F -c $U/decode_step.hip -o /tmp/ds.o && hipcc --offload-arch=gfx950 /tmp/ds.o $B/llm.hip.o $B/synth.hip.o -o $U/decode_step
 hipcc $F $U/edge_chain.hip -o $U/edge_chain
+hipcc $F -DFA_GEMV_STAMPS -x hip -c fun-asr-gguf_amd/csrc/llm.hip -o /tmp/llm_gstamps.o
+hipcc $F -c $U/gemv_stamps.hip -o /tmp/gs.o && hipcc --offload-arch=gfx950 /tmp/gs.o /tmp/llm_gstamps.o $B/synth.hip.o -o $U/gemv_stamps
