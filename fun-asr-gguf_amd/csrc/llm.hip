@@ -259,7 +259,7 @@ __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int 
 template <int NCH, int MT, int EPI>
 __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, int r0, int lane, int m0, int mt,
                                               const int8_t* s_q, const float* s_d, const RowGroup<NCH, EPI>& G,
-                                              float (&best_v)[MT], int (&best_i)[MT]) {
+                                              float (&best_v)[MT], int (&best_i)[MT], const float (&res0)[4]) {
   constexpr int K = NCH * 1024, NB = K / 32;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
@@ -289,7 +289,7 @@ __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, i
       if (lane == 0 && (r0 + rr < a.rpw) && row < a.O) {
         float* op = a.out + (int64_t)(m0 + m) * a.ldo + row;
         if (EPI == 0 || EPI == 3) *op = y;
-        else if (EPI == 1) *op = a.res[(int64_t)(m0 + m) * a.ldr + row] + y;
+        else if (EPI == 1) *op = (MT == 1 && r0 == 0 ? res0[rr] : a.res[(int64_t)(m0 + m) * a.ldr + row]) + y;
         else *op = (y / (1.0f + expf(-y))) * y2;
         if (EPI == 3) argmax_combine(best_v[m], best_i[m], y, row);
       }
@@ -345,6 +345,14 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
       xv[j] = f.x; xv[j + 1] = f.y; xv[j + 2] = f.z; xv[j + 3] = f.w;
     }
   }
+  // residual epilogue: the first row group's residual values ride with the activation loads (a load after the
+  // dot products would be one more serial memory latency at the tail)
+  float res0[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == 1 && MT == 1) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) res0[rr] = a.res[(int64_t)m0 * a.ldr + min(row_base + rr, a.O - 1)];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // the scheduler would otherwise sink these loads below the weight stream
   RowGroup<NCH, EPI> G0, G1;
   load_group<NCH, EPI>(a, row_base, 0, lane, G0);
   // keep the prologue math below the weight loads: otherwise the scheduler hoists it and waits for the
@@ -385,10 +393,10 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   // two-deep register pipeline over 4-row groups (static buffer names, no runtime-indexed arrays)
   for (int r0 = 0; r0 < a.rpw; r0 += 8) {
     if (r0 + 4 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 4, lane, G1);
-    compute_group<NCH, MT, EPI>(a, row_base, r0, lane, m0, mt, s_q, s_d, G0, best_v, best_i);
+    compute_group<NCH, MT, EPI>(a, row_base, r0, lane, m0, mt, s_q, s_d, G0, best_v, best_i, res0);
     if (r0 + 4 >= a.rpw) break;
     if (r0 + 8 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 8, lane, G0);
-    compute_group<NCH, MT, EPI>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i);
+    compute_group<NCH, MT, EPI>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i, res0);
   }
   GSTAMP(2);
   if (EPI == 3 && lane == 0) {
