@@ -909,6 +909,7 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
   int4 kt[NI], vt[NI];
   load_kv_groups<NI>(kb, KV, g0, n_keys, kq, dq, kt);
   load_kv_groups<NI>(vb, KV, g0, n_keys, kq, dq, vt);
+  __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
   if (decode) {
 #pragma unroll
@@ -1040,6 +1041,9 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // loads and re-arms the counter (MI355X_MICROARCH.md hand-off table, row 1: no fences needed).
 // Prefill mode (decode_mode = 0): q is already normed/roped (qk_rope_store) and K/V[pos] are in the cache.
 // (parameter order = kernarg layout: everything the prologue needs sits in the first 64-B line)
+// DM = decode_mode as a template constant: a runtime branch between the q loads and the K/V stream made the
+// wait-count pass drain the q loads at the join, before the K/V loads were issued
+template <int DM>
 __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
                                                          int lg_nsplit, int decode_mode, int H, int KV,
                                                          int64_t seq_stride, __half* __restrict__ kc,
@@ -1082,12 +1086,12 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
   }
-  const int fresh_group = decode_mode ? (pos >> 2) : -1;
+  const int fresh_group = DM ? (pos >> 2) : -1;
   const bool fresh_here = fresh_group >= gb && fresh_group < ge && (fresh_group - gb) % AWV == wave;
   const int g0 = gb + wave;
   if (g0 < ge) {
     AttnQIn qi;
-    if (decode_mode) {
+    if (DM) {
       const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
       for (int j = 0; j < GQ; ++j) {
@@ -1117,16 +1121,16 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     __half* vd = vb + (int64_t)pos * KV * D;
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
-      attn_wave<1>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<1>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                    s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 2)
-      attn_wave<2>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<2>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                    s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 4)
-      attn_wave<4>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<4>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                    s_q[wave], s_kn, s_vn, mx, l, acc);
     else
-      attn_wave<8>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, decode_mode, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<8>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                    s_q[wave], s_kn, s_vn, mx, l, acc);
   }
   // publish per-wave (m, l) and per-row partial o
@@ -1229,7 +1233,8 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // 4 at batch 32, 1 for prefill
   int lg = 0;
   while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= 1024) ++lg;
-  hipLaunchKernelGGL(k_attn_block, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode, H, KV,
+  hipLaunchKernelGGL(decode_mode ? k_attn_block<1> : k_attn_block<0>, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq,
+                     tok_pos, lg, decode_mode, H, KV,
                      seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials, qout,
                      dout);
 }
