@@ -844,8 +844,16 @@ void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const floa
 // consumes the fresh row from LDS (with the cache's fp16 rounding). PREFILL mode: q comes pre-roped from
 // qk_rope_store and the cache is complete.
 #ifdef FA_ATTN_STAMPS
-__device__ unsigned long long g_attn_stamps[16];
-#define STAMP(i) do { if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) g_attn_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+// per-block s_memrealtime (100 MHz, chip-wide) stamps of wave 0, lane 0: [i] at the STAMP(i) points
+__device__ unsigned long long g_attn_stamps[4096][12];
+#define STAMP(i) do { if (threadIdx.x == 0) g_attn_stamps[(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+void attn_stamps_read(unsigned long long* host, int n_blocks) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)n_blocks * 96, 0, hipMemcpyDeviceToHost);
+}
+void attn_stamps_clear() {
+  static unsigned long long z[4096][12];
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
 #else
 #define STAMP(i) do { } while (0)
 #endif
@@ -859,13 +867,13 @@ constexpr int APART = ATTN_PART_FLOATS;  // per-split partial: o[GQ][128], m[GQ]
 // Lane (kq = lane>>4, dq = lane&15) holds dims [8 dq, 8 dq + 8) of key 4 q + kq: each load instruction
 // reads 4 whole 256-B rows. Groups past the wave's share are loaded clamped (valid rows, compute skipped):
 // no branches around loads.
-template <int NI>
+template <int NI, int AW>
 __device__ __forceinline__ void load_kv_groups(const __half* __restrict__ base, int KV, int g0, int n_keys, int kq,
                                                int dq, int4 (&t)[NI]) {
   constexpr int D = 128;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int k = min(4 * (g0 + AWV * i) + kq, n_keys - 1);
+    const int k = min(4 * (g0 + AW * i) + kq, n_keys - 1);
     t[i] = *reinterpret_cast<const int4*>(base + (int64_t)k * KV * D + dq * 8);
   }
 }
@@ -900,15 +908,15 @@ struct AttnQIn {
 // One wave's share of one key split: NI = its 4-key groups per pass rounded up to a power of two (loads of
 // the rounded-up slots are clamped duplicates, masked). Issues the K/V stream first, then finishes q while
 // it is in flight.
-template <int NI>
+template <int NI, int AW>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
                                           float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8]) {
   int4 kt[NI], vt[NI];
-  load_kv_groups<NI>(kb, KV, g0, n_keys, kq, dq, kt);
-  load_kv_groups<NI>(vb, KV, g0, n_keys, kq, dq, vt);
+  load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+  load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
   __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
   if (decode) {
@@ -952,12 +960,12 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
   STAMP(3);
   const int fresh = fresh_here ? pos : -1;
   for (;;) {
-    // scores of key 4 (g0 + AWV i) + kq: 8-dim partial dot per lane, summed over the row's 16 lanes (DPP)
+    // scores of key 4 (g0 + AW i) + kq: 8-dim partial dot per lane, summed over the row's 16 lanes (DPP)
     float sc[NI][GQ];
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int key = 4 * (g0 + AWV * i) + kq;
-      const bool valid = (g0 + AWV * i) < ge && key < n_keys;
+      const int key = 4 * (g0 + AW * i) + kq;
+      const bool valid = (g0 + AW * i) < ge && key < n_keys;
       float kv[8];
       unpack8(kt[i], kv);
       if (key == fresh) {
@@ -1000,7 +1008,7 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
     // p.V with p still in registers
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int key = 4 * (g0 + AWV * i) + kq;
+      const int key = 4 * (g0 + AW * i) + kq;
       float v[8];
       unpack8(vt[i], v);
       if (key == fresh) {
@@ -1013,10 +1021,10 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
         for (int e = 0; e < 8; ++e) acc[j][e] += sc[i][j] * v[e];
     }
     STAMP(6);
-    g0 += AWV * NI;
+    g0 += AW * NI;
     if (g0 >= ge) break;
-    load_kv_groups<NI>(kb, KV, g0, n_keys, kq, dq, kt);
-    load_kv_groups<NI>(vb, KV, g0, n_keys, kq, dq, vt);
+    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
   }
 }
 
@@ -1054,7 +1062,6 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
                                                          int* __restrict__ counters, float* __restrict__ partials,
                                                          int8_t* __restrict__ qout, float* __restrict__ dout) {
   constexpr int D = 128;
-  STAMP(0);
   const int g = blockIdx.x, sp = blockIdx.y, m = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int pos = tok_pos[m];
@@ -1063,6 +1070,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   // fetched together, before the first use (otherwise each is a serial scalar-load latency)
   asm volatile("" : "+s"(pos) : "s"(seq), "s"(qsrc), "s"(kc), "s"(vc), "s"(rcos), "s"(rsin), "s"(qn), "s"(kn),
                "s"(seq_stride), "s"(out), "s"(partials));
+  STAMP(0);
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
   const int gps = max(AMIN_G, (n_groups + (1 << lg_nsplit) - 1) >> lg_nsplit);  // groups per split
@@ -1074,9 +1082,9 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   __half* kb = kc + (int64_t)seq * seq_stride + g * D;
   __half* vb = vc + (int64_t)seq * seq_stride + g * D;
   __shared__ float s_q[AWV][GQ][D];          // per-wave q (scaled, roped) in natural dim order
-  __shared__ float s_kn[D], s_vn[D];         // fresh K/V row (decode)
+  __shared__ float s_kn[D], s_vn[D];        // fresh K/V row (decode)
   __shared__ float s_ml[AWV][GQ][2];
-  __shared__ float s_o[AWV][4][GQ][D];       // [wave][key row kq][head][dim]
+  __shared__ float s_o[AWV][GQ][D];          // [wave][head][dim], summed over the wave's 4 key rows
   const int kq = lane >> 4, dq = lane & 15;
   float mx[GQ], l[GQ], acc[GQ][8];
 #pragma unroll
@@ -1121,28 +1129,48 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     __half* vd = vb + (int64_t)pos * KV * D;
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
-      attn_wave<1>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                   s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<1, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 2)
-      attn_wave<2>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                   s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<2, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 4)
-      attn_wave<4>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                   s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<4, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else
-      attn_wave<8>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                   s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<8, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
   }
-  // publish per-wave (m, l) and per-row partial o
+  // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
+  // unscaled): permlane32_swap pairs fold rows {r, r^2}, permlane16_swap pairs fold {r, r^1}; afterwards
+  // red[k] of a lane in row r holds element t = 4k + 2(r&1) + (r>>1) of acc (t = 8 head + dim-in-lane).
+  float red[4];
+  {
+    float h8[8];
 #pragma unroll
-  for (int j = 0; j < GQ; ++j) {
-    if (lane == 0) {
+    for (int i = 0; i < 8; ++i) {
+      const float a = acc[(2 * i) >> 3][(2 * i) & 7], b = acc[(2 * i + 1) >> 3][(2 * i + 1) & 7];
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+      h8[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(h8[2 * k]), __float_as_uint(h8[2 * k + 1]),
+                                                      false, false);
+      red[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int t = 4 * k + 2 * (kq & 1) + (kq >> 1);
+    s_o[wave][t >> 3][dq * 8 + (t & 7)] = red[k];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < GQ; ++j) {
       s_ml[wave][j][0] = mx[j];
       s_ml[wave][j][1] = l[j];
     }
-    float4* dst = reinterpret_cast<float4*>(&s_o[wave][kq][j][dq * 8]);
-    dst[0] = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-    dst[1] = make_float4(acc[j][4], acc[j][5], acc[j][6], acc[j][7]);
   }
   STAMP(7);
   __syncthreads();
@@ -1160,14 +1188,11 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     const float mw = s_ml[w][j][0];
     const float wt = mw == -INFINITY ? 0.f : __expf(mw - M);
     L += wt * s_ml[w][j][1];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float4 t = *reinterpret_cast<const float4*>(&s_o[w][r][j][d0]);
-      o.x += wt * t.x;
-      o.y += wt * t.y;
-      o.z += wt * t.z;
-      o.w += wt * t.w;
-    }
+    const float4 t = *reinterpret_cast<const float4*>(&s_o[w][j][d0]);
+    o.x += wt * t.x;
+    o.y += wt * t.y;
+    o.z += wt * t.z;
+    o.w += wt * t.w;
   }
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;
   if (n_active == 1) {
@@ -1189,38 +1214,47 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STAMP(11);
   int last = 0;
   if (lane == 0) last = __hip_atomic_fetch_add(counters + (m * KV + g) * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   last = __builtin_amdgcn_readfirstlane(last);
   if (last != n_active - 1) return;
   STAMP(9);
-  // last split: combine all n_active partials
-  f4v pml[ASPLIT], po[ASPLIT];
-#pragma unroll
-  for (int t = 0; t < ASPLIT; ++t) {
-    const int tt = min(t, n_active - 1);
-    pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
-    po[t] = ld_sc1_f4(rs, (tt * APART + j * D + d0) * 4);
-  }
-  float MM = -INFINITY;
-#pragma unroll
-  for (int t = 0; t < ASPLIT; ++t)
-    if (t < n_active) MM = fmaxf(MM, j ? pml[t].z : pml[t].x);
-  float LL = 0.f;
+  // last split: combine all n_active partials, CH at a time (all loads of a chunk in flight together)
+  constexpr int CH = ASPLIT;
+  float MM = -INFINITY, LL = 0.f;
   f4v oo = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < n_active; c0 += CH) {
+    f4v pml[CH], po[CH];
 #pragma unroll
-  for (int t = 0; t < ASPLIT; ++t) {
-    if (t < n_active) {
-      const float mt = j ? pml[t].z : pml[t].x;
-      const float wt = mt == -INFINITY ? 0.f : __expf(mt - MM);
-      LL += wt * (j ? pml[t].w : pml[t].y);
-      oo += wt * po[t];
+    for (int t = 0; t < CH; ++t) {
+      const int tt = min(c0 + t, n_active - 1);
+      pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
+      po[t] = ld_sc1_f4(rs, (tt * APART + j * D + d0) * 4);
     }
+    float mn = MM;
+#pragma unroll
+    for (int t = 0; t < CH; ++t)
+      if (c0 + t < n_active) mn = fmaxf(mn, j ? pml[t].z : pml[t].x);
+    const float alpha = MM == -INFINITY ? 0.f : __expf(MM - mn);
+    LL *= alpha;
+    oo *= alpha;
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      if (c0 + t < n_active) {
+        const float mt = j ? pml[t].z : pml[t].x;
+        const float wt = mt == -INFINITY ? 0.f : __expf(mt - mn);
+        LL += wt * (j ? pml[t].w : pml[t].y);
+        oo += wt * po[t];
+      }
+    }
+    MM = mn;
   }
   const float4 r = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
   *reinterpret_cast<float4*>(op) = r;
   if (qout) store_q8_row4(qout, dout, (int64_t)m * H * D + (g * GQ + j) * D + d0, lane, r);
   if (lane == 0) __hip_atomic_store(counters + (m * KV + g) * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  STAMP(10);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
@@ -1233,10 +1267,9 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // 4 at batch 32, 1 for prefill
   int lg = 0;
   while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= 1024) ++lg;
-  hipLaunchKernelGGL(decode_mode ? k_attn_block<1> : k_attn_block<0>, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq,
-                     tok_pos, lg, decode_mode, H, KV,
-                     seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials, qout,
-                     dout);
+  hipLaunchKernelGGL(decode_mode ? k_attn_block<1> : k_attn_block<0>, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode,
+                     H, KV, seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials,
+                     qout, dout);
 }
 
 // ------------------------------------------------------------------------------------------------
