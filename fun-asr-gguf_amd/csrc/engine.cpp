@@ -1,7 +1,7 @@
 // libfunasr_hip: C-ABI engine for the Fun-ASR hot path on MI355X (see include/funasr_hip.h).
 //
 // Owns, per GPU: all weights (encoder f32, decoder q8_0 in engine layout), activation arenas sized
-// for max_batch x max_samples, the fp16 KV cache [layer][seq][n_ctx][kv*128], one HIP stream.
+// for max_batch x max_samples, the fp16 KV cache [layer][seq][kv head][n_ctx][128], one HIP stream.
 // Encoder math follows model_definition.py (SenseVoiceEncoderSmall / CorrectTransformerAdaptor /
 // CTC head); decoder math follows llama.cpp's qwen3 graph with ggml q8_0 numerics (oracle/qwen3.py).
 #include <algorithm>
@@ -577,8 +577,8 @@ struct Engine {
     FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * CNT_LINE * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
     // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)
-    gk_cnt_n = 256;
-    gk_part_n = (int64_t)256 * 8 * 2 * 1024;
+    gk_cnt_n = 1024;                             // tiles of a split-K launch
+    gk_part_n = (int64_t)1024 * 2 * 1024;        // tiles x splits x (1 or 2 matrices) x 32 x 32 partial floats
     gk_cnt = alloc<int>(gk_cnt_n * CNT_LINE);
     FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * CNT_LINE * sizeof(int)));
     gk_part = alloc<float>(gk_part_n);

@@ -301,12 +301,20 @@ __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, i
 // decode GEMV: [start, prologue done, rows done, end] -> g_gstamps[block]
 #ifdef FA_GEMV_STAMPS
 __device__ unsigned long long g_gstamps[4096][4];
-#define GSTAMP(i) do { if (threadIdx.x == 0 && blockIdx.y == 0) g_gstamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define GSTAMP(i) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4096) g_gstamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 void gemv_stamps_read(unsigned long long* host, int n) {
   (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gstamps), (size_t)n * 32, 0, hipMemcpyDeviceToHost);
 }
+// split-K GEMM: [start, loads landed, reduced in LDS, partial published, arrival counted, end], linear block id
+__device__ unsigned long long g_kstamps[4096][6];
+#define KSTAMP(i) do { const unsigned bid = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x; \
+  if (threadIdx.x == 0 && bid < 4096) g_kstamps[bid][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+void gemm_stamps_read(unsigned long long* host, int n) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_kstamps), (size_t)n * 48, 0, hipMemcpyDeviceToHost);
+}
 #else
 #define GSTAMP(i) do { } while (0)
+#define KSTAMP(i) do { } while (0)
 #endif
 
 template <int NCH, int MT, bool FUSED, int EPI>
@@ -438,66 +446,117 @@ static void launch_gemv_k(int K, const GemvArgs& a, hipStream_t s) {
 // LDS in fixed wave order (deterministic). Epilogues as k_gemv_q8.
 typedef int i32x16_t __attribute__((ext_vector_type(16)));
 
-template <int EPI>
-__global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS) {
-  constexpr int NG = 4;  // q8_0 blocks per load group
-  const int nb = K >> 5, nbk = nb / KS;  // blocks per K split
+// Scales of NBW consecutive q8_0 blocks of one weight row (fp16, NBW/2 dwords): one load instruction
+template <int NBW>
+__device__ __forceinline__ void load_scales(const __half* p, uint32_t (&d)[NBW / 2]) {
+  if constexpr (NBW == 8) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  } else if constexpr (NBW == 4) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    d[0] = v.x; d[1] = v.y;
+  } else {
+    d[0] = *reinterpret_cast<const uint32_t*>(p);
+  }
+}
+
+// SwiGLU epilogue's q8_0 rows: the tile's 32 rows of a token are one q8_0 block of the down projection's input,
+// quantised exactly as norm_quant_row does (no prep launch). s_act = tile [token][row]; threads 0..63: token
+// t & 31, rows [16 (t >> 5), +16)
+__device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const GemvArgs& a, int t0, int o0) {
+  if (threadIdx.x >= 64) return;
+  const int tk = threadIdx.x & 31, hh = threadIdx.x >> 5;
+  float vv[16], am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    vv[i] = s_act[tk][16 * hh + i];
+    am = fmaxf(am, fabsf(vv[i]));
+  }
+  am = fmaxf(am, __shfl_xor(am, 32, 64));
+  const float d = am / 127.0f;
+  const float id = d != 0.0f ? 1.0f / d : 0.0f;
+  int32_t pk[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b0 = (int)roundf(__fmul_rn(vv[4 * j], id)) & 0xFF, b1 = (int)roundf(__fmul_rn(vv[4 * j + 1], id)) & 0xFF;
+    const int b2 = (int)roundf(__fmul_rn(vv[4 * j + 2], id)) & 0xFF, b3 = (int)roundf(__fmul_rn(vv[4 * j + 3], id)) & 0xFF;
+    pk[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  }
+  if (t0 + tk < a.M) {
+    *reinterpret_cast<int4*>(a.qout + (int64_t)(t0 + tk) * a.ldo + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+    if (hh == 0) a.dout[(int64_t)(t0 + tk) * (a.ldo / 32) + o0 / 32] = __half2float(__float2half_rn(d));
+  }
+}
+
+// Split-K form (few-tile shapes: batched decode, the o GEMM of prefill). Block = 4 waves over one 32x32 tile and one
+// K split of 4 NBW q8_0 blocks (SwiGLU: 2 waves per matrix); every wave issues ALL its weight / activation / scale
+// loads before its MFMAs (one memory round trip), and the residual is fetched before the hop. Splits merge by last
+// arriver (sc1 partials, MI355X_MICROARCH.md hand-off table row 1) with the KSM partial loads in flight together,
+// summed in split order (deterministic).
+template <int EPI, int NBW, int KSM>
+__global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
+  constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
+  constexpr int NS = EPI == 2 ? 2 : 1;
+  const int nb = K >> 5;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32, ks = blockIdx.z;
-  // SwiGLU: waves 0-1 take the gate matrix, 2-3 the up matrix (one accumulator set per wave);
-  // otherwise the 4 waves take K quarters
   const bool upw = EPI == 2 && wave >= 2;
-  const int nbw = EPI == 2 ? nbk >> 1 : nbk >> 2;
-  const int bw0 = ks * nbk + (EPI == 2 ? (wave & 1) : wave) * nbw;
+  const int bw0 = (ks * WPM + (EPI == 2 ? (wave & 1) : wave)) * NBW;  // host: nb == KS * WPM * NBW
   const int8_t* wq = upw ? a.wq2 : a.wq;
   const __half* wd = upw ? a.wd2 : a.wd;
-  const int o_a = min(o0 + r, a.O - 1);
+  const int8_t* wa = wq + (int64_t)min(o0 + r, a.O - 1) * K + 16 * h + bw0 * 32;
   const int t_b = min(t0 + r, a.M - 1);
-  const int8_t* wa = wq + (int64_t)o_a * K + 16 * h;
-  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h;
-  const float* xd = a.xd + (int64_t)t_b * nb;
+  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + bw0 * 32;
+  KSTAMP(0);
+  i32x4_t A[NBW], B[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
+    B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
+  }
+  uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg)
+    load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
+  float2 dx2[NBW / 2];
+#pragma unroll
+  for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + bw0 + 2 * q);
+  // this thread finalises regs [4 g, 4 g + 4) of lane l (token col, rows rrow): residual fetched now, used after the hop
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6, col = l & 31, tok = t0 + col;
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int reg = 4 * g + q, row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5), a.O - 1);
+      rv[q] = a.res[(int64_t)min(tok, a.M - 1) * a.ldr + row];
+    }
+  }
+#ifdef FA_GEMV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  KSTAMP(1);
+#endif
   float acc[16];
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
   const i32x16_t zero = {};
-  for (int b0 = bw0; b0 < bw0 + nbw; b0 += NG) {
-    i32x4_t A[NG], B[NG];
 #pragma unroll
-    for (int j = 0; j < NG; ++j) {
-#ifdef FA_GEMM_NT_LOADS
-      A[j] = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(wa + (b0 + j) * 32));
-#else
-      A[j] = *reinterpret_cast<const i32x4_t*>(wa + (b0 + j) * 32);
-#endif
-      B[j] = *reinterpret_cast<const i32x4_t*>(xb + (b0 + j) * 32);
-    }
-    uint2 dw[16];  // NG fp16 scales of each of this lane's 16 rows
+  for (int j = 0; j < NBW; ++j) {
+    const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
+    const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
-      dw[reg] = *reinterpret_cast<const uint2*>(wd + (int64_t)row * nb + b0);
-    }
-    const float4 dx4 = *reinterpret_cast<const float4*>(xd + b0);
-    const float dx[NG] = {dx4.x, dx4.y, dx4.z, dx4.w};
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-      const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const __half* hw = reinterpret_cast<const __half*>(&dw[reg]);
-        acc[reg] += (float)D[reg] * (__half2float(hw[j]) * dx[j]);
-      }
+      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 1]);
+      acc[reg] += (float)D[reg] * (__half2float(hw[j & 1]) * dx);
     }
   }
-  // fixed-order reduction over the waves; thread t finalises regs [4 (t>>6), +4) of lane t&63
+  // fixed-order reduction over the waves
   __shared__ float s_red[4][16][64];
-  __shared__ float s_out[32][33];  // EPI 3: [token][row] for the per-token argmax
+  __shared__ float s_act[EPI >= 2 ? 32 : 1][33];  // tile [token][row]: SwiGLU q8_0 epilogue, lm_head argmax
   __shared__ int s_last;
-  constexpr int NS = EPI == 2 ? 2 : 1;
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
   __syncthreads();
-  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  KSTAMP(2);
   float y[4], y2[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -510,58 +569,70 @@ __global__ __launch_bounds__(256) void k_gemm_q8_mfma(GemvArgs a, int K, int KS)
       y2[q] = 0.f;
     }
   }
-  if (KS > 1) {
-    // split-K: publish this split's tile (sc1), count arrivals; the last split sums all KS tiles in
-    // split order (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1)
+  if (KSM > 1 && KS > 1) {
     typedef float f4v __attribute__((ext_vector_type(4)));
-      const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     float* base = a.kpart + (int64_t)tile * KS * (NS * 1024);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * NS * 1024 * 4);
-    const f4v v = {y[0], y[1], y[2], y[3]};
-    st_sc1_f4(v, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4);
-    if (EPI == 2) {
-      const f4v v2 = {y2[0], y2[1], y2[2], y2[3]};
-      st_sc1_f4(v2, rs, (ks * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
-    }
+    st_sc1_f4(f4v{y[0], y[1], y[2], y[3]}, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4);
+    if (EPI == 2) st_sc1_f4(f4v{y2[0], y2[1], y2[2], y2[3]}, rs, (ks * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    KSTAMP(3);
     if (threadIdx.x == 0)
       s_last = __hip_atomic_fetch_add(a.kcnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
     __syncthreads();
     if (!s_last) return;
-    f4v sum = {0.f, 0.f, 0.f, 0.f}, sum2 = {0.f, 0.f, 0.f, 0.f};
-    for (int k2 = 0; k2 < KS; ++k2) {
-      sum += ld_sc1_f4(rs, (k2 * NS * 1024 + threadIdx.x * 4) * 4);
-      if (EPI == 2) sum2 += ld_sc1_f4(rs, (k2 * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
+    KSTAMP(4);
+    f4v pv[KSM], pv2[EPI == 2 ? KSM : 1];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) {  // all in flight (clamped duplicates past KS are not summed)
+      const int kk = min(k2, KS - 1);
+      pv[k2] = ld_sc1_f4(rs, (kk * NS * 1024 + threadIdx.x * 4) * 4);
+      if (EPI == 2) pv2[k2] = ld_sc1_f4(rs, (kk * NS * 1024 + 1024 + threadIdx.x * 4) * 4);
+    }
+    f4v sum = pv[0], sum2 = EPI == 2 ? pv2[0] : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k2 = 1; k2 < KSM; ++k2) {
+      if (k2 < KS) {
+        sum += pv[k2];
+        if (EPI == 2) sum2 += pv2[k2];
+      }
     }
     y[0] = sum.x; y[1] = sum.y; y[2] = sum.z; y[3] = sum.w;
     y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
     if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const int col = l & 31, tok = t0 + col;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int reg = 4 * g + q;
     const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
     const int row = o0 + rrow;
-    if (EPI == 3) s_out[col][rrow] = row < a.O ? y[q] : -INFINITY;
+    float v = 0.f;
     if (row < a.O && tok < a.M) {
       float* op = a.out + (int64_t)tok * a.ldo + row;
-      if (EPI == 0 || EPI == 3) *op = y[q];
-      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y[q];
-      else *op = (y[q] / (1.0f + expf(-y[q]))) * y2[q];
+      if (EPI == 0 || EPI == 3) *op = v = y[q];
+      else if (EPI == 1) *op = rv[q] + y[q];
+      else *op = v = (y[q] / (1.0f + expf(-y[q]))) * y2[q];
     }
+    if (EPI == 2) s_act[col][rrow] = v;
+    if (EPI == 3) s_act[col][rrow] = row < a.O ? v : -INFINITY;
   }
   if (EPI == 3) {
     __syncthreads();
     if (threadIdx.x < 32 && t0 + threadIdx.x < a.M) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
-      for (int rr = 0; rr < 32; ++rr) argmax_combine(bv, bi, s_out[threadIdx.x][rr], o0 + rr);
+      for (int rr = 0; rr < 32; ++rr) argmax_combine(bv, bi, s_act[threadIdx.x][rr], o0 + rr);
       a.pval[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bv;
       a.pidx[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bi;
     }
   }
+  if (EPI == 2 && a.qout) {
+    __syncthreads();
+    swiglu_tile_q8(s_act, a, t0, o0);
+  }
+  KSTAMP(5);
 }
 
 // Same GEMM with K split over the NW waves of ONE block instead of over blocks: no cross-block split-K hop (on
@@ -584,6 +655,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   const int8_t* wa = wq + (int64_t)min(o0 + r, a.O - 1) * K + 16 * h + b0 * 32;
   const int t_b = min(t0 + r, a.M - 1);
   const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + b0 * 32;
+  GSTAMP(0);
   i32x4_t A[NBW], B[NBW];
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
@@ -604,6 +676,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
   const i32x16_t zero = {};
+#ifdef FA_GEMV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GSTAMP(1);
+#endif
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
@@ -638,6 +714,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
     for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
   }
   __syncthreads();
+  GSTAMP(2);
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int col = l & 31, tok = t0 + col;
 #pragma unroll
@@ -673,33 +750,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
     }
   }
   if (EPI == 2 && a.qout) {
-    // the tile's 32 rows of a token are one q8_0 block of the down projection's input: quantise it here, exactly
-    // as norm_quant_row does (no prep launch); thread t < 64: token t & 31, rows [16 (t >> 5), +16)
     __syncthreads();
-    if (threadIdx.x < 64) {
-      const int tk = threadIdx.x & 31, hh = threadIdx.x >> 5;
-      float vv[16], am = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        vv[i] = s_act[tk][16 * hh + i];
-        am = fmaxf(am, fabsf(vv[i]));
-      }
-      am = fmaxf(am, __shfl_xor(am, 32, 64));
-      const float d = am / 127.0f;
-      const float id = d != 0.0f ? 1.0f / d : 0.0f;
-      int32_t pk[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int b0 = (int)roundf(__fmul_rn(vv[4 * j], id)) & 0xFF, b1 = (int)roundf(__fmul_rn(vv[4 * j + 1], id)) & 0xFF;
-        const int b2 = (int)roundf(__fmul_rn(vv[4 * j + 2], id)) & 0xFF, b3 = (int)roundf(__fmul_rn(vv[4 * j + 3], id)) & 0xFF;
-        pk[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
-      }
-      if (t0 + tk < a.M) {
-        *reinterpret_cast<int4*>(a.qout + (int64_t)(t0 + tk) * a.ldo + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
-        if (hh == 0) a.dout[(int64_t)(t0 + tk) * (a.ldo / 32) + o0 / 32] = __half2float(__float2half_rn(d));
-      }
-    }
+    swiglu_tile_q8(s_act, a, t0, o0);
   }
+  GSTAMP(3);
 }
 
 template <int EPI, int NW, int NBW>
@@ -714,7 +768,7 @@ static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
   constexpr int nw = 8;
   // batched decode (a few hundred tiles or less) measured 2.6 % faster per step on the split-K block kernel
   // (1.974 vs 2.027 ms at batch 32, same box); prefill-sized grids take this one
-  if ((int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) < 256) return false;
+  if (g_gemm_q8_kw < 2 && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) < 256) return false;
   const int nb = (K / 32) * (epi == 2 ? 2 : 1);
   if (nb % nw) return false;
   switch (epi * 100 + nb / nw) {
@@ -725,19 +779,32 @@ static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
     case 108: launch_gemm_kw<1, nw, 8>(a, K, s); return true;
     case 112: launch_gemm_kw<1, nw, 12>(a, K, s); return true;
     case 208: launch_gemm_kw<2, nw, 8>(a, K, s); return true;
-    case 304: launch_gemm_kw<3, nw, 4>(a, K, s); return true;
     default: return false;
   }
 }
 
-int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0)
+int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0); 2: K-in-block for all
 
-int gemm_k_splits(int O, int M, int K) {
-  const int tiles = cdiv(O, 32) * cdiv(M, 32);
-  const int nb = K / 32;
-  int ks = 1;
-  for (int c : {2, 3, 4, 6, 8})
-    if (tiles * ks < 256 && nb % (16 * c) == 0 && tiles * c <= 1024) ks = c;
+// split-K shape: NBW q8_0 blocks per wave (8, 4 or 2: one load round trip) and KS = nb / (waves per matrix x NBW)
+// splits; the largest NBW whose split count fills the chip (>= 256 blocks), else the most splits. lm_head's argmax
+// needs whole sums: one split.
+void gemm_sk_shape(int O, int M, int K, int epi, int* nbw, int* ks) {
+  const int tiles = cdiv(O, 32) * cdiv(M, 32), nb = K / 32, wpm = epi == 2 ? 2 : 4;
+  *nbw = 0;
+  *ks = 0;
+  for (int c : {8, 4, 2}) {
+    if (nb % (wpm * c)) continue;
+    const int k = nb / (wpm * c);
+    if (k > (epi == 2 ? 4 : 16) || (epi == 3 && k != 1)) continue;
+    *nbw = c;
+    *ks = k;
+    if (tiles * k >= 256) return;
+  }
+}
+
+int gemm_k_splits(int O, int M, int K, int epi) {
+  int nbw, ks;
+  gemm_sk_shape(O, M, K, epi, &nbw, &ks);
   return ks;
 }
 
@@ -766,20 +833,24 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
   if (g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
-  int KS = (a.kpart && a.kcnt && epi != 3) ? gemm_k_splits(a.O, a.M, K) : 1;
+  int NBW, KS;
+  gemm_sk_shape(a.O, a.M, K, epi, &NBW, &KS);
+  FA_REQUIRE(NBW > 0, "gemm_q8: no split-K shape");
   if (KS > 1)
-    FA_REQUIRE((int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) <= a.kcnt_n &&
+    FA_REQUIRE(a.kpart && a.kcnt && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) <= a.kcnt_n &&
                    (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) * KS * (epi == 2 ? 2 : 1) * 1024 <= a.kpart_n,
                "gemm_q8: split-K workspace too small");
-  dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
-  switch (epi) {
-    case 0: hipLaunchKernelGGL(k_gemm_q8_mfma<0>, grid, dim3(256), 0, s, a, K, KS); break;
-    case 1: hipLaunchKernelGGL(k_gemm_q8_mfma<1>, grid, dim3(256), 0, s, a, K, KS); break;
-    case 2: hipLaunchKernelGGL(k_gemm_q8_mfma<2>, grid, dim3(256), 0, s, a, K, KS); break;
-    case 3: hipLaunchKernelGGL(k_gemm_q8_mfma<3>, grid, dim3(256), 0, s, a, K, KS); break;
+  const dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
+  const int ksm = KS == 1 ? 1 : KS <= 4 ? 4 : 16;
+  switch (epi * 1000 + NBW * 100 + ksm) {
+#define SK(E, N, Q) case E * 1000 + N * 100 + Q: hipLaunchKernelGGL((k_gemm_q8_sk<E, N, Q>), grid, dim3(256), 0, s, a, K, KS); break;
+    SK(0, 2, 1) SK(0, 2, 4) SK(0, 2, 16) SK(0, 4, 1) SK(0, 4, 4) SK(0, 4, 16) SK(0, 8, 1) SK(0, 8, 4) SK(0, 8, 16)
+    SK(1, 2, 1) SK(1, 2, 4) SK(1, 2, 16) SK(1, 4, 1) SK(1, 4, 4) SK(1, 4, 16) SK(1, 8, 1) SK(1, 8, 4) SK(1, 8, 16)
+    SK(2, 2, 1) SK(2, 2, 4) SK(2, 4, 1) SK(2, 4, 4) SK(2, 8, 1) SK(2, 8, 4)
+    SK(3, 8, 1)
+#undef SK
+    default: FA_REQUIRE(false, "gemm_q8: split-K shape not instantiated");
   }
-  // this kernel has no quantising epilogue: produce the requested q8_0 rows of out with a prep launch
-  if (a.qout) prep_q8(a.out, a.ldo, nullptr, 0.f, a.M, a.O, a.qout, a.dout, s);
 }
 
 int lm_head_parts(int O, int M) { return M <= 4 ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
@@ -801,12 +872,14 @@ __global__ void k_qk_rope_store(const float* __restrict__ qkv, int M, int H, int
   if (slot >= n_slots || m >= M) return;
   const float* src = qkv + (int64_t)m * (H + 2 * KV) * D + slot * D;
   const int pos = tok_pos[m];
-  const int64_t cbase = (int64_t)tok_seq[m] * seq_stride + (int64_t)pos * KV * D;
+  // head-major cache [seq][kv head][n_ctx][D]: kv head g's rows at cbase + g * (seq_stride / KV)
+  const int64_t cbase = (int64_t)tok_seq[m] * seq_stride + (int64_t)pos * D;
+  const int64_t hs = seq_stride / KV;
   float x0 = src[lane], x1 = src[lane + 64];
   if (slot >= H + KV) {  // V: store as-is
     const int g = slot - H - KV;
-    vc[cbase + g * D + lane] = __float2half_rn(x0);
-    vc[cbase + g * D + lane + 64] = __float2half_rn(x1);
+    vc[cbase + g * hs + lane] = __float2half_rn(x0);
+    vc[cbase + g * hs + lane + 64] = __float2half_rn(x1);
     return;
   }
   const float* w = slot < H ? qn : kn;
@@ -821,8 +894,8 @@ __global__ void k_qk_rope_store(const float* __restrict__ qkv, int M, int H, int
     qout[((int64_t)m * H + slot) * D + lane + 64] = y1;
   } else {
     const int g = slot - H;
-    kc[cbase + g * D + lane] = __float2half_rn(y0);
-    kc[cbase + g * D + lane + 64] = __float2half_rn(y1);
+    kc[cbase + g * hs + lane] = __float2half_rn(y0);
+    kc[cbase + g * hs + lane + 64] = __float2half_rn(y1);
   }
 }
 
@@ -859,6 +932,8 @@ void attn_stamps_clear() {
 #endif
 constexpr int GQ = 2;     // query heads per kv head (Qwen3-0.6B: 16 / 8)
 constexpr int AWV = 4;    // waves per block
+int g_attn_blocks = 1024;  // key splits are added while (token, kv head, split) blocks stay within this many
+int g_attn_lean = -1;      // -1: lean blocks when a launch needs more than 3 per CU; 0 / 1 force (A/B)
 constexpr int AGI = 16;   // 4-key groups per wave per pass (registers: 16 int4 of K + 16 of V)
 constexpr int ASPLIT = ATTN_SPLITS;  // key splits (blocks) per (token, kv head)
 constexpr int AMIN_G = 8;            // minimum 4-key groups per split (32 keys = 16 KB of K+V)
@@ -874,7 +949,7 @@ __device__ __forceinline__ void load_kv_groups(const __half* __restrict__ base, 
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int k = min(4 * (g0 + AW * i) + kq, n_keys - 1);
-    t[i] = *reinterpret_cast<const int4*>(base + (int64_t)k * KV * D + dq * 8);
+    t[i] = *reinterpret_cast<const int4*>(base + (int64_t)k * D + dq * 8);  // head-major cache: rows D apart
   }
 }
 
@@ -1051,10 +1126,13 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // (parameter order = kernarg layout: everything the prologue needs sits in the first 64-B line)
 // DM = decode_mode as a template constant: a runtime branch between the q loads and the K/V stream made the
 // wait-count pass drain the q loads at the join, before the K/V loads were issued
-template <int DM>
-__global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+// LEAN (batched decode, several blocks per CU): at most 4 groups per wave pass and a 4-partial combine chunk, so
+// the kernel fits 128 VGPRs and 4 blocks share a CU (every block of a batch-32 launch resident at once)
+template <int DM, int LEAN>
+__global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
                                                          int lg_nsplit, int decode_mode, int H, int KV,
-                                                         int64_t seq_stride, __half* __restrict__ kc,
+                                                         int64_t seq_stride, int64_t head_stride,
+                                                         __half* __restrict__ kc,
                                                          __half* __restrict__ vc, const float* __restrict__ qsrc,
                                                          const float* __restrict__ qn, const float* __restrict__ kn,
                                                          const float* __restrict__ rcos, const float* __restrict__ rsin,
@@ -1069,7 +1147,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   // pos "depends" on seq and on the pointer arguments: the two index loads and every kernarg line are
   // fetched together, before the first use (otherwise each is a serial scalar-load latency)
   asm volatile("" : "+s"(pos) : "s"(seq), "s"(qsrc), "s"(kc), "s"(vc), "s"(rcos), "s"(rsin), "s"(qn), "s"(kn),
-               "s"(seq_stride), "s"(out), "s"(partials));
+               "s"(seq_stride), "s"(head_stride), "s"(out), "s"(partials));
   STAMP(0);
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
@@ -1079,8 +1157,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   if (sp >= n_active) return;                                      // uniform over the block
   const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
   STAMP(1);
-  __half* kb = kc + (int64_t)seq * seq_stride + g * D;
-  __half* vb = vc + (int64_t)seq * seq_stride + g * D;
+  __half* kb = kc + (int64_t)seq * seq_stride + g * head_stride;
+  __half* vb = vc + (int64_t)seq * seq_stride + g * head_stride;
   __shared__ float s_q[AWV][GQ][D];          // per-wave q (scaled, roped) in natural dim order
   __shared__ float s_kn[D], s_vn[D];        // fresh K/V row (decode)
   __shared__ float s_ml[AWV][GQ][2];
@@ -1125,8 +1203,8 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
         qi.x1[j] = qp[lane + 64];
       }
     }
-    __half* kd = kb + (int64_t)pos * KV * D;
-    __half* vd = vb + (int64_t)pos * KV * D;
+    __half* kd = kb + (int64_t)pos * D;
+    __half* vd = vb + (int64_t)pos * D;
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
       attn_wave<1, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
@@ -1134,7 +1212,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
     else if (ni <= 2)
       attn_wave<2, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
-    else if (ni <= 4)
+    else if (ni <= 4 || LEAN)
       attn_wave<4, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
     else
@@ -1221,7 +1299,7 @@ __global__ __launch_bounds__(AWV * 64) void k_attn_block(const int* __restrict__
   if (last != n_active - 1) return;
   STAMP(9);
   // last split: combine all n_active partials, CH at a time (all loads of a chunk in flight together)
-  constexpr int CH = ASPLIT;
+  constexpr int CH = LEAN ? 4 : ASPLIT;
   float MM = -INFINITY, LL = 0.f;
   f4v oo = {0.f, 0.f, 0.f, 0.f};
   for (int c0 = 0; c0 < n_active; c0 += CH) {
@@ -1266,9 +1344,12 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // key splits (a power of two) only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1,
   // 4 at batch 32, 1 for prefill
   int lg = 0;
-  while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= 1024) ++lg;
-  hipLaunchKernelGGL(decode_mode ? k_attn_block<1> : k_attn_block<0>, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode,
-                     H, KV, seq_stride, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials,
+  while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= g_attn_blocks) ++lg;
+  const bool lean = g_attn_lean >= 0 ? g_attn_lean != 0 : (M * KV << lg) > 3 * 256;
+  auto kern = lean ? (decode_mode ? k_attn_block<1, 1> : k_attn_block<0, 1>)
+                   : (decode_mode ? k_attn_block<1, 0> : k_attn_block<0, 0>);
+  hipLaunchKernelGGL(kern, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode,
+                     H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials,
                      qout, dout);
 }
 

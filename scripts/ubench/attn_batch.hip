@@ -1,0 +1,61 @@
+// Batched decode attention (C3 shape): 32 tokens, each its own sequence at n_past in [200, 460], 28 layers of
+// distinct fp16 K/V caches (cold, like the engine), graph-replayed. Prints us per launch and the K/V bytes
+// rate for each (split target, lean) setting.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+#include "../../fun-asr-gguf_amd/csrc/kernels.h"
+namespace fa {
+void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
+void log(int, const std::string&) {}
+}
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+using namespace fa;
+template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T))); return (T*)p; }
+int main(int argc, char** argv) {
+  hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int M = 32, H = 16, KV = 8, D = 128, NCTX = argc > 1 ? atoi(argv[1]) : 1024, L = 28, QKV = (H + 2 * KV) * D;
+  AttnWork wk; wk.max_tokens = M; wk.max_kv = KV;
+  CK(hipMalloc(&wk.counters, (size_t)M * KV * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, (size_t)M * KV * CNT_LINE * 4));
+  CK(hipMalloc(&wk.partials, (size_t)M * KV * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
+  const int64_t seq_stride = (int64_t)NCTX * KV * D;  // per sequence per layer
+  const size_t layer = (size_t)M * seq_stride;
+  float* qkv = dalloc<float>((size_t)M * QKV); launch_synth_fill(qkv, (int64_t)M * QKV, 9, 1.f, 0.f, s);
+  float* att = dalloc<float>((size_t)M * H * D);
+  __half* kc = dalloc<__half>(L * layer); __half* vc = dalloc<__half>(L * layer);
+  CK(hipMemset(kc, 0, L * layer * 2)); CK(hipMemset(vc, 0, L * layer * 2));
+  float* rc = dalloc<float>(NCTX * 64); float* rs = dalloc<float>(NCTX * 64);
+  launch_synth_fill(rc, NCTX * 64, 12, 1.f, 0.f, s); launch_synth_fill(rs, NCTX * 64, 13, 1.f, 0.f, s);
+  float* qn = dalloc<float>(D); launch_synth_fill(qn, D, 14, 0.1f, 1.f, s);
+  std::vector<int> hseq(M), hpos(M);
+  double keys = 0;
+  for (int m = 0; m < M; ++m) { hseq[m] = m; hpos[m] = 200 + (m * 97) % 261; keys += hpos[m] + 1; }
+  int* seq = dalloc<int>(M); int* pos = dalloc<int>(M);
+  CK(hipMemcpy(seq, hseq.data(), M * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(pos, hpos.data(), M * 4, hipMemcpyHostToDevice));
+  CK(hipStreamSynchronize(s));
+  const double bytes = keys * KV * D * 2 * 2;  // K and V rows read per layer
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  printf("n_ctx per sequence slot %d\n", NCTX);
+  for (int target : {256, 1024}) {
+    for (int lean : {0, 1}) {
+      g_attn_blocks = target; g_attn_lean = lean;
+      hipGraph_t g; hipGraphExec_t ex;
+      CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      for (int l = 0; l < L; ++l)
+        attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, M, H, KV, seq, pos, seq_stride, att, wk, s);
+      CK(hipStreamEndCapture(s, &g)); CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(ex, s));
+      CK(hipStreamSynchronize(s));
+      const int R = 20;
+      CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
+      const double us = ms * 1e3 / R / L;
+      printf("blocks target %4d lean %d: %6.2f us per launch, K/V %.1f MB -> %.2f TB/s\n", target, lean, us, bytes / 1e6,
+             bytes / (us * 1e-6) / 1e12);
+      CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
+    }
+  }
+  return 0;
+}

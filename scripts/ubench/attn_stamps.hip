@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include "../../fun-asr-gguf_amd/csrc/kernels.h"
@@ -22,36 +23,49 @@ static void stats(const char* name, std::vector<double> v) {
   printf("  %-24s n=%3zu  min %6.2f  p50 %6.2f  p90 %6.2f  max %6.2f us\n", name, v.size(), v[0], v[v.size() / 2],
          v[v.size() * 9 / 10], v.back());
 }
-int main() {
+int main(int argc, char** argv) {
+  // argv[1] = M tokens (default 1: one sequence at n_past 40 / 330 / 700; M > 1: token m is sequence m at
+  // n_past 200 + (97 m) % 261, the C3 batch shape)
+  const int M = argc > 1 ? atoi(argv[1]) : 1;
+  if (const char* e = getenv("FUNASR_ATTN_LEAN")) g_attn_lean = atoi(e);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
-  CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
-  CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
-  const int H = 16, KV = 8, D = 128, NCTX = 2048, QKV = 4096;
-  float* qkv = dalloc<float>(QKV); launch_synth_fill(qkv, QKV, 9, 1.f, 0.f, s);
-  float* att = dalloc<float>(H * D);
-  __half* kc = dalloc<__half>((size_t)28 * NCTX * KV * D); __half* vc = dalloc<__half>((size_t)28 * NCTX * KV * D);
-  CK(hipMemset(kc, 0, (size_t)28 * NCTX * KV * D * 2)); CK(hipMemset(vc, 0, (size_t)28 * NCTX * KV * D * 2));
+  const int H = 16, KV = 8, D = 128, NCTX = 1024, QKV = 4096;
+  AttnWork wk; wk.max_tokens = M; wk.max_kv = KV;
+  CK(hipMalloc(&wk.counters, (size_t)M * KV * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, (size_t)M * KV * CNT_LINE * 4));
+  CK(hipMalloc(&wk.partials, (size_t)M * KV * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
+  const int64_t seq_stride = (int64_t)NCTX * KV * D;
+  const size_t layer = (size_t)M * seq_stride;
+  float* qkv = dalloc<float>((size_t)M * QKV); launch_synth_fill(qkv, (int64_t)M * QKV, 9, 1.f, 0.f, s);
+  float* att = dalloc<float>((size_t)M * H * D);
+  __half* kc = dalloc<__half>(28 * layer); __half* vc = dalloc<__half>(28 * layer);
+  CK(hipMemset(kc, 0, 28 * layer * 2)); CK(hipMemset(vc, 0, 28 * layer * 2));
   float* rc = dalloc<float>(NCTX * 64); float* rs = dalloc<float>(NCTX * 64);
   launch_synth_fill(rc, NCTX * 64, 12, 1.f, 0.f, s); launch_synth_fill(rs, NCTX * 64, 13, 1.f, 0.f, s);
   float* qn = dalloc<float>(D); launch_synth_fill(qn, D, 14, 0.1f, 1.f, s);
-  int* seq = dalloc<int>(1); int* pos = dalloc<int>(1); CK(hipMemset(seq, 0, 4));
-  const int nblk = KV * ATTN_SPLITS;
+  int* seq = dalloc<int>(M); int* pos = dalloc<int>(M);
+  std::vector<int> hseq(M);
+  for (int m = 0; m < M; ++m) hseq[m] = m;
+  CK(hipMemcpy(seq, hseq.data(), M * 4, hipMemcpyHostToDevice));
+  const int nblk = M * KV * ATTN_SPLITS;
+  if (nblk > 4096) { printf("M too large for the stamp buffer\n"); return 1; }
   std::vector<unsigned long long> st((size_t)nblk * 12);
-  for (int p0 : {40, 330, 700}) {
-    CK(hipMemcpy(pos, &p0, 4, hipMemcpyHostToDevice));
+  std::vector<int> cases = M == 1 ? std::vector<int>{40, 330, 700} : std::vector<int>{-1};
+  for (int p0 : cases) {
+    std::vector<int> hpos(M);
+    for (int m = 0; m < M; ++m) hpos[m] = p0 >= 0 ? p0 : 200 + (m * 97) % 261;
+    CK(hipMemcpy(pos, hpos.data(), M * 4, hipMemcpyHostToDevice));
     CK(hipStreamSynchronize(s));
     attn_stamps_clear();
     for (int rep = 0; rep < 30; ++rep) {
       const int l = rep % 28;  // rotate layers: cold K/V like in the engine
-      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, 1, H, KV, seq,
-                 pos, (int64_t)NCTX * KV * D, att, wk, s);
+      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, M, H, KV, seq, pos, seq_stride, att, wk, s);
     }
     CK(hipStreamSynchronize(s));
     attn_stamps_read(st.data(), nblk);
     unsigned long long t0 = ~0ull;
     for (int b = 0; b < nblk; ++b) if (st[b * 12]) t0 = std::min(t0, st[b * 12]);
-    printf("decode attention, n_past %d:\n", p0);
+    if (p0 >= 0) printf("decode attention, n_past %d:\n", p0);
+    else printf("decode attention, batch %d, n_past 200-460:\n", M);
     const int slot[] = {0, 1, 3, 7, 11, 9, 10};
     const char* nm[] = {"block start", "pos/splits known", "q normed/roped", "split merged", "partial stored",
                         "combine / direct start", "combined out"};
