@@ -136,6 +136,7 @@ struct Engine {
   std::vector<int> n_past, last_tok, logits_row;
   AttnWork attn_wk;
   AttnF32Work enc_attn_wk;
+  GemmF32Work enc_gemm_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
   int* gk_cnt = nullptr;
   int64_t gk_part_n = 0, gk_cnt_n = 0;
@@ -519,6 +520,11 @@ struct Engine {
     enc_attn_wk.cnt_n = ATTN_F32_COUNTERS;
     enc_attn_wk.cnt = alloc<int>(enc_attn_wk.cnt_n * CNT_LINE);
     FA_HIP(hipMemset(enc_attn_wk.cnt, 0, enc_attn_wk.cnt_n * CNT_LINE * sizeof(int)));
+    enc_gemm_wk.cnt_n = 512;
+    enc_gemm_wk.part_n = (int64_t)512 * 256 * 16;  // tiles x splits <= 512
+    enc_gemm_wk.part = alloc<float>(enc_gemm_wk.part_n);
+    enc_gemm_wk.cnt = alloc<int>(enc_gemm_wk.cnt_n * CNT_LINE);
+    FA_HIP(hipMemset(enc_gemm_wk.cnt, 0, enc_gemm_wk.cnt_n * CNT_LINE * sizeof(int)));
     mel = alloc<float>((size_t)max_batch * tm_max * ec.n_mels);
     const int wmax = std::max({ec.d_in, ec.d_llm, d});
     xa = alloc<float>((size_t)R * wmax);
@@ -628,7 +634,7 @@ struct Engine {
                int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0) {
     hipEvent_t ev;
     prof_begin(1, &ev);
-    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W));
+    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W), &enc_gemm_wk);
     prof_end(1, 0, 2.0 * M * N * K);
   }
 
@@ -953,6 +959,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();
     e->build_encoder();

@@ -18,16 +18,19 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ float r16v(float v, int r16) { return r16 ? __half2float(__float2half_rn(v)) : v; }
 
 constexpr int BK = 32;
+int g_gemm_f32_split = 1;  // 0: no K splits (A/B)
 
 // Block tile (64 WM) x (64 WN) x 32: 2x2 waves, each wave 32WM x 32WN = WM x WN accumulators of 32x32.
 // LDS is row-major [row][k] with row stride 34 floats: the MFMA operand read of lane (r, h) hits bank
 // (34 r + 2 kk + h) mod 64 = 2 (17 r mod 32) + h -> 64 distinct banks (17 is odd); each thread stores its
 // 16-B global chunk as two aligned 8-B writes. Global loads cover 8 rows x 128 B per wave instruction.
-constexpr int LDK = BK + 2;
-template <int WM, int WN>
+// KB (the k depth of a stage) is 32, 64 or 128: row stride KB + 2 keeps (KB + 2) / 2 odd, so the bank argument holds.
+template <int WM, int WN, int KB = BK>
 struct Tile {
   static constexpr int BM = 64 * WM, BN = 64 * WN;
-  static constexpr int NA = BM * BK / 4 / 256, NB = BN * BK / 4 / 256;  // float4 per thread
+  static constexpr int LDK = KB + 2;
+  static constexpr int R4 = KB / 4;                                     // float4 per tile row
+  static constexpr int NA = BM * KB / 4 / 256, NB = BN * KB / 4 / 256;  // float4 per thread
   static constexpr int STAGE = (BM + BN) * LDK;                         // floats per LDS stage
 };
 
@@ -72,39 +75,40 @@ __device__ __forceinline__ float4 load_w4(const float* __restrict__ W, int64_t l
   return r;
 }
 
-template <int WM, int WN, class AL>
+template <int WM, int WN, int KB, class AL>
 __device__ __forceinline__ void load_tiles(const AL& al, const float* __restrict__ W, int64_t ldw, int m0, int n0,
-                                           int k0, int M, int N, int K, float4 (&ra)[Tile<WM, WN>::NA],
-                                           float4 (&rb)[Tile<WM, WN>::NB]) {
+                                           int k0, int M, int N, int K, float4 (&ra)[Tile<WM, WN, KB>::NA],
+                                           float4 (&rb)[Tile<WM, WN, KB>::NB]) {
+  using T = Tile<WM, WN, KB>;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < Tile<WM, WN>::NA; ++i) {
-    const int idx = t + i * 256;  // (row idx >> 3, k4 idx & 7)
-    ra[i] = al.load4(m0 + (idx >> 3), k0 + 4 * (idx & 7), M, K);
+  for (int i = 0; i < T::NA; ++i) {
+    const int idx = t + i * 256;  // (row idx / R4, k4 idx % R4)
+    ra[i] = al.load4(m0 + idx / T::R4, k0 + 4 * (idx % T::R4), M, K);
   }
 #pragma unroll
-  for (int i = 0; i < Tile<WM, WN>::NB; ++i) {
+  for (int i = 0; i < T::NB; ++i) {
     const int idx = t + i * 256;
-    rb[i] = load_w4(W, ldw, n0 + (idx >> 3), k0 + 4 * (idx & 7), N, K);
+    rb[i] = load_w4(W, ldw, n0 + idx / T::R4, k0 + 4 * (idx % T::R4), N, K);
   }
 }
 
-template <int WM, int WN>
-__device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (&ra)[Tile<WM, WN>::NA],
-                                            const float4 (&rb)[Tile<WM, WN>::NB]) {
-  using T = Tile<WM, WN>;
+template <int WM, int WN, int KB>
+__device__ __forceinline__ void store_tiles(float* As, float* Bs, const float4 (&ra)[Tile<WM, WN, KB>::NA],
+                                            const float4 (&rb)[Tile<WM, WN, KB>::NB]) {
+  using T = Tile<WM, WN, KB>;
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
-    float* d = As + (idx >> 3) * LDK + 4 * (idx & 7);
+    float* d = As + (idx / T::R4) * T::LDK + 4 * (idx % T::R4);
     reinterpret_cast<float2*>(d)[0] = make_float2(ra[i].x, ra[i].y);
     reinterpret_cast<float2*>(d)[1] = make_float2(ra[i].z, ra[i].w);
   }
 #pragma unroll
   for (int i = 0; i < T::NB; ++i) {
     const int idx = t + i * 256;
-    float* d = Bs + (idx >> 3) * LDK + 4 * (idx & 7);
+    float* d = Bs + (idx / T::R4) * T::LDK + 4 * (idx % T::R4);
     reinterpret_cast<float2*>(d)[0] = make_float2(rb[i].x, rb[i].y);
     reinterpret_cast<float2*>(d)[1] = make_float2(rb[i].z, rb[i].w);
   }
@@ -225,12 +229,34 @@ struct EpiArgmax {
   }
 };
 
-template <class AL, class EPI, int WM, int WN>
+// XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one L2,
+// MI355X_MICROARCH.md "Workgroup dispatch"), so block b takes tile id (b % 8) * per + b / 8: each XCD owns one
+// contiguous run of tile ids, and ids run through bands of 4 M-tiles (all N-tiles of a band, M fastest), so an XCD's
+// blocks share a few A row bands and W column bands in its L2 instead of every XCD streaming all of A and W.
+// Placement only decides speed; every tile is computed exactly once either way. false: padding block (no tile).
+__device__ __forceinline__ bool xcd_tile(int nbx, int nby, int& tm, int& tn) {
+  const int T = nbx * nby, per = (T + 7) >> 3, b = blockIdx.x;
+  const int t = (b & 7) * per + (b >> 3);
+  if (t >= T) return false;
+  const int g = t / (4 * nbx), fm = 4 * g, gs = min(4, nby - fm), r = t - g * 4 * nbx;
+  tm = fm + r % gs;
+  tn = r / gs;
+  return true;
+}
+inline dim3 xcd_grid(int nbx, int nby, int ks = 1) { return dim3(((nbx * nby + 7) >> 3) << 3, 1, ks); }
+
+// gridDim.z = KS > 1 (64x64 tiles only): split z covers k in [z kper, (z + 1) kper); each split publishes its
+// accumulators (sc1), counts its arrival on the tile's counter, and the last one sums all KS partials in split order
+// (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1)
+template <class AL, class EPI, int WM, int WN, int KB, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
-                                                  EPI epi) {
-  using T = Tile<WM, WN>;
+                                                  EPI epi, float* __restrict__ part, int* __restrict__ cnt) {
+  using T = Tile<WM, WN, KB>;
+  constexpr int LDK = T::LDK;
   extern __shared__ float smem[];  // 2 stages x (A [BM][LDK], B [BN][LDK])
-  const int m0 = blockIdx.y * T::BM, n0 = blockIdx.x * T::BN;
+  int tm, tn;
+  if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
+  const int m0 = tm * T::BM, n0 = tn * T::BN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 31, h = lane >> 5;
@@ -240,17 +266,20 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
   float4 ra[T::NA], rb[T::NB];
-  load_tiles<WM, WN>(al, W, ldw, m0, n0, 0, M, N, K, ra, rb);
-  store_tiles<WM, WN>(smem, smem + T::BM * LDK, ra, rb);
+  const int KS = SPLIT ? gridDim.z : 1;
+  const int kper = (K + KB * KS - 1) / (KB * KS) * KB;
+  const int kb0 = blockIdx.z * kper, ke = min(K, kb0 + kper);  // this split's k range (zero-filled past ke)
+  load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0, M, N, ke, ra, rb);
+  store_tiles<WM, WN, KB>(smem, smem + T::BM * LDK, ra, rb);
   __syncthreads();
-  const int nk = (K + BK - 1) / BK;
+  const int nk = (ke - kb0 + KB - 1) / KB;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles<WM, WN>(al, W, ldw, m0, n0, (kt + 1) * BK, M, N, K, ra, rb);
+    if (kt + 1 < nk) load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rb);
     const float* a = smem + cur * T::STAGE + (wr * 32 * WM + r) * LDK + h;
     const float* b = smem + cur * T::STAGE + T::BM * LDK + (wc * 32 * WN + r) * LDK + h;
 #pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
+    for (int kk = 0; kk < KB / 2; ++kk) {
       float av[WM], bv[WN];
 #pragma unroll
       for (int i = 0; i < WM; ++i) av[i] = a[32 * i * LDK + 2 * kk];
@@ -261,8 +290,40 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
 #pragma unroll
         for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles<WM, WN>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
+    if (kt + 1 < nk) store_tiles<WM, WN, KB>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
     __syncthreads();
+  }
+  if constexpr (SPLIT && WM == 1 && WN == 1) {
+    {
+      __shared__ int s_last;
+      const int tile = tm * ((N + T::BN - 1) / T::BN) + tn;
+      float* base = part + (int64_t)tile * KS * 256 * 16;
+      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * 256 * 16 * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st_sc1_f4(f32x4_t{acc[0][0][4 * q], acc[0][0][4 * q + 1], acc[0][0][4 * q + 2], acc[0][0][4 * q + 3]}, rs,
+                  ((blockIdx.z * 256 + threadIdx.x) * 16 + 4 * q) * 4);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+      __syncthreads();
+      if (!s_last) return;
+      f32x4_t pv[GEMM_F32_KS_MAX][4];
+#pragma unroll
+      for (int z = 0; z < GEMM_F32_KS_MAX; ++z)  // all in flight; clamped duplicates past KS are not summed
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pv[z][q] = ld_sc1_f4(rs, ((min(z, KS - 1) * 256 + threadIdx.x) * 16 + 4 * q) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4_t t = pv[0][q];
+#pragma unroll
+        for (int z = 1; z < GEMM_F32_KS_MAX; ++z)
+          if (z < KS) t += pv[z][q];
+        acc[0][0][4 * q] = t.x; acc[0][0][4 * q + 1] = t.y; acc[0][0][4 * q + 2] = t.z; acc[0][0][4 * q + 3] = t.w;
+      }
+      if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -270,17 +331,32 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
 }
 
-template <class AL, class EPI, int WM, int WN>
-static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
-  using T = Tile<WM, WN>;
-  dim3 grid(cdiv(N, T::BN), cdiv(M, T::BM));
+template <class AL, class EPI, int WM, int WN, int KB = BK>
+static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
+                        const GemmF32Work* wk = nullptr) {
+  using T = Tile<WM, WN, KB>;
+  // K splits (64x64 tiles, workspace given) while the tiles leave most CUs idle: up to 4, >= 512 of k per split
+  // (measured: ffn2 of one clip, N 512 K 2048, 60.7 -> 55.8 us; the K = 512 projections lose with 2 splits)
+  int ks = 1;
+  const int64_t tiles = (int64_t)cdiv(N, T::BN) * cdiv(M, T::BM);
+  if (WM == 1 && WN == 1 && wk && wk->part && g_gemm_f32_split)
+    while (ks < GEMM_F32_KS_MAX && tiles * ks * 2 <= 512 && K / (2 * ks) >= 512 && tiles <= wk->cnt_n &&
+           tiles * ks * 2 * 256 * 16 <= wk->part_n)
+      ks *= 2;
+  const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM), ks);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   static bool attr = false;
   if (!attr && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi);
+  if (ks > 1)
+    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB, true>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi,
+                       wk->part, wk->cnt);
+  else
+    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi, nullptr,
+                       nullptr);
 }
 
 // 128x128 blocks (4 MFMA accumulators per wave: half the LDS reads per MFMA) when they still give every CU
@@ -289,12 +365,16 @@ int g_gemm_f32_force = 0;  // microbenchmark hook: 1 = 64x64 blocks, 2 = 128x128
 
 template <class AL, class EPI>
 static void run_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
-                     bool allow_big = true) {
+                     bool allow_big = true, const GemmF32Work* wk = nullptr) {
   const bool big = g_gemm_f32_force ? g_gemm_f32_force == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
   if (allow_big && big)
     launch_gemm<AL, EPI, 2, 2>(al, W, ldw, M, N, K, epi, s);
+  else if (g_gemm_f32_force == 3)
+    launch_gemm<AL, EPI, 1, 1, 64>(al, W, ldw, M, N, K, epi, s);
+  else if (g_gemm_f32_force == 4)
+    launch_gemm<AL, EPI, 1, 1, 128>(al, W, ldw, M, N, K, epi, s);
   else
-    launch_gemm<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);
+    launch_gemm<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s, wk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -355,7 +435,9 @@ __global__ __launch_bounds__(256) void k_gemm_f16(AL al, const __half* __restric
   using T = Tile16<WM, WN>;
   extern __shared__ float smem[];  // 2 stages x (A [BM][LDKH], W [BN][LDKH]) halves; the epilogue reuses it
   _Float16* sh = reinterpret_cast<_Float16*>(smem);
-  const int m0 = blockIdx.y * T::BM, n0 = blockIdx.x * T::BN;
+  int tm, tn;
+  if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
+  const int m0 = tm * T::BM, n0 = tn * T::BN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 31, h = lane >> 5;
@@ -401,7 +483,7 @@ static void launch_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int
                           hipStream_t s) {
   using T = Tile16<WM, WN>;
   FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_f16: K and ldw must be multiples of 8");
-  dim3 grid(cdiv(N, T::BN), cdiv(M, T::BM));
+  const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM));
   const size_t lds = std::max<size_t>(2 * T::STAGE * sizeof(_Float16), 1024);  // >= EpiArgmax scratch
   hipLaunchKernelGGL((k_gemm_f16<AL, EPI, WM, WN>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi);
 }
@@ -415,11 +497,11 @@ static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N,
 
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16) {
+                 hipStream_t s, const __half* W16, const GemmF32Work* wk) {
   ALoadPlain al{A, lda};
   EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
   if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
-  else run_gemm(al, W, ldw, M, N, K, epi, s);
+  else run_gemm(al, W, ldw, M, N, K, epi, s, true, wk);
 }
 
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,

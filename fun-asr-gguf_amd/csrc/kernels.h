@@ -21,10 +21,21 @@ void launch_h2f(const __half* a, float* b, int64_t n, hipStream_t s);
 void launch_f2h_initializer(const float* a, __half* b, float* b32, int64_t n, hipStream_t s);
 
 // gemm_f32.hip
+// K-split workspace of the f32 GEMM (few-tile shapes, e.g. a single clip's N = 512 projections): partial
+// accumulators of up to cnt_n tiles x GEMM_F32_KS_MAX splits x 256 threads x 16 floats, one arrival counter per
+// tile (zeroed once; re-armed by the summing block)
+#define GEMM_F32_KS_MAX 4
+struct GemmF32Work {
+  float* part = nullptr;
+  int64_t part_n = 0;
+  int* cnt = nullptr;  // [cnt_n][CNT_LINE]
+  int64_t cnt_n = 0;
+};
+extern int g_gemm_f32_split;  // 1 (default): K splits where the tiles leave the chip idle; 0: none
 // W16 != nullptr: fp16 mode (C5) on the f16 MFMA kernel with the fp16 weight copy W16, every op output rounded to fp16
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16 = nullptr);
+                 hipStream_t s, const __half* W16 = nullptr, const GemmF32Work* wk = nullptr);
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
                      int64_t ldp, hipStream_t s, int r16 = 0);
 void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,

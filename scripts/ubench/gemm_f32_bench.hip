@@ -35,9 +35,12 @@ int main() {
   launch_synth_fill(A, (int64_t)Mmax * Kmax, 1, 1.f, 0.f, s); launch_synth_fill(W, (int64_t)Nmax * Kmax, 2, 0.05f, 0.f, s);
   launch_synth_fill(bias, Nmax, 3, 0.1f, 0.f, s);
   CK(hipStreamSynchronize(s));
+  GemmF32Work wk; wk.cnt_n = 512; wk.part_n = (int64_t)512 * 256 * 16;
+  CK(hipMalloc(&wk.part, wk.part_n * 4)); CK(hipMalloc(&wk.cnt, wk.cnt_n * CNT_LINE * 4));
+  CK(hipMemset(wk.cnt, 0, wk.cnt_n * CNT_LINE * 4));
   {  // spot check: M=100 N=96 K=72 (partial tiles) against the CPU
     const int M = 100, N = 96, K = 72;
-    for (int v : {1, 2}) {
+    for (int v : {1, 2, 3, 4}) {
       g_gemm_f32_force = v;
       gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s);
       CK(hipStreamSynchronize(s));
@@ -52,16 +55,33 @@ int main() {
       printf("check variant %d: max|err| %.3g %s\n", v, err, err < 1e-4 ? "ok" : "FAIL");
     }
   }
+  {  // split-K spot check: M=70 N=64 K=2048 (4 splits) against the CPU
+    const int M = 70, N = 64, K = 2048;
+    g_gemm_f32_force = 1;
+    gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s, nullptr, &wk);
+    CK(hipStreamSynchronize(s));
+    std::vector<float> a((size_t)M * K), w((size_t)N * K), b(N), c((size_t)M * N);
+    CK(hipMemcpy(a.data(), A, a.size() * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(w.data(), W, w.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), bias, N * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(c.data(), C, c.size() * 4, hipMemcpyDeviceToHost));
+    double err = 0;
+    for (int i = 0; i < M; ++i) for (int j = 0; j < N; ++j) {
+      double r = b[j]; for (int k = 0; k < K; ++k) r += (double)a[i * K + k] * w[j * K + k];
+      err = std::max(err, std::fabs(r - c[i * N + j]));
+    }
+    printf("check split-K: max|err| %.3g %s\n", err, err < 1e-3 ? "ok" : "FAIL");
+  }
   struct Sh { const char* name; int N, K; };
   const Sh shapes[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
   for (int M : {1001, 32032}) {
     for (const Sh& sh : shapes) {
       printf("M=%5d %-9s N=%4d K=%4d:", M, sh.name, sh.N, sh.K);
-      for (int v : {1, 2}) {
-        g_gemm_f32_force = v;
-        const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s); },
+      for (int v : {1, 5, 3, 2}) {
+        g_gemm_f32_force = v == 5 ? 1 : v;
+        const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
+                                                       nullptr, v == 5 ? &wk : nullptr); },
                                      M > 2000 ? 10 : 50);
-        printf("  %s %8.1f us %6.1f TF/s", v == 1 ? "64x64" : "128x128", us, 2.0 * M * sh.N * sh.K / us / 1e6);
+        const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K"};
+        printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
       printf("\n");
     }
