@@ -256,6 +256,10 @@ __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int 
   }
 }
 
+// the first row group's residual values are loaded with the activations (1; 0: at the epilogue, A/B builds)
+#ifndef FA_RES0_PRELOAD
+#define FA_RES0_PRELOAD 1
+#endif
 template <int NCH, int MT, int EPI>
 __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, int r0, int lane, int m0, int mt,
                                               const int8_t* s_q, const float* s_d, const RowGroup<NCH, EPI>& G,
@@ -289,7 +293,7 @@ __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, i
       if (lane == 0 && (r0 + rr < a.rpw) && row < a.O) {
         float* op = a.out + (int64_t)(m0 + m) * a.ldo + row;
         if (EPI == 0 || EPI == 3) *op = y;
-        else if (EPI == 1) *op = (MT == 1 && r0 == 0 ? res0[rr] : a.res[(int64_t)(m0 + m) * a.ldr + row]) + y;
+        else if (EPI == 1) *op = (MT == 1 && r0 == 0 && FA_RES0_PRELOAD ? res0[rr] : a.res[(int64_t)(m0 + m) * a.ldr + row]) + y;
         else *op = (y / (1.0f + expf(-y))) * y2;
         if (EPI == 3) argmax_combine(best_v[m], best_i[m], y, row);
       }
@@ -356,7 +360,7 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   // residual epilogue: the first row group's residual values ride with the activation loads (a load after the
   // dot products would be one more serial memory latency at the tail)
   float res0[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == 1 && MT == 1) {
+  if constexpr (EPI == 1 && MT == 1 && FA_RES0_PRELOAD) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) res0[rr] = a.res[(int64_t)m0 * a.ldr + min(row_base + rr, a.O - 1)];
   }
