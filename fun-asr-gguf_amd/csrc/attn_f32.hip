@@ -230,34 +230,40 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
     *s_flag = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
   __syncthreads();
   if (!*s_flag) return;
-  // merged max / sum per query, then the weighted sum of the splits' O
+  // merged max / sum per query and each split's weight exp(m_k - m) -> LDS (the O staging area is free now), with
+  // every split's (m, l) load in flight at once; then the weighted sum of the splits' O, KSM loads per output in
+  // flight (clamped duplicates past KS carry weight 0)
+  constexpr int KSM = 8;
+  float* s_w = lds;  // [KSM][AQ]
   if (threadIdx.x < AQ) {
     const int q = threadIdx.x;
+    f4v ml[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) ml[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + AQ * D + 2 * (q & ~1)) * 4);
     float mm = -INFINITY;
-    for (int k2 = 0; k2 < KS; ++k2) {
-      const f4v v = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
-      mm = fmaxf(mm, (q & 1) ? v.z : v.x);
-    }
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2)
+      if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
     float ll = 0.f;
-    for (int k2 = 0; k2 < KS; ++k2) {
-      const f4v v = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
-      const float mk = (q & 1) ? v.z : v.x, lk = (q & 1) ? v.w : v.y;
-      ll += mk == -INFINITY ? 0.f : __expf(mk - mm) * lk;
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) {
+      const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
+      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
+      ll += w * lk;
+      s_w[k2 * AQ + q] = w;
     }
-    s_m[q] = mm;
     s_l[q] = ll;
   }
   __syncthreads();
   for (int f = threadIdx.x; f < AQ * D4; f += 256) {
     const int q = f / D4, d4 = f % D4;
     if (q0 + q >= t_stride) continue;
-    f4v acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k2 = 0; k2 < KS; ++k2) {
-      const f4v ml = ld_sc1_f4(rs, (k2 * PSZ + AQ * D + 2 * (q & ~1)) * 4);
-      const float mk = (q & 1) ? ml.z : ml.x;
-      const float w = mk == -INFINITY ? 0.f : __expf(mk - s_m[q]);
-      acc += w * ld_sc1_f4(rs, (k2 * PSZ + q * D + 4 * d4) * 4);
-    }
+    f4v pv[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
+    f4v acc = s_w[q] * pv[0];
+#pragma unroll
+    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
     const float inv = 1.0f / s_l[q];
     float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
     if (r16) v = round_f16x4(v);
@@ -281,6 +287,7 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
               const AttnF32Work& wk, hipStream_t s, int r16) {
   const int KS = attn_f32_splits(batch, t_stride, n_heads);
+  FA_REQUIRE(KS >= 1 && KS <= 8, "attn_f32: 1-8 key splits (16 measured slower: 60 vs 39 us at T = 1001)");
   const int n_tiles = cdiv(t_stride, AQ) * n_heads * batch;
   if (KS > 1)
     FA_REQUIRE(wk.part && wk.cnt && n_tiles <= wk.cnt_n &&
