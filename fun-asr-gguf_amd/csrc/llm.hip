@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // the kernel fits 128 VGPRs and 4 blocks share a CU (every block of a batch-32 launch resident at once)
 template <int DM, int LEAN>
 __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
-                                                         int lg_nsplit, int decode_mode, int H, int KV,
+                                                         int nsplit, int decode_mode, int H, int KV,
                                                          int64_t seq_stride, int64_t head_stride,
                                                          __half* __restrict__ kc,
                                                          __half* __restrict__ vc, const float* __restrict__ qsrc,
@@ -1155,7 +1155,8 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   STAMP(0);
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
-  const int gps = max(AMIN_G, (n_groups + (1 << lg_nsplit) - 1) >> lg_nsplit);  // groups per split
+  // groups per split = ceil(n_groups / nsplit) without an integer-division sequence (exact below 2^24)
+  const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)nsplit));
   // n_active = ceil(n_groups / gps) without an integer-division sequence (gps <= n_groups < 2^24: exact)
   int n_active = (int)ceilf((float)n_groups / (float)gps);
   if (sp >= n_active) return;                                      // uniform over the block
@@ -1345,14 +1346,15 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
-  // key splits (a power of two) only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1,
-  // 4 at batch 32, 1 for prefill
-  int lg = 0;
-  while ((2 << lg) <= ASPLIT && (2 << lg) * M * KV <= g_attn_blocks) ++lg;
-  const bool lean = g_attn_lean >= 0 ? g_attn_lean != 0 : (M * KV << lg) > 3 * 256;
+  // key splits only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1-4, 4 at batch 32, 1 for
+  // prefill. Batch 32 measured 14.7-17.0 us for every target of 256-1024 blocks, lean or not (attn_batch.hip): the
+  // K/V stream of 512 (sequence, kv head) pairs comes in at ~2.8 TB/s whatever the block shape.
+  int ns = 1;
+  while (ns < ASPLIT && (ns + 1) * M * KV <= g_attn_blocks) ++ns;
+  const bool lean = g_attn_lean >= 0 ? g_attn_lean != 0 : M * KV * ns > 3 * 256;
   auto kern = lean ? (decode_mode ? k_attn_block<1, 1> : k_attn_block<0, 1>)
                    : (decode_mode ? k_attn_block<1, 0> : k_attn_block<0, 0>);
-  hipLaunchKernelGGL(kern, dim3(KV, 1 << lg, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, lg, decode_mode,
+  hipLaunchKernelGGL(kern, dim3(KV, ns, M), dim3(AWV * 64), 0, s, tok_seq, tok_pos, ns, decode_mode,
                      H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters, wk.partials,
                      qout, dout);
 }
@@ -1401,7 +1403,19 @@ __global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logit
   if (temperature <= 0.f || top_k == 1) {
     float v = -INFINITY;
     int i = 0x7fffffff;
-    for (int t = threadIdx.x; t < n_part; t += 1024) argmax_combine(v, i, pval[(int64_t)m * n_part + t], pidx[(int64_t)m * n_part + t]);
+    // partials 4 per thread in flight at once (a plain strided loop waits on each load before the next)
+    for (int t0 = 0; t0 < n_part; t0 += 4096) {
+      float pv[4];
+      int pi[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = min(t0 + u * 1024 + (int)threadIdx.x, n_part - 1);  // clamped duplicates: argmax unchanged
+        pv[u] = pval[(int64_t)m * n_part + t];
+        pi[u] = pidx[(int64_t)m * n_part + t];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) argmax_combine(v, i, pv[u], pi[u]);
+    }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       float v2 = __shfl_xor(v, o, 64);

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
   const double bytes = keys * KV * D * 2 * 2;  // K and V rows read per layer
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   printf("n_ctx per sequence slot %d\n", NCTX);
-  for (int target : {256, 1024}) {
+  for (int target : {256, 512, 768, 1024}) {
     for (int lean : {0, 1}) {
       g_attn_blocks = target; g_attn_lean = lean;
       hipGraph_t g; hipGraphExec_t ex;
