@@ -75,12 +75,12 @@ int main() {
   for (int M : {1001, 32032}) {
     for (const Sh& sh : shapes) {
       printf("M=%5d %-9s N=%4d K=%4d:", M, sh.name, sh.N, sh.K);
-      for (int v : {1, 5, 3, 2}) {
-        g_gemm_f32_force = v == 5 ? 1 : v;
+      for (int v : {1, 5, 3, 2, 6}) {
+        g_gemm_f32_force = v == 5 ? 1 : v == 6 ? 0 : v;
         const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
-                                                       nullptr, v == 5 ? &wk : nullptr); },
+                                                       nullptr, v >= 5 ? &wk : nullptr); },
                                      M > 2000 ? 10 : 50);
-        const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K"};
+        const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K", "engine default"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
       printf("\n");
