@@ -5,6 +5,7 @@ set -e
 B=fun-asr-gguf_amd/build; U=scripts/ubench; F="-O3 -std=c++17 --offload-arch=gfx950 -Iinclude"
 hipcc $F -c $U/decode_step.hip -o /tmp/ds.o && hipcc --offload-arch=gfx950 /tmp/ds.o $B/llm.hip.o $B/synth.hip.o -o $U/decode_step
 hipcc $F $U/edge_chain.hip -o $U/edge_chain
+hipcc $F $U/kv_stream.hip -o $U/kv_stream
 hipcc $F -c $U/attn_f32_check.hip -o /tmp/afc.o && hipcc --offload-arch=gfx950 /tmp/afc.o $B/attn_f32.hip.o $B/synth.hip.o -o $U/attn_f32_check
 hipcc $F -c $U/attn_f32_bench.hip -o /tmp/af.o && hipcc --offload-arch=gfx950 /tmp/af.o $B/attn_f32.hip.o $B/synth.hip.o -o $U/attn_f32_bench
 hipcc $F -c $U/gemm_f32_bench.hip -o /tmp/gf.o && hipcc --offload-arch=gfx950 /tmp/gf.o $B/gemm_f32.hip.o $B/synth.hip.o -o $U/gemm_f32_bench
