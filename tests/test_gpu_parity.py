@@ -254,6 +254,33 @@ def test_llm_batched_decode_mfma_teacher_forced(tiny_engine, llm_tiny_oracle):
             fed[s_].append(int(nxt[s_]))
 
 
+def test_llm_batch20_lean_attention_chunked_combine(llm_tiny_oracle):
+    """20 sequences decode as one M=20 batch: 6 key splits x 20 x 8 blocks > 3 per CU, so the lean (128-VGPR)
+    attention variant runs, and contexts past 160 keys give 5-6 active splits, merged in two chunks of 4; the
+    split-K GEMMs and the batched LM head at M=20. Rows checked against the oracle run of that sequence alone."""
+    from fun_asr_gguf import _native
+    eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=320, max_seqs=20), max_batch=1, max_samples=16000)
+    eng.synthetic_weights(0)
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(8)
+    lens = [int(n) for n in rng.integers(3, 280, 20)]
+    lens[0], lens[1] = 250, 200  # at least two contexts with 6 and 5 active splits
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in lens]
+    toks = []
+    for s_, p in enumerate(prompts):
+        eng.llm_reset(s_)
+        toks.append(eng.llm_prefill(s_, p))
+    nxt = eng.llm_generate(list(range(20)), 1)[:, 0]
+    for s_ in (0, 1, 5, 9, 14, 19):
+        lg = eng.llm_logits(s_)
+        m.reset()
+        m.forward(prompts[s_], 0)
+        ref = m.forward(m.embed_tokens([toks[s_]]), prompts[s_].shape[0])
+        _check_step(lg, ref)
+        assert int(nxt[s_]) == int(np.argmax(lg))
+    eng.close()
+
+
 def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
     rng = np.random.default_rng(4)
     prompts = [llm_tiny_oracle.embed_prompt(rng.integers(0, 4096, n)) for n in (9, 17, 5)]
