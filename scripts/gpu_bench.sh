@@ -12,4 +12,5 @@ print("C2 value", d["value"], "ms/step", d["ms_per_step"], d["stage_ms"])
 print("roofline", {k: d["roofline"][k] for k in ("kernel", "achieved", "frac", "avg_launch_us")}, d["kernel_class_avg_us"])
 print("C3", d["c3"].get("value"), d["c3"].get("ms_per_step"), d["c3"].get("stage_ms"))
 print("C5", d["c5"].get("value"), d["c5"].get("ms_per_step"), d["c5"].get("stage_ms"))
+print("C4", d.get("c4"))
 PY
