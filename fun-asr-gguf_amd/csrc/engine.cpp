@@ -761,7 +761,7 @@ struct Engine {
     // prefill: rows are consecutive positions of one sequence, logits for the last row only.
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
-    const bool small = M <= 4;
+    const bool small = gemv_small(M);
     (void)max_pos;
     for (int l = 0; l < lc.n_layer; ++l) {
       const LlmLayerW& w = layers[l];
@@ -824,7 +824,7 @@ struct Engine {
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
     h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows);
-    if (n_rows <= 4) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
+    if (gemv_small(n_rows)) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
     gemv(h, E, 3);
   }
@@ -959,6 +959,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_GEMV_SMALL")) fa::g_gemv_small_max = atoi(g);
+    if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g);
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();

@@ -89,11 +89,14 @@ struct GemvArgs {
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
 int gemv_rows_per_wave(int O);
-// argmax partials per token written by the lm_head launch for M tokens (GEMV for M <= 4, MFMA GEMM above)
+// argmax partials per token written by the lm_head launch for M tokens (GEMV for gemv_small(M), MFMA GEMM above)
 int lm_head_parts(int O, int M);
 int gemm_k_splits(int O, int M, int K, int epi);  // K splits of the split-K GEMM form for this shape
 extern int g_attn_lean;    // -1 auto, 0/1 force the 128-VGPR attention variant (A/B)
 extern int g_attn_blocks;  // attention key-split target (blocks per launch), 1024 by default
+extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 7); MFMA GEMM above
+extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)
+bool gemv_small(int M);
 extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,

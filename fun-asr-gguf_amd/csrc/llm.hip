@@ -335,26 +335,38 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   // behind the weight stream they would arrive only with it), then the first weight row group, then the
   // prologue math: the weights stream in while the activations are normalised and quantised
   // (branch-free: a branch here makes the wait-count pass drain the loads at the join, before the weight stream)
+  // MT > 1 (small decode batches: every weight row streamed once for all the block's tokens): the same
+  // block-cooperative / per-chunk prologue once per token row, so a token's q8_0 input rows are bit-identical to
+  // the MT == 1 launch's (continuous batch == single sequence). Rows past mt load a clamped valid row, unused.
   constexpr int PERB = NCH * 4;  // block-cooperative prologue: values per thread
-  const bool pro_blk = FUSED && mt == 1 && NCH < 3;
-  const bool pro_chunk = FUSED && mt == 1 && NCH == 3 && !a.norm_w;  // K = 3072, no norm (down projection)
-  float xv[NCH < 3 ? PERB : 16], xw[PERB];
+  const bool pro_blk = FUSED && NCH < 3;
+  const bool pro_chunk = FUSED && NCH == 3 && !a.norm_w;  // K = 3072, no norm (down projection)
+  float xv[MT][NCH < 3 ? PERB : 16], xw[PERB];
   if constexpr (FUSED && NCH < 3) {
-    const float* xr = a.x + (int64_t)m0 * a.ldx + threadIdx.x * PERB;
     const float* wr = (a.norm_w ? a.norm_w : a.x) + threadIdx.x * PERB;  // no norm: a valid dummy row, unused
 #pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float* xr = a.x + (int64_t)(m0 + min(m, mt - 1)) * a.ldx + threadIdx.x * PERB;
+#pragma unroll
+      for (int j = 0; j < PERB; j += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(xr + j);
+        xv[m][j] = f.x; xv[m][j + 1] = f.y; xv[m][j + 2] = f.z; xv[m][j + 3] = f.w;
+      }
+    }
+#pragma unroll
     for (int j = 0; j < PERB; j += 4) {
-      const float4 f = *reinterpret_cast<const float4*>(xr + j);
-      xv[j] = f.x; xv[j + 1] = f.y; xv[j + 2] = f.z; xv[j + 3] = f.w;
       const float4 g = *reinterpret_cast<const float4*>(wr + j);
       xw[j] = g.x; xw[j + 1] = g.y; xw[j + 2] = g.z; xw[j + 3] = g.w;
     }
   } else if constexpr (FUSED && NCH == 3) {
-    const float* xr = a.x + (int64_t)m0 * a.ldx + min(wave, 2) * 1024 + lane * 16;  // wave 3: a duplicate, unused
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) {
-      const float4 f = *reinterpret_cast<const float4*>(xr + j);
-      xv[j] = f.x; xv[j + 1] = f.y; xv[j + 2] = f.z; xv[j + 3] = f.w;
+    for (int m = 0; m < MT; ++m) {
+      const float* xr = a.x + (int64_t)(m0 + min(m, mt - 1)) * a.ldx + min(wave, 2) * 1024 + lane * 16;  // wave 3: unused
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(xr + j);
+        xv[m][j] = f.x; xv[m][j + 1] = f.y; xv[m][j + 2] = f.z; xv[m][j + 3] = f.w;
+      }
     }
   }
   // residual epilogue: the first row group's residual values ride with the activation loads (a load after the
@@ -372,17 +384,27 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   // ---- prologue: activation tile -> LDS (int8 q + f32 d)
   if (pro_blk) {
-    __shared__ float s_red[4];
-    float v[PERB];
+    __shared__ float s_red[MT][4];
 #pragma unroll
-    for (int j = 0; j < PERB; ++j) v[j] = xv[j];
-    norm_quant_block_regs<PERB>(v, xw, a.norm_w != nullptr, a.eps, NCH * 1024, s_q, s_d, s_red);
+    for (int m = 0; m < MT; ++m) {
+      if (m < mt) {  // block-uniform
+        float v[PERB];
+#pragma unroll
+        for (int j = 0; j < PERB; ++j) v[j] = xv[m][j];
+        norm_quant_block_regs<PERB>(v, xw, a.norm_w != nullptr, a.eps, NCH * 1024, s_q + m * K, s_d + m * NB, s_red[m]);
+      }
+    }
   } else if (pro_chunk) {
     if (wave < NCH) {
-      float v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = xv[j];
-      quant_chunk_regs(v, lane, s_q + wave * 1024, s_d + wave * 32);
+      for (int m = 0; m < MT; ++m) {
+        if (m < mt) {
+          float v[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) v[j] = xv[m][j];
+          quant_chunk_regs(v, lane, s_q + m * K + wave * 1024, s_d + m * NB + wave * 32);
+        }
+      }
     }
   } else if (FUSED) {
     for (int m = wave; m < mt; m += 4)
@@ -820,17 +842,37 @@ int gemv_rows_per_wave(int O) {
   return rpw < 1 ? 1 : rpw;
 }
 
+// decode batches up to g_gemv_small_max tokens take the fused GEMV (above: prep + MFMA GEMM); from 3 tokens on,
+// g_gemv_mt tokens share a block (weights streamed once per block for its tokens). Measured decode step (full
+// model, graph-replayed, scripts/prof_batch_decode.py): batch 3 / 4 / 5 / 6 / 7 = 0.82 / 0.94 / 1.03 / 1.15 /
+// 1.21 ms with 2 tokens per block, vs 0.86 / 0.97 / 1.11 / 1.21 / 1.35 with one token per block and 0.86 / 0.97 /
+// 1.25 / 1.26 / 1.29 on the MFMA GEMM; batch 8 and up: the MFMA GEMM (1.30 vs 1.35). More tokens per block
+// serialise more prologue / dot work per block than the saved weight re-reads (MT 4 / 8: slower).
+int g_gemv_small_max = 7;
+int g_gemv_mt = 2;
+
+bool gemv_small(int M) { return M <= g_gemv_small_max; }
+
+template <int MT>
+static void launch_gemv_fused(int K, int epi, const GemvArgs& a, hipStream_t s) {
+  switch (epi) {
+    case 0: launch_gemv_k<MT, true, 0>(K, a, s); break;
+    case 1: launch_gemv_k<MT, true, 1>(K, a, s); break;
+    case 2: launch_gemv_k<MT, true, 2>(K, a, s); break;
+    case 3: launch_gemv_k<MT, true, 3>(K, a, s); break;
+  }
+}
+
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   const bool fused = a.x != nullptr;
-  if (a.M <= 4 && fused) {
+  if (gemv_small(a.M) && fused) {
     FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemv_q8: n_part");
-    // decode path: tokens handled one per block row
-    switch (epi) {
-      case 0: launch_gemv_k<1, true, 0>(K, a, s); break;
-      case 1: launch_gemv_k<1, true, 1>(K, a, s); break;
-      case 2: launch_gemv_k<1, true, 2>(K, a, s); break;
-      case 3: launch_gemv_k<1, true, 3>(K, a, s); break;
-    }
+    // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens)
+    const int mt = a.M <= 2 ? 1 : std::min(g_gemv_mt, a.M);
+    if (mt <= 1) launch_gemv_fused<1>(K, epi, a, s);
+    else if (mt <= 2) launch_gemv_fused<2>(K, epi, a, s);
+    else if (mt <= 4) launch_gemv_fused<4>(K, epi, a, s);
+    else launch_gemv_fused<8>(K, epi, a, s);
     return;
   }
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
@@ -857,7 +899,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
 }
 
-int lm_head_parts(int O, int M) { return M <= 4 ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
+int lm_head_parts(int O, int M) { return gemv_small(M) ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
 
 // ------------------------------------------------------------------------------------------------
 // q/k RMSNorm per head (attn_q_norm/attn_k_norm) + NEOX RoPE + KV-cache store (fp16).

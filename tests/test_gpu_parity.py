@@ -228,12 +228,14 @@ def test_llm_long_context_split_attention(tiny_engine, llm_tiny_oracle):
         tok, pos = int(nxt), pos + 1
 
 
-def test_llm_batched_decode_mfma_teacher_forced(tiny_engine, llm_tiny_oracle):
-    """6 sequences decode as one M=6 batch: every GEMM (and the lm_head + argmax partials) runs on the int8
-    MFMA path; each row's logits are checked against the oracle run of that sequence alone."""
+@pytest.mark.parametrize("n_seq", [6, 8])
+def test_llm_batched_decode_teacher_forced(tiny_engine, llm_tiny_oracle, n_seq):
+    """n_seq sequences decode as one batch: M=6 on the fused GEMV with 2 tokens per block (3 blocks rows), M=8
+    with every GEMM (and the lm_head + argmax partials) on the int8 MFMA path; each row's logits are checked
+    against the oracle run of that sequence alone."""
     m = llm_tiny_oracle
     rng = np.random.default_rng(6)
-    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (7, 19, 33, 12, 70, 45)]
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (7, 19, 33, 12, 70, 45, 26, 9)[:n_seq]]
     toks = []
     for s_, p in enumerate(prompts):
         tiny_engine.llm_reset(s_)
