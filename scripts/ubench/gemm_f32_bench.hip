@@ -26,9 +26,10 @@ static double time_graph(std::function<void()> f, int reps) {
   CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
   return ms * 1e3 / (3.0 * reps);
 }
-int main() {
+int main(int argc, char** argv) {
+  const int pad = argc > 1 ? atoi(argv[1]) : 0;  // extra floats per A / W row (stride study)
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  const int Mmax = 32032, Kmax = 2048, Nmax = 2048;
+  const int Mmax = 32032, Kmax = 2048 + 128, Nmax = 2048;
   float *A, *W, *bias, *C;
   CK(hipMalloc(&A, (size_t)Mmax * Kmax * 4)); CK(hipMalloc(&W, (size_t)Nmax * Kmax * 4));
   CK(hipMalloc(&bias, Nmax * 4)); CK(hipMalloc(&C, (size_t)Mmax * Nmax * 4));
@@ -72,12 +73,14 @@ int main() {
   }
   struct Sh { const char* name; int N, K; };
   const Sh shapes[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
+  printf("row stride pad %d floats\n", pad);
   for (int M : {1001, 32032}) {
+    if (pad && M > 2000) break;
     for (const Sh& sh : shapes) {
       printf("M=%5d %-9s N=%4d K=%4d:", M, sh.name, sh.N, sh.K);
       for (int v : {1, 5, 3, 2, 6}) {
         g_gemm_f32_force = v == 5 ? 1 : v == 6 ? 0 : v;
-        const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
+        const double us = time_graph([&] { gemm_linear(A, sh.K + pad, W, sh.K + pad, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
                                                        nullptr, v >= 5 ? &wk : nullptr); },
                                      M > 2000 ? 10 : 50);
         const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K", "engine default"};
