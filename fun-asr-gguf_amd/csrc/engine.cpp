@@ -133,7 +133,10 @@ struct Engine {
   int *d_tok_seq = nullptr, *d_tok_pos = nullptr, *d_step = nullptr, *d_tok_cur = nullptr, *d_tok_hist = nullptr,
       *d_ids = nullptr;
   int hist_max = 0;
-  std::vector<int> n_past, last_tok, logits_row;
+  SampleParams* d_samp = nullptr;  // sampler chain parameters of the current call (read by the sampler launch)
+  SampleParams h_samp{};
+  std::vector<int> n_past, last_tok;
+  std::vector<int> logits_row;  // per sequence: its row of `logits` in the most recent forward (-1: none)
   AttnWork attn_wk;
   AttnF32Work enc_attn_wk;
   GemmF32Work enc_gemm_wk;
@@ -147,7 +150,7 @@ struct Engine {
     double ms = 0, bytes = 0, flops = 0;
     int64_t launches = 0;
   } pcls[5];
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool, graph_events;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   struct Pending {
     int cls;
     hipEvent_t a, b;
@@ -155,11 +158,7 @@ struct Engine {
   };
   std::vector<Pending> pending;
   size_t ev_next = 0;
-  struct StepGraph {
-    hipGraphExec_t exec = nullptr;
-    std::vector<Pending> events;  // profiled variant: (class, start, end) event pairs inside the graph
-  };
-  std::unordered_map<int, StepGraph> step_graphs, prof_graphs;
+  std::unordered_map<int, hipGraphExec_t> step_graphs;
   bool use_graphs = true;
 
   template <class T>
@@ -171,13 +170,11 @@ struct Engine {
   }
   ~Engine() {
     if (stream) hipStreamSynchronize(stream);
-    for (auto& g : step_graphs) hipGraphExecDestroy(g.second.exec);
-    for (auto& g : prof_graphs) hipGraphExecDestroy(g.second.exec);
-    for (auto* pool : {&ev_pool, &graph_events})
-      for (auto& e : *pool) {
-        hipEventDestroy(e.first);
-        hipEventDestroy(e.second);
-      }
+    for (auto& g : step_graphs) hipGraphExecDestroy(g.second);
+    for (auto& e : ev_pool) {
+      hipEventDestroy(e.first);
+      hipEventDestroy(e.second);
+    }
     for (void* p : allocs) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -577,6 +574,7 @@ struct Engine {
     hist_max = 4096;
     d_tok_hist = alloc<int>((size_t)lc.max_seqs * hist_max);
     d_ids = alloc<int>(m_max);
+    d_samp = alloc<SampleParams>(1);
     attn_wk.max_tokens = m_max;
     attn_wk.max_kv = KV;
     attn_wk.counters = alloc<int>((size_t)m_max * KV * CNT_LINE);
@@ -590,6 +588,7 @@ struct Engine {
     gk_part = alloc<float>(gk_part_n);
     n_past.assign(lc.max_seqs, 0);
     last_tok.assign(lc.max_seqs, -1);
+    logits_row.assign(lc.max_seqs, -1);
   }
 
   // ---------------------------------------------------------------------------------------------
@@ -830,7 +829,7 @@ struct Engine {
   }
 
   // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
-  void decode_step(int n, const fa_sampling* s) {
+  void decode_step(int n) {
     // profiled (eager) steps: give the host a head start so the sampled event pairs time back-to-back kernels,
     // not host launch gaps
     if (prof) gpu_delay_us(1500, stream);
@@ -839,50 +838,22 @@ struct Engine {
     // embedded by fa_llm_generate before the steps)
     EmbedNext en;
     en.qs = tok_embd.q; en.d = tok_embd.d; en.E = lc.n_embd; en.x = lx; en.tok_pos = d_tok_pos;
-    sample(n, s, d_step, d_tok_cur, d_tok_hist, &en);
+    sample(n, d_tok_seq, d_tok_pos, d_step, d_tok_cur, d_tok_hist, &en);
   }
 
-  // hipGraph of one decode step (all per-step state lives in device memory, grids are n_past-independent).
-  // The profiled variant also captures event-record nodes around each timed kernel class, so the event
-  // timestamps are taken by the GPU between back-to-back graph nodes (no host launch gaps inside).
-  StepGraph& step_graph(int n, const fa_sampling* s, bool profiled) {
-    auto& cache = profiled ? prof_graphs : step_graphs;
-    auto it = cache.find(n);
-    if (it != cache.end()) return it->second;
-    StepGraph sg;
-    const bool save_prof = prof;
-    const size_t ev0 = ev_next;
-    prof = profiled;
-    std::vector<Pending> saved;
-    saved.swap(pending);
+  // hipGraph of one decode step (all per-step state, the sampler parameters included, lives in device memory;
+  // grids are n_past-independent), one per batch width
+  hipGraphExec_t step_graph(int n) {
+    auto it = step_graphs.find(n);
+    if (it != step_graphs.end()) return it->second;
     hipGraph_t g;
+    hipGraphExec_t ex;
     FA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    decode_step(n, s);
+    decode_step(n);
     FA_HIP(hipStreamEndCapture(stream, &g));
-    prof = save_prof;
-    if (profiled) {
-      // keep this graph's events out of the shared pool: they belong to the graph from now on
-      sg.events.swap(pending);
-      std::vector<std::pair<hipEvent_t, hipEvent_t>> mine(ev_pool.begin() + ev0, ev_pool.begin() + ev_next);
-      ev_pool.erase(ev_pool.begin() + ev0, ev_pool.begin() + ev_next);
-      graph_events.insert(graph_events.end(), mine.begin(), mine.end());
-      ev_next = ev0;
-    }
-    pending.swap(saved);
-    FA_HIP(hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0));
+    FA_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     FA_HIP(hipGraphDestroy(g));
-    return cache[n] = sg;
-  }
-
-  void collect_graph_events(const StepGraph& sg) {
-    for (const auto& p : sg.events) {
-      float ms = 0;
-      FA_HIP(hipEventElapsedTime(&ms, p.a, p.b));
-      pcls[p.cls].ms += ms;
-      pcls[p.cls].bytes += p.bytes;
-      pcls[p.cls].flops += p.flops;
-      pcls[p.cls].launches++;
-    }
+    return step_graphs[n] = ex;
   }
 
   void gemv(const GemvArgs& a0, int K, int epi) {
@@ -899,10 +870,17 @@ struct Engine {
     prof_end(cls, wbytes, 2.0 * a.M * a.O * K * (epi == 2 ? 2.0 : 1.0));
   }
 
-  void sample(int M, const fa_sampling* s, int* step_ctr, int* tok_out, int* hist, const EmbedNext* en = nullptr) {
-    const float temp = s ? s->temperature : 0.f;
-    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, M, temp, s ? s->top_k : 1, s ? s->top_p : 1.f,
-                  s ? s->seed : 0u, step_ctr, tok_out, hist, hist_max, en, stream);
+  // stage the call's sampler parameters in device memory (stream-ordered before the launches that read them;
+  // h_samp stays untouched until the call's closing synchronise)
+  void set_sampling(const fa_sampling* s) {
+    h_samp = SampleParams{s ? s->temperature : 0.f, s ? s->top_p : 1.f, s ? s->top_k : 1, s ? s->seed : 0u};
+    FA_REQUIRE(h_samp.temperature == h_samp.temperature && h_samp.top_p == h_samp.top_p, "sampling: NaN parameter");
+    FA_HIP(hipMemcpyAsync(d_samp, &h_samp, sizeof(SampleParams), hipMemcpyHostToDevice, stream));
+  }
+  void sample(int M, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out, int* hist,
+              const EmbedNext* en = nullptr) {
+    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, M, d_samp, row_seq, row_pos, step_ctr, tok_out,
+                  hist, hist_max, en, stream);
   }
 };
 
@@ -959,8 +937,10 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
-    if (const char* g = getenv("FUNASR_GEMV_SMALL")) fa::g_gemv_small_max = atoi(g);
-    if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g);
+    // A/B knobs of the decode GEMV: fused-GEMV batch limit (0..7; lm_head partials are sized for <= 7) and
+    // tokens per fused-GEMV block (1 or 2: the instantiated and tested variants)
+    if (const char* g = getenv("FUNASR_GEMV_SMALL")) fa::g_gemv_small_max = std::min(7, std::max(0, atoi(g)));
+    if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();
@@ -1201,6 +1181,7 @@ int fa_llm_reset(fa_engine* h, int32_t seq) {
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   e->n_past[seq] = 0;
   e->last_tok[seq] = -1;
+  e->logits_row[seq] = -1;
   FA_API_END
 }
 
@@ -1216,8 +1197,10 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   for (int i = 0; i < n_tokens; ++i) ps[i] = e->n_past[seq] + i;
   FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
+  e->set_sampling(s);
   e->llm_forward(n_tokens, false, e->n_past[seq] + n_tokens - 1);
-  e->sample(1, s, nullptr, e->d_tok_cur, nullptr);
+  // the first token's draw is keyed by the last prompt row's (seq, position)
+  e->sample(1, e->d_tok_seq + (n_tokens - 1), e->d_tok_pos + (n_tokens - 1), nullptr, e->d_tok_cur, nullptr);
   int tok = 0;
   FA_HIP(hipMemcpyAsync(&tok, e->d_tok_cur, 4, hipMemcpyDeviceToHost, e->stream));
   if (logits_out)
@@ -1226,6 +1209,8 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   e->prof_collect();
   e->n_past[seq] += n_tokens;
   e->last_tok[seq] = tok;
+  std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
+  e->logits_row[seq] = 0;
   if (tok_out) *tok_out = tok;
   FA_API_END
 }
@@ -1236,9 +1221,12 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   Engine* e = h->e;
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs && n_steps >= 1 && n_steps <= e->hist_max, "generate args");
   std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0);
+  std::vector<char> seen(e->lc.max_seqs, 0);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = seqs[i];
     FA_REQUIRE(q >= 0 && q < e->lc.max_seqs, "seq out of range");
+    FA_REQUIRE(!seen[q], "duplicate sequence id in one generate call");  // rows would share a KV slot / position
+    seen[q] = 1;
     FA_REQUIRE(e->last_tok[q] >= 0, "sequence has no sampled token (prefill first)");
     FA_REQUIRE(e->n_past[q] + n_steps <= e->lc.n_ctx, "generate exceeds n_ctx");
     sq[i] = q;
@@ -1251,34 +1239,35 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   FA_HIP(hipMemcpyAsync(e->d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
   // input row of the first step (later steps get theirs from the sampler launch)
   fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_tok_cur, n_seqs, e->lc.n_embd, 0, e->lx, e->stream);
-  // sampling parameters are baked into a captured graph: graphs only for the greedy path.
-  // With profiling on, the last step of the call replays the profiled graph variant (sampled timing).
-  // (event nodes inside graphs do not time individual nodes on ROCm 7.2: profiling runs eager)
-  const bool graph = e->use_graphs && !e->prof && (!s || s->temperature <= 0.f);
-  const Engine::StepGraph* pg = nullptr;
-  if (graph) {
-    const Engine::StepGraph& sg = e->step_graph(n_seqs, s, false);
-    for (int st = 0; st < n_steps; ++st) FA_HIP(hipGraphLaunch(sg.exec, e->stream));
+  e->set_sampling(s);
+  // the sampler reads its parameters from device memory, so the captured step graph serves every setting.
+  // Profiling runs eager (event nodes inside graphs do not time individual nodes on ROCm 7.2).
+  if (e->use_graphs && !e->prof) {
+    const hipGraphExec_t ex = e->step_graph(n_seqs);
+    for (int st = 0; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, e->stream));
   } else {
-    for (int st = 0; st < n_steps; ++st) e->decode_step(n_seqs, s);
+    for (int st = 0; st < n_steps; ++st) e->decode_step(n_seqs);
   }
   std::vector<int> hist((size_t)n_seqs * e->hist_max);
   FA_HIP(hipMemcpyAsync(hist.data(), e->d_tok_hist, hist.size() * 4, hipMemcpyDeviceToHost, e->stream));
   FA_HIP(hipStreamSynchronize(e->stream));
-  if (pg) e->collect_graph_events(*pg);
   e->prof_collect();
+  std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
     for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hist[(size_t)i * e->hist_max + st];
     e->n_past[seqs[i]] += n_steps;
     e->last_tok[seqs[i]] = hist[(size_t)i * e->hist_max + n_steps - 1];
+    e->logits_row[seqs[i]] = i;
   }
   FA_API_END
 }
 
-int fa_llm_logits(fa_engine* h, int32_t row, float* out) {
+int fa_llm_logits(fa_engine* h, int32_t seq, float* out) {
   FA_API_BEGIN
   Engine* e = h->e;
-  FA_REQUIRE(row >= 0 && row < e->lc.max_seqs, "row");
+  FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
+  const int row = e->logits_row[seq];
+  FA_REQUIRE(row >= 0, "fa_llm_logits: the most recent forward did not include this sequence");
   FA_HIP(hipMemcpy(out, e->logits + (size_t)row * e->lc.n_vocab, (size_t)e->lc.n_vocab * 4, hipMemcpyDeviceToHost));
   FA_API_END
 }

@@ -127,8 +127,15 @@ struct EmbedNext {
   float* x = nullptr;
   int* tok_pos = nullptr;
 };
+// Sampler chain parameters (fa_sampling) in device memory: one captured decode-step graph serves every setting.
+struct SampleParams {
+  float temperature, top_p;
+  int top_k;
+  uint32_t seed;
+};
+// row_seq / row_pos [M]: sequence id and position of each row's token (the draw's counter: (seed, seq, pos))
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   float temperature, int top_k, float top_p, uint32_t seed, int* step_ctr, int* tok_out,
+                   const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out,
                    int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s);
 void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s);
 void gpu_delay_us(int us, hipStream_t s);

@@ -81,13 +81,10 @@ __device__ __forceinline__ void norm_quant_row_block(const float* __restrict__ x
                                                      float* __restrict__ s_red) {
   constexpr int PER = NCH * 4;          // values per thread (K = NCH * 1024)
   constexpr int TPB = 32 / PER;         // threads per quant block (8, 4 or 2 for NCH 1, 2, 3 -> NCH 3 uses 12/32)
+  // K = 3072: 12 values per thread do not tile 32-blocks; that width uses per-wave chunks (norm_quant_row)
+  static_assert(NCH == 1 || NCH == 2, "norm_quant_row_block: K must be 1024 or 2048");
   const int t = threadIdx.x;
   float v[PER];
-  if (NCH == 3) {
-    // K = 3072: 12 values per thread do not tile 32-blocks evenly; use 256 threads x 12 = 3072 with
-    // blocks of 32 spanning 8/3 threads -> fall back to per-wave chunks (3 waves x 1024)
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < PER; j += 4) {
     const float4 f = *reinterpret_cast<const float4*>(x + t * PER + j);
@@ -870,12 +867,10 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens)
     const int mt = a.M <= 2 ? 1 : std::min(g_gemv_mt, a.M);
     if (mt <= 1) launch_gemv_fused<1>(K, epi, a, s);
-    else if (mt <= 2) launch_gemv_fused<2>(K, epi, a, s);
-    else if (mt <= 4) launch_gemv_fused<4>(K, epi, a, s);
-    else launch_gemv_fused<8>(K, epi, a, s);
+    else launch_gemv_fused<2>(K, epi, a, s);
     return;
   }
-  FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M<=4");
+  FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
   if (g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
@@ -1421,37 +1416,157 @@ void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E,
 }
 
 // ------------------------------------------------------------------------------------------------
-// D6 sampling. Greedy: reduce the lm_head's per-wave argmax partials. Temperature > 0: top-k (by
-// bisection on the value threshold) -> top-p -> temperature -> categorical draw with a counter-based RNG
-// (llama.cpp's mt19937 draw is seeded from np.random per call, decoder.py:89, i.e. nondeterministic:
-// parity is defined at temperature 0 only).
+// D6 sampling: the LlamaSampler chain (llama.py:599-605). temperature <= 0 or top_k == 1: greedy (reduce the
+// lm_head's per-wave argmax partials). Otherwise top_k -> top_p (min_keep 1) -> temp -> dist, as llama.cpp's
+// chain applies them:
+//   * top_k keeps the k largest logits (top_k <= 0: all); ties at the k-th value keep the lowest token ids;
+//   * top_p < 1 keeps the shortest prefix of those, sorted by logit, whose softmax mass at temperature 1
+//     reaches top_p (at least one token); top_p >= 1 is a no-op;
+//   * dist draws by inverse CDF over softmax(l / T) of the kept tokens in sorted order. The uniform u is a
+//     counter-based hash of (seed, sequence, position), so every (sequence, position) draws afresh, in every
+//     call (llama.cpp seeds an mt19937 per call from np.random, decoder.py:89: nondeterministic, so the
+//     distribution is the contract, not the draw).
+// Fast path (k <= SAMPLE_CAP): the lm_head's per-chunk maxima bound the k-th largest logit from below (k chunks
+// have a maximum >= tau), so ONE pass over the logits gathers a superset of the top-k into LDS, where it is
+// sorted (bitonic, by logit desc then id asc). Wide path (top_k <= 0 or > SAMPLE_CAP, or a superset larger
+// than SAMPLE_CAP): radix selects of the count (top-k) and mass (top-p) thresholds over the whole row, the draw
+// in token-id order; ties AT a threshold value are all kept there (real-valued logits: measure zero).
+// Sampling parameters are read from device memory, so one captured decode-step graph serves every setting.
+constexpr int SAMPLE_CAP = 4096;
+constexpr int SAMPLE_T = 1024;  // threads per row (16 waves)
+
 __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
   x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
   return x;
 }
-
-__global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logits, int64_t ldl, int V,
-                                                 const float* __restrict__ pval, const int* __restrict__ pidx, int n_part,
-                                                 float temperature, int top_k, float top_p, uint32_t seed,
-                                                 int* __restrict__ step_ctr, int* __restrict__ tok_out,
-                                                 int* __restrict__ tok_hist, int hist_stride, EmbedNext en) {
-  const int m = blockIdx.x;
+// order-preserving float -> uint32 map (larger float <-> larger key) and back
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+// exclusive prefix of v over the block's threads (1024) in thread order; *total = block sum (block-uniform)
+template <typename T>
+__device__ T block_excl_scan(T v, T* s_w, T* total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ float sv[16];
-  __shared__ int si[16];
-  __shared__ float s_thr;
-  __shared__ int s_cnt[16];
+  const T inc = wave_incl_scan(v);
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  T off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < SAMPLE_T / 64; ++w) {
+    const T x = s_w[w];
+    if (w < wave) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + inc - v;
+}
+template <typename T>
+__device__ T block_sum(T v, T* s_w) {
+  T tot;
+  (void)block_excl_scan(v, s_w, &tot);
+  return tot;
+}
+
+// Radix select, descending: over the items get(i, &key, &w) -> valid (i in [0, n), strided over the block),
+// the largest key P with weight(key > P) < need <= weight(key >= P) (need clamped to the total weight: the
+// smallest valid key then). T = int: counts (k-th largest); T = float: softmax mass (top-p cut).
+template <typename T, typename Get>
+__device__ uint32_t radix_select_desc(Get get, int n, T need, T* hist, int* s_dig, T* s_need) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t prefix = 0, mask = 0;
+  if (threadIdx.x == 0) *s_need = need;
+  for (int sh = 24; sh >= 0; sh -= 8) {
+    for (int i = threadIdx.x; i < 256; i += SAMPLE_T) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += SAMPLE_T) {
+      uint32_t key;
+      T w;
+      if (get(i, key, w) && (key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255], w);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      T c[4], s = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * lane - j];
+        s += c[j];
+      }
+      const T inc = wave_incl_scan(s);
+      const T tot = __shfl(inc, 63, 64);
+      T nd = *s_need;
+      if (nd > tot) nd = tot;
+      const T exc = inc - s;
+      if (inc >= nd && exc < nd) {  // exactly one lane (nd > 0); a zero total keeps digit 0
+        T acc = exc;
+        int d = 255 - 4 * lane - 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (acc + c[j] >= nd) { d = 255 - 4 * lane - j; break; }
+          acc += c[j];
+        }
+        *s_dig = d;
+        *s_need = nd - acc;
+      } else if (lane == 0 && !(tot > 0)) {
+        *s_dig = 0;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint32_t)(*s_dig) << sh;
+    mask |= 0xFFu << sh;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+struct SampleShared {
+  unsigned long long list[SAMPLE_CAP];  // fast path: (~key << 32 | id), sorted ascending = logit desc, id asc
+  float hist_f[256];
+  int hist_i[256];
+  float wf[SAMPLE_T / 64];
+  int wi[SAMPLE_T / 64];
+  float need_f;
+  int need_i, dig, cnt, pick, last_thr;
+  float argv[16];
+  int argi[16];
+};
+
+__global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ logits, int64_t ldl, int V,
+                                                     const float* __restrict__ pval, const int* __restrict__ pidx,
+                                                     int n_part, const SampleParams* __restrict__ sp,
+                                                     const int* __restrict__ row_seq, const int* __restrict__ row_pos,
+                                                     int* __restrict__ step_ctr, int* __restrict__ tok_out,
+                                                     int* __restrict__ tok_hist, int hist_stride, EmbedNext en) {
+  __shared__ SampleShared S;
+  const int m = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float temperature = sp->temperature, top_p = sp->top_p;
+  const int top_k = sp->top_k;
   int tok;
   if (temperature <= 0.f || top_k == 1) {
     float v = -INFINITY;
     int i = 0x7fffffff;
     // partials 4 per thread in flight at once (a plain strided loop waits on each load before the next)
-    for (int t0 = 0; t0 < n_part; t0 += 4096) {
+    for (int t0 = 0; t0 < n_part; t0 += 4 * SAMPLE_T) {
       float pv[4];
       int pi[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int t = min(t0 + u * 1024 + (int)threadIdx.x, n_part - 1);  // clamped duplicates: argmax unchanged
+        const int t = min(t0 + u * SAMPLE_T + tid, n_part - 1);  // clamped duplicates: argmax unchanged
         pv[u] = pval[(int64_t)m * n_part + t];
         pi[u] = pidx[(int64_t)m * n_part + t];
       }
@@ -1464,78 +1579,173 @@ __global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logit
       int i2 = __shfl_xor(i, o, 64);
       argmax_combine(v, i, v2, i2);
     }
-    if (lane == 0) { sv[wave] = v; si[wave] = i; }
+    if (lane == 0) { S.argv[wave] = v; S.argi[wave] = i; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int w = 1; w < 16; ++w) argmax_combine(v, i, sv[w], si[w]);
-      si[0] = i;
+    if (tid == 0) {
+      for (int w = 1; w < 16; ++w) argmax_combine(v, i, S.argv[w], S.argi[w]);
+      S.argi[0] = i;
     }
     __syncthreads();
-    tok = si[0];
+    tok = S.argi[0];
   } else {
     const float* lg = logits + (int64_t)m * ldl;
-    // max
-    float mx = -INFINITY;
-    for (int t = threadIdx.x; t < V; t += 1024) mx = fmaxf(mx, lg[t]);
-    mx = wave_max(mx);
-    if (lane == 0) sv[wave] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) { float a = sv[0]; for (int w = 1; w < 16; ++w) a = fmaxf(a, sv[w]); sv[0] = a; }
-    __syncthreads();
-    mx = sv[0];
-    __syncthreads();
-    // threshold for top-k by bisection: count(lg >= thr) >= k
-    float lo = mx - 1e4f, hi = mx;
-    const int k = top_k <= 0 ? V : min(top_k, V);
-    for (int it = 0; it < 40; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      int c = 0;
-      for (int t = threadIdx.x; t < V; t += 1024) c += lg[t] >= mid;
-      c = wave_sum_i(c);
-      if (lane == 0) s_cnt[wave] = c;
+    const int k = (top_k <= 0 || top_k >= V) ? V : top_k;
+    uint32_t h = hash_u32(sp->seed ^ 0x5BD1E995u);
+    h = hash_u32(h ^ ((uint32_t)row_seq[m] * 0x9E3779B9u));
+    h = hash_u32(h ^ ((uint32_t)row_pos[m] * 0x85EBCA6Bu + 0x632BE5ABu));
+    const float u = (float)(h >> 8) * 5.9604644775390625e-08f;  // [0, 1)
+    bool fast = k <= SAMPLE_CAP && k <= n_part && n_part <= 2 * SAMPLE_CAP;
+    if (fast) {
+      // tau = k-th largest chunk maximum (keys staged in LDS, reusing the candidate list's space)
+      uint32_t* pk = reinterpret_cast<uint32_t*>(S.list);
+      for (int i = tid; i < n_part; i += SAMPLE_T) pk[i] = fkey(pval[(int64_t)m * n_part + i]);
+      if (tid == 0) S.cnt = 0;
       __syncthreads();
-      if (threadIdx.x == 0) { int a = 0; for (int w = 0; w < 16; ++w) a += s_cnt[w]; s_cnt[0] = a; }
-      __syncthreads();
-      if (s_cnt[0] >= k) lo = mid; else hi = mid;
-      __syncthreads();
-    }
-    const float thr = lo;
-    // softmax mass of the candidates at temperature (top_p >= 1 is a no-op in llama.cpp)
-    float z = 0.f;
-    for (int t = threadIdx.x; t < V; t += 1024) if (lg[t] >= thr) z += expf((lg[t] - mx) / temperature);
-    z = wave_sum(z);
-    if (lane == 0) sv[wave] = z;
-    __syncthreads();
-    if (threadIdx.x == 0) { float a = 0; for (int w = 0; w < 16; ++w) a += sv[w]; sv[0] = a; }
-    __syncthreads();
-    z = sv[0];
-    const uint32_t ctr = step_ctr ? (uint32_t)step_ctr[m] : 0u;
-    const float u = (float)(hash_u32(seed ^ hash_u32(ctr * 0x9E3779B9u + (uint32_t)m)) >> 8) * 5.9604644775390625e-08f;
-    if (threadIdx.x == 0) {
-      // sequential inverse-CDF over candidates in index order (one thread: only ~k candidates pass)
-      float acc = 0.f;
-      int pick = -1, last = 0;
-      const float target = u * z;
-      for (int t = 0; t < V; ++t) {
-        if (lg[t] >= thr) {
-          acc += expf((lg[t] - mx) / temperature);
-          last = t;
-          if (acc > target) { pick = t; break; }
+      const uint32_t tau = radix_select_desc<int>(
+          [&](int i, uint32_t& key, int& w) { key = pk[i]; w = 1; return true; }, n_part, k, S.hist_i, &S.dig,
+          &S.need_i);
+      // one pass over the row: every logit >= tau into the list (a superset of the top-k)
+      for (int i = tid; i < V; i += SAMPLE_T) {
+        const uint32_t key = fkey(lg[i]);
+        if (key >= tau) {
+          const int slot = atomicAdd(&S.cnt, 1);
+          if (slot < SAMPLE_CAP) S.list[slot] = ((unsigned long long)(~key) << 32) | (uint32_t)i;
         }
       }
-      si[0] = pick < 0 ? last : pick;
+      __syncthreads();
+      fast = S.cnt <= SAMPLE_CAP;  // block-uniform
     }
-    __syncthreads();
-    tok = si[0];
+    if (fast) {
+      const int c = S.cnt;
+      int P = 2;
+      while (P < c) P <<= 1;
+      for (int i = c + tid; i < P; i += SAMPLE_T) S.list[i] = ~0ull;
+      __syncthreads();
+      for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int i = tid; i < (P >> 1); i += SAMPLE_T) {
+            const int pos = 2 * i - (i & (stride - 1));
+            const unsigned long long x = S.list[pos], y = S.list[pos + stride];
+            if ((x > y) == ((pos & size) == 0)) { S.list[pos] = y; S.list[pos + stride] = x; }
+          }
+          __syncthreads();
+        }
+      }
+      int nk = min(k, c);
+      const float v0 = fkey_inv(~(uint32_t)(S.list[0] >> 32));
+      // thread t holds sorted entries [4t, 4t + 4)
+      float lv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * tid + j;
+        lv[j] = i < nk ? fkey_inv(~(uint32_t)(S.list[i] >> 32)) : -INFINITY;
+      }
+      if (top_p < 1.f) {
+        float w[4], s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          w[j] = 4 * tid + j < nk ? expf(lv[j] - v0) : 0.f;
+          s += w[j];
+        }
+        const float z1 = block_sum(s, S.wf);
+        float ps = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { w[j] /= z1; ps += w[j]; }
+        float tot;
+        float cum = block_excl_scan(ps, S.wf, &tot);
+        if (tid == 0) S.pick = nk;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cum += w[j];
+          if (4 * tid + j < nk && cum >= top_p) { atomicMin(&S.pick, 4 * tid + j + 1); break; }
+        }
+        __syncthreads();
+        nk = S.pick;
+      }
+      float e[4], s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = 4 * tid + j < nk ? expf((lv[j] - v0) / temperature) : 0.f;
+        s += e[j];
+      }
+      float z;
+      float cum = block_excl_scan(s, S.wf, &z);
+      const float target = u * z;
+      if (tid == 0) S.pick = nk - 1;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cum += e[j];
+        if (4 * tid + j < nk && cum > target) { atomicMin(&S.pick, 4 * tid + j); break; }
+      }
+      __syncthreads();
+      tok = (int)(uint32_t)S.list[S.pick];
+    } else {
+      // wide path over the whole row
+      float mx = -INFINITY;
+      for (int i = tid; i < V; i += SAMPLE_T) mx = fmaxf(mx, lg[i]);
+      mx = wave_max(mx);
+      if (lane == 0) S.wf[wave] = mx;
+      __syncthreads();
+      mx = S.wf[0];
+      for (int w = 1; w < SAMPLE_T / 64; ++w) mx = fmaxf(mx, S.wf[w]);
+      __syncthreads();
+      uint32_t keep = 0;
+      if (k < V)
+        keep = radix_select_desc<int>([&](int i, uint32_t& key, int& w) { key = fkey(lg[i]); w = 1; return true; },
+                                      V, k, S.hist_i, &S.dig, &S.need_i);
+      if (top_p < 1.f) {
+        float s = 0.f;
+        for (int i = tid; i < V; i += SAMPLE_T) s += fkey(lg[i]) >= keep ? expf(lg[i] - mx) : 0.f;
+        const float z1 = block_sum(s, S.wf);
+        const uint32_t kk = keep;
+        keep = radix_select_desc<float>(
+            [&](int i, uint32_t& key, float& w) {
+              key = fkey(lg[i]);
+              w = expf(lg[i] - mx);
+              return key >= kk;
+            },
+            V, top_p * z1, S.hist_f, &S.dig, &S.need_f);
+      }
+      // draw in token-id order: thread t owns ids [t C, t C + C)
+      const int C = (V + SAMPLE_T - 1) / SAMPLE_T;
+      const int i0 = min(V, tid * C), i1 = min(V, i0 + C);
+      float s = 0.f;
+      int lastc = -1;
+      for (int i = i0; i < i1; ++i)
+        if (fkey(lg[i]) >= keep) { s += expf((lg[i] - mx) / temperature); lastc = i; }
+      float z;
+      const float excl = block_excl_scan(s, S.wf, &z);
+      const float target = u * z;
+      if (tid == 0) { S.pick = -1; S.last_thr = -1; }
+      __syncthreads();
+      if (lastc >= 0) atomicMax(&S.last_thr, tid);
+      if (s > 0.f && excl <= target && target < excl + s) {
+        float acc = excl;
+        int pk = lastc;
+        for (int i = i0; i < i1; ++i) {
+          if (fkey(lg[i]) >= keep) {
+            acc += expf((lg[i] - mx) / temperature);
+            if (acc > target) { pk = i; break; }
+          }
+        }
+        atomicMax(&S.pick, pk);
+      }
+      __syncthreads();
+      if (S.pick < 0 && tid == S.last_thr) S.pick = lastc;  // target rounded past the total: last candidate
+      __syncthreads();
+      tok = S.pick;
+    }
   }
   if (en.x) {
     // decode step tail: the next step's input row (D0, f32 token_embd row) and the position advance ride along,
     // so a step is forward + this launch (the row was consumed by the lm_head launch before this one)
     const int64_t row = tok;
-    for (int i = threadIdx.x; i < en.E; i += 1024)
+    for (int i = tid; i < en.E; i += SAMPLE_T)
       en.x[(int64_t)m * en.E + i] = __half2float(en.d[row * (en.E / 32) + i / 32]) * (float)en.qs[row * en.E + i];
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     tok_out[m] = tok;
     const int c = step_ctr ? step_ctr[m] : 0;
     if (tok_hist) tok_hist[(int64_t)m * hist_stride + c] = tok;
@@ -1547,11 +1757,12 @@ __global__ __launch_bounds__(1024) void k_sample(const float* __restrict__ logit
 }
 
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   float temperature, int top_k, float top_p, uint32_t seed, int* step_ctr, int* tok_out,
+                   const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out,
                    int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s) {
   FA_REQUIRE(!en || (step_ctr && en->tok_pos && en->qs && en->d && en->E % 32 == 0), "sample_tokens: embed-next args");
-  hipLaunchKernelGGL(k_sample, dim3(M), dim3(1024), 0, s, logits, ldl, V, pval, pidx, n_part, temperature, top_k, top_p,
-                     seed, step_ctr, tok_out, tok_hist, hist_stride, en ? *en : EmbedNext{});
+  FA_REQUIRE(d_params && row_seq && row_pos, "sample_tokens: params / row ids");
+  hipLaunchKernelGGL(k_sample, dim3(M), dim3(SAMPLE_T), 0, s, logits, ldl, V, pval, pidx, n_part, d_params, row_seq,
+                     row_pos, step_ctr, tok_out, tok_hist, hist_stride, en ? *en : EmbedNext{});
 }
 
 // Profiling aid: one wave spins for `us` microseconds (100 MHz reference clock), so an eager host that

@@ -257,9 +257,10 @@ class Engine:
                "fa_llm_generate")
         return out
 
-    def llm_logits(self, row=0):
+    def llm_logits(self, seq=0):
+        """Logits of `seq`'s row in the most recent forward (prefill or generate step) that included it."""
         out = np.empty(self.llm_cfg["n_vocab"], np.float32)
-        _check(self.lib.fa_llm_logits(self.h, row, _ptr(out)), "fa_llm_logits")
+        _check(self.lib.fa_llm_logits(self.h, seq, _ptr(out)), "fa_llm_logits")
         return out
 
     def llm_n_past(self, seq=0):

@@ -130,6 +130,32 @@ class LLMDecoder:
                top_p=1.0, top_k=50):
         return self.decode_many([full_embd], n_predict, temperature, top_p, top_k, reporter, stream_output)[0]
 
+    def decode_with_retry(self, embds, n_predict, temperature=0.3, top_p=1.0, top_k=50, reporter=None,
+                          stream_output=False, attempts=6):
+        """The reference's retry policy (decoder.py:201-211) per sequence: an attempt cut by the repetition
+        breaker is decoded again at temperature + 0.3, up to 6 attempts in all; the final attempt's text keeps the
+        abort marker when it was cut too. Sequences still pending retry together as one batch."""
+        B = len(embds)
+        temps = [temperature] * B
+        final = [None] * B
+        pending = list(range(B))
+        for attempt in range(attempts):
+            rs = self.decode_many([embds[b] for b in pending], n_predict, temps[pending[0]], top_p, top_k, reporter,
+                                  stream_output)
+            nxt = []
+            for b, r in zip(pending, rs):
+                if r.is_aborted and attempt < attempts - 1:
+                    temps[b] += 0.3
+                    nxt.append(b)
+                else:
+                    if r.is_aborted:
+                        r.text += ABORT_MARK
+                    final[b] = r
+            if not nxt:
+                break
+            pending = nxt
+        return final
+
 
 class StreamDecoder:
     def __init__(self, models):
@@ -177,26 +203,8 @@ class StreamDecoder:
         for tm in timings:
             tm.prepare = dt / B
         # 4. LLM with the reference's retry policy (decoder.py:201-211), per sequence
-        n_predict = m.config.n_predict
-        temps = [temperature] * B
-        final = [None] * B
-        pending = list(range(B))
-        for attempt in range(6):
-            rs = self.llm_decoder.decode_many([embds[b] for b in pending], n_predict, temps[pending[0]], top_p, top_k,
-                                              reporter, verbose)
-            nxt = []
-            for b, r in zip(pending, rs):
-                if r.is_aborted and attempt < 5:
-                    temps[b] += 0.3
-                    nxt.append(b)
-                elif r.is_aborted:
-                    r.text += ABORT_MARK
-                    final[b] = r
-                else:
-                    final[b] = r
-            if not nxt:
-                break
-            pending = nxt
+        final = self.llm_decoder.decode_with_retry(embds, m.config.n_predict, temperature, top_p, top_k, reporter,
+                                                   verbose)
         results = []
         for b in range(B):
             r = final[b]

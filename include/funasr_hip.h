@@ -47,8 +47,9 @@ typedef struct fa_llm_config {
   float rope_theta, rms_eps;
 } fa_llm_config;
 
-/* Sampler chain of LlamaSampler (llama.py:577-605): temperature <= 0 -> greedy;
- * else top_k -> top_p -> temp -> dist(seed). */
+/* Sampler chain of LlamaSampler (llama.py:577-605): temperature <= 0 (or top_k == 1) -> greedy;
+ * else top_k (<= 0: all) -> top_p (min_keep 1; >= 1: no-op) -> temp -> dist. The draw of a token is keyed
+ * by (seed, sequence id, position), so every step and every call draws afresh. */
 typedef struct fa_sampling {
   float temperature, top_p;
   int32_t top_k;
@@ -117,12 +118,13 @@ int fa_llm_reset(fa_engine* e, int32_t seq);
  * token with `s`. logits_out (nullable) receives the last-row logits [n_vocab]. */
 int fa_llm_prefill(fa_engine* e, int32_t seq, const float* embd, int32_t n_tokens, const fa_sampling* s,
                    int32_t* tok_out, float* logits_out);
-/* Run n_steps decode steps for n_seqs sequences in one continuous batch: each step feeds every
- * sequence's last sampled token at its next position and samples the next one on device
+/* Run n_steps decode steps for n_seqs sequences (distinct ids) in one continuous batch: each step feeds
+ * every sequence's last sampled token at its next position and samples the next one on device
  * (decoder.py:91-98). tokens_out [n_seqs, n_steps]. No host round trip inside the call. */
 int fa_llm_generate(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
                     int32_t* tokens_out);
-/* Logits of the most recent forward for a sequence slot (test hook) [n_vocab]. */
+/* Logits [n_vocab] of sequence `seq` from the most recent forward (fa_llm_prefill, or the last step of
+ * fa_llm_generate) when that forward included it; FA_ERR_ARG otherwise (test hook; llama_get_logits_ith). */
 int fa_llm_logits(fa_engine* e, int32_t seq, float* out);
 /* Current length (n_past) of a sequence slot. */
 int fa_llm_n_past(fa_engine* e, int32_t seq, int32_t* out);

@@ -222,7 +222,7 @@ def test_llm_long_context_split_attention(tiny_engine, llm_tiny_oracle):
     pos = prompt.shape[0]
     for _ in range(5):
         nxt = tiny_engine.llm_generate([1], 1)[0][0]
-        lg_new = tiny_engine.llm_logits(0)  # row 0 of the 1-sequence batch
+        lg_new = tiny_engine.llm_logits(1)
         ref = m.forward(m.embed_tokens([tok]), pos)
         _check_step(lg_new, ref)
         tok, pos = int(nxt), pos + 1
