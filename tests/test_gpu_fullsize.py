@@ -1,0 +1,242 @@
+"""GPU parity at the BENCHMARKED sizes (BASELINE.json configs[0..4]): the full 70-block encoder, the full Qwen3-0.6B
+q8_0 decoder (28 layers, vocab 151936) and the 300 s long-audio path, on the synthetic weights of oracle/synth.py.
+
+Oracles:
+  * reference goldens generated from /root/reference's model_definition.py (tests/golden/make_golden.py):
+    encoder_full_60s (configs[1] clip, T_lfr 1001) and encoder_full_10s (configs[0] clip);
+  * oracle/cref (C++/OpenMP restatement, pinned in tests/test_cref.py to those goldens and to the numpy oracle)
+    for the decoder at full dims and for clips no golden holds (batch of 32, C4 segments);
+  * oracle/encoder_fp16 (numpy) for the fp16 graph (configs[4]).
+Tolerances as test_gpu_parity.py: encoder fp32 max-abs/max <= 5e-4 and cosine >= 0.99999 (full depth); CTC ids
+exact where the top-1/top-2 margin exceeds 1e-3; decoder teacher-forced logits cosine >= 0.9995 with equal argmax
+where the oracle's top-2 margin exceeds 0.25 (q8_0 activation rounding noise, tests/test_oracle_golden.py).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import cref, ctc as octc, synth
+
+pytestmark = pytest.mark.gpu
+
+SR = 16000
+ENC_ATOL = 5e-4
+TIE_MARGIN = 0.25
+
+
+def _cos(a, b):
+    a = np.asarray(a, np.float64).ravel()
+    b = np.asarray(b, np.float64).ravel()
+    return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b) + 1e-30))
+
+
+def _rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(1e-6, float(np.abs(b).max())))
+
+
+def _check_step(gpu, ref):
+    assert _cos(gpu, ref) > 0.9995
+    s = np.sort(ref)
+    if s[-1] - s[-2] > TIE_MARGIN:
+        assert int(np.argmax(gpu)) == int(np.argmax(ref))
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fun_asr_gguf import _native
+    e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_FULL, n_ctx=512, max_seqs=32), max_batch=32,
+                       max_samples=SR * 62)
+    e.synthetic_weights(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def cenc():
+    e = cref.CEncoder(synth.ENC_FULL)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def cllm():
+    m = cref.CQwen3(synth.LLM_FULL, n_ctx=512, max_seqs=1)
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def g60():
+    from fun_asr_gguf.synthetic import synth_audio
+    g = dict(np.load(os.path.join(GOLDEN, "encoder_full_60s.npz")))
+    a = synth_audio(960000, int(g["audio_seed"]))
+    assert hashlib.sha256(a.tobytes()).digest() == g["audio_sha256"].tobytes(), "synthetic audio changed"
+    g["audio"] = a
+    return g
+
+
+def _check_encoder(out_enc, out_emb, out_ids, ref_enc, ref_emb, ref_ids, margin, tag):
+    assert _rel(out_enc, ref_enc) < ENC_ATOL and _cos(out_enc, ref_enc) > 0.99999, tag
+    assert out_emb.shape == ref_emb.shape, tag
+    assert _rel(out_emb, ref_emb) < ENC_ATOL and _cos(out_emb, ref_emb) > 0.99999, tag
+    bad = (out_ids != ref_ids) & (margin > 1e-3)
+    assert bad.sum() == 0, f"{tag}: {int(bad.sum())} non-tie CTC ids differ"
+
+
+def test_encoder_60s_vs_reference_golden(eng, g60):
+    """configs[1] clip: T_lfr 1001 (key splits, XCD tile order and K-split GEMMs of the one-clip shapes)."""
+    out = eng.encode([g60["audio"]], want_enc=True)
+    T = int(g60["t_lfr_valid"])
+    assert T == 1001 and out["enc"][0].shape[0] == T and int(out["target_len"][0]) == 126
+    rows = g60["enc_rows"]
+    _check_encoder(out["enc"][0][rows], out["audio_embd"][0], out["ctc_ids"][0], g60["enc"], g60["adaptor"],
+                   g60["ctc_ids"], g60["ctc_margin"], "60 s")
+
+
+def test_encoder_batch32_vs_oracle(eng, cenc):
+    """configs[2]: 32 clips in one encoder batch (32 x 1001 rows: the 128x128-tile f32 GEMM path), ragged lengths
+    included; clips 0, 5, 17 and 31 against the oracle run of each clip alone (CPU-EP policy, unpadded)."""
+    from fun_asr_gguf.synthetic import synth_audio
+    lens = [960000] * 32
+    lens[5], lens[17], lens[31] = 661234, 192000, 959999
+    clips = [synth_audio(n, 1000 + i) for i, n in enumerate(lens)]
+    out = eng.encode(clips, want_enc=True)
+    for b in (0, 5, 17, 31):
+        r = cenc.encode(clips[b])
+        _check_encoder(out["enc"][b], out["audio_embd"][b], out["ctc_ids"][b], r["enc"], r["audio_embd"],
+                       r["ctc_ids"], r["ctc_margin"], f"clip {b}")
+
+
+def test_encoder_fp16_60s_vs_oracle(eng, g60):
+    """configs[4] encoder: the float16 graphs (02-Quantize-ONNX.py:13-27) at 60 s against oracle/encoder_fp16, and
+    within fp16 accuracy of the fp32 reference golden."""
+    from oracle import encoder_fp16 as oe16
+    W = synth.make_weights(synth.encoder_tensors(synth.ENC_FULL))
+    eng.set_encoder_fp16(True)
+    try:
+        out = eng.encode([g60["audio"]], want_enc=True)
+    finally:
+        eng.set_encoder_fp16(False)
+    r = oe16.encode(g60["audio"], W, synth.ENC_FULL)
+    del W
+    enc, emb = out["enc"][0], out["audio_embd"][0]
+    assert (emb.astype(np.float16).astype(np.float32) == emb).all()
+    assert _rel(enc, r["enc"]) < 1e-2 and _cos(enc, r["enc"]) > 0.9999
+    assert _rel(emb, r["audio_embd"]) < 1e-2 and _cos(emb, r["audio_embd"]) > 0.9999
+    assert _cos(emb, g60["adaptor"]) > 0.999
+    lg = r["ctc_logits"]
+    top2 = np.sort(lg, -1)[:, -2:]
+    nontie = (top2[:, 1] - top2[:, 0]) > 0.05
+    assert ((out["ctc_ids"][0] != r["ctc_ids"]) & nontie).sum() == 0
+
+
+def _prompt(cllm, audio_rows, seed):
+    rng = np.random.default_rng(seed)
+    return np.concatenate([cllm.embed_prompt(rng.integers(0, 151933, 73)), audio_rows.astype(np.float32),
+                           cllm.embed_prompt(rng.integers(0, 151933, 5))], 0)
+
+
+@pytest.mark.parametrize("clip", ["10s", "60s"])
+def test_llm_full_prefill_and_steps_teacher_forced(eng, cllm, g60, clip):
+    """configs[0]/[1] decoder at full dims: 73 + target_len + 5 prefill rows (99 / 204), then 6 steps; every
+    step's full-vocab logits against the oracle fed the same token, and the device's greedy pick (argmax-partial
+    reduction of the 151936-wide LM head) equal to the argmax of its own logits."""
+    audio_rows = g60["adaptor"] if clip == "60s" else np.load(os.path.join(GOLDEN, "encoder_full_10s.npz"))["adaptor"]
+    p = _prompt(cllm, audio_rows, 1 if clip == "60s" else 2)
+    assert p.shape[0] == (204 if clip == "60s" else 99)
+    eng.llm_reset(0)
+    tok, lg = eng.llm_prefill(0, p, want_logits=True)
+    ref = cllm.forward(p, 0)
+    _check_step(lg, ref)
+    assert tok == int(np.argmax(lg))
+    pos = p.shape[0]
+    for _ in range(6):
+        nxt = int(eng.llm_generate([0], 1)[0][0])
+        lg = eng.llm_logits(0)
+        ref = cllm.forward(cllm.embed_tokens([tok]), pos)
+        _check_step(lg, ref)
+        assert nxt == int(np.argmax(lg))
+        tok, pos = nxt, pos + 1
+    assert eng.llm_n_past(0) == p.shape[0] + 6
+
+
+@pytest.mark.parametrize("n_seq", [5, 32])
+def test_llm_full_batched_decode_rows(eng, cllm, n_seq):
+    """configs[2] continuous batch at full dims: M = 32 (int8 MFMA GEMMs + the batched LM head with its argmax
+    partials) and M = 5 (fused GEMV, 2 tokens per block); sampled rows against the oracle run of that sequence
+    alone, two steps."""
+    rng = np.random.default_rng(40 + n_seq)
+    lens = [int(n) for n in rng.integers(6, 48, n_seq)]
+    prompts = [cllm.embed_prompt(rng.integers(0, 151933, n)) for n in lens]
+    firsts = []
+    for s, p in enumerate(prompts):
+        eng.llm_reset(s)
+        firsts.append(eng.llm_prefill(s, p))
+    seqs = list(range(n_seq))
+    steps = [eng.llm_generate(seqs, 1)[:, 0]]
+    logits1 = {s: eng.llm_logits(s) for s in (0, n_seq // 3, n_seq - 1)}
+    steps.append(eng.llm_generate(seqs, 1)[:, 0])
+    logits2 = {s: eng.llm_logits(s) for s in logits1}
+    for s in logits1:
+        cllm.forward(prompts[s], 0)
+        r1 = cllm.forward(cllm.embed_tokens([firsts[s]]), lens[s])
+        _check_step(logits1[s], r1)
+        assert int(steps[0][s]) == int(np.argmax(logits1[s]))
+        r2 = cllm.forward(cllm.embed_tokens([int(steps[0][s])]), lens[s] + 1)
+        _check_step(logits2[s], r2)
+        assert int(steps[1][s]) == int(np.argmax(logits2[s]))
+
+
+def test_sampler_full_vocab_membership(eng, cllm, g60):
+    """Default transcribe() sampling (temperature 0.4, top_k 50; asr_engine.py:65) on the 151936-wide LM head:
+    every draw in the top-k set of that step's logits (and in the top-p prefix when top_p < 1)."""
+    p = _prompt(cllm, g60["adaptor"], 3)
+    eng.llm_reset(0)
+    eng.llm_prefill(0, p, temperature=0.4, top_k=50, seed=5)
+    for step in range(8):
+        top_p = 1.0 if step % 2 == 0 else 0.7
+        t = int(eng.llm_generate([0], 1, temperature=0.4, top_k=50, top_p=top_p, seed=99 + step)[0][0])
+        lg = eng.llm_logits(0).astype(np.float64)
+        order = np.argsort(-lg, kind="stable")[:50]
+        assert lg[t] >= lg[order[-1]]
+        if top_p < 1:
+            v = lg[order]
+            w = np.exp(v - v[0])
+            cum = np.cumsum(w / w.sum())
+            n = int(np.searchsorted(cum, top_p - 1e-6)) + 1
+            assert lg[t] >= v[n - 1]
+
+
+def test_c4_300s_long_audio_full_model(cenc):
+    """configs[3]: one 300 s file, segment 60 / overlap 4 -> 6 segments through the public transcribe() long path
+    (one device batch), 253 greedy tokens per segment (pinned length). Pinned: the windows (oracle of
+    orchestrator.py:123-136), every segment's CTC ids / audio rows against the oracle encoder on the unpadded
+    chunk, and the merged text + char timestamps = the reference merge rule (oracle.ctc.merge_results, pinned to
+    text_merge.py goldens) applied to the per-segment results."""
+    from fun_asr_gguf import create_asr_engine
+    from fun_asr_gguf.synthetic import synth_audio
+    api = create_asr_engine("synthetic", "synthetic", "synthetic", "synthetic", verbose=False, model="full",
+                            max_batch=6, n_ctx=512, n_predict=253, ignore_eos=True)
+    try:
+        audio = synth_audio(300 * SR, 4000)
+        res = api.transcribe(audio, segment_size=60.0, overlap=4.0, temperature=0.0, verbose=False)
+        wins = octc.segments_info(300.0, 60.0, 4.0)
+        assert wins == [(0.0, 60.0), (56.0, 116.0), (112.0, 172.0), (168.0, 228.0), (224.0, 284.0), (280.0, 300.0)]
+        chunks = [audio[int(s * SR):int(e * SR)] for s, e in wins]
+        per = api.transcribe_batch(chunks, temperature=0.0)
+        assert [d.n_gen for d in per] == [253] * 6
+        seg_results = [{"text": d.text, "segments": d.aligned or []} for d in per]
+        text, segs = octc.merge_results(seg_results, [s for s, _ in wins], 4.0)
+        assert res.text == text and len(text) > 0
+        assert [(c["char"], round(c["start"], 6)) for c in res.segments] == \
+               [(c["char"], round(c["start"], 6)) for c in segs]
+        out = api.models.engine.encode(chunks, want_enc=True)
+        for b, c in enumerate(chunks):
+            r = cenc.encode(c)
+            _check_encoder(out["enc"][b], out["audio_embd"][b], out["ctc_ids"][b], r["enc"], r["audio_embd"],
+                           r["ctc_ids"], r["ctc_margin"], f"segment {b}")
+    finally:
+        api.cleanup()
