@@ -26,7 +26,8 @@ int main(int argc, char** argv) {
   const bool arena = argc > 1 && !strcmp(argv[1], "arena");
   // "mall": layers reuse 6 distinct weight sets (~100 MB < 256 MB Infinity Cache): the step reads MALL-resident
   // weights (what a run-ahead prefetcher could at best achieve)
-  const int n_distinct = (argc > 1 && !strcmp(argv[1], "mall")) ? 6 : 28;
+  // "l2": every layer reuses ONE weight set (16.7 MB, 2.1 MB per XCD L2): the upper bound of an L2 prefetcher
+  const int n_distinct = (argc > 1 && !strcmp(argv[1], "mall")) ? 6 : (argc > 1 && !strcmp(argv[1], "l2")) ? 1 : 28;
   char* arena_p = nullptr; size_t arena_off = 0;
   if (arena) CK(hipMalloc(&arena_p, (size_t)700 << 20));
   auto take = [&](size_t bytes) -> void* {
