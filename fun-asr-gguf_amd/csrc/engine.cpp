@@ -1020,6 +1020,16 @@ int fa_get_tensor_q8_0(fa_engine* h, const char* name, uint8_t* out, int64_t n_b
   FA_API_END
 }
 
+int fa_get_tensor_f32(fa_engine* h, const char* name, float* out, int64_t n) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  fa::Slot& s = e->slot(name);
+  FA_REQUIRE(s.kind == 0 && n == s.n, "fa_get_tensor_f32: size/kind");
+  FA_HIP(hipMemcpyAsync(out, s.f, n * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
 int fa_load_gguf(fa_engine* h, const char* path) {
   FA_API_BEGIN
   Engine* e = h->e;

@@ -43,5 +43,6 @@ struct GGUFFile {
 
 const char* gguf_error();
 float half_to_float_host(uint16_t h);
+uint16_t float_to_half_host(float f);  // IEEE binary16, round to nearest even
 
 }  // namespace fa

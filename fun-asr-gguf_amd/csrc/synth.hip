@@ -20,13 +20,16 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
 }
 
 __global__ void k_synth_fill(float* __restrict__ out, int64_t n, uint32_t key, float scale, float offset) {
+  // two IEEE roundings: hipcc fused fl(u * scale) + offset into one fma (the ocml bodies of __fmul_rn / __fadd_rn
+  // carry the contract flag), which made ~2% of the offset-1 norm weights differ by 1 ulp from the spec
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) {
     uint32_t h = lowbias32((uint32_t)i ^ key);
     float u = __fsub_rn(__fmul_rn(__fmul_rn((float)(h >> 8), 5.9604644775390625e-08f), 2.0f), 1.0f);
-    float w = __fmul_rn(u, scale);
-    if (offset != 0.0f) w = __fadd_rn(w, offset);
+    float w = u * scale;
+    asm volatile("" : "+v"(w));  // an opaque hop: the product is rounded before the add (no fma)
+    if (offset != 0.0f) w = w + offset;
     out[i] = w;
   }
 }

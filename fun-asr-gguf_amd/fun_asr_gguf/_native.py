@@ -17,6 +17,7 @@ EXPORTS = [
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
     "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
+    "fa_get_tensor_f32", "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
 ]
 
 
@@ -62,6 +63,7 @@ def load():
     lib.fa_set_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_set_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_get_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_get_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_load_gguf.argtypes = [P, ctypes.c_char_p]
     lib.fa_encode.argtypes = [P, P, P, I32, I64, P, I64, P, I64, P, P, P]
     lib.fa_encode_device.argtypes = [P, P, P, I32, I64]
@@ -81,6 +83,12 @@ def load():
     lib.fa_synchronize.argtypes = [P]
     lib.fa_align_timestamps.argtypes = [P, P, I32, P, I32, P, P]
     lib.fa_pcm_upload.argtypes = [P, P, I64]
+    lib.fa_vocab_load_gguf.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
+    lib.fa_vocab_free.argtypes = [P]
+    lib.fa_vocab_info.argtypes = [P, P, P]
+    lib.fa_tokenize.argtypes = [P, ctypes.c_char_p, I32, I32, P, I32, P]
+    lib.fa_token_piece.argtypes = [P, I32, ctypes.c_char_p, I32, P]
+    lib.fa_gguf_read_tensor.argtypes = [ctypes.c_char_p, ctypes.c_char_p, I32, P, I64]
     _lib = lib
     return lib
 
@@ -148,6 +156,11 @@ class Engine:
     def get_tensor_q8_0(self, name, n_elements):
         out = np.empty(n_elements // 32 * 34, np.uint8)
         _check(self.lib.fa_get_tensor_q8_0(self.h, name.encode(), _ptr(out), out.size), "fa_get_tensor_q8_0")
+        return out
+
+    def get_tensor_f32(self, name, n_elements):
+        out = np.empty(n_elements, np.float32)
+        _check(self.lib.fa_get_tensor_f32(self.h, name.encode(), _ptr(out), out.size), "fa_get_tensor_f32")
         return out
 
     def load_gguf(self, path):
@@ -280,3 +293,56 @@ class Engine:
 
     def synchronize(self):
         _check(self.lib.fa_synchronize(self.h), "fa_synchronize")
+
+
+class Vocab:
+    """Native GGUF tokenizer (fa_vocab): llama_tokenize(add_special=False, parse_special=True) and
+    llama_token_to_piece(special=True) of the reference (llama.py:738-748)."""
+
+    def __init__(self, gguf_path):
+        lib = load()
+        h = ctypes.c_void_p()
+        _check(lib.fa_vocab_load_gguf(os.fspath(gguf_path).encode(), ctypes.byref(h)), "fa_vocab_load_gguf")
+        self.h, self.lib = h, lib
+        n, eos = ctypes.c_int32(), ctypes.c_int32()
+        _check(lib.fa_vocab_info(h, ctypes.byref(n), ctypes.byref(eos)), "fa_vocab_info")
+        self.n_vocab, self.eos = n.value, eos.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fa_vocab_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def tokenize(self, text, parse_special=True):
+        b = text.encode("utf-8")
+        cap = len(b) + 32
+        out = np.empty(cap, np.int32)
+        n = ctypes.c_int32()
+        _check(self.lib.fa_tokenize(self.h, b, len(b), 1 if parse_special else 0, _ptr(out), cap, ctypes.byref(n)),
+               "fa_tokenize")
+        return [int(t) for t in out[:n.value]]
+
+    def token_to_bytes(self, tid):
+        buf = ctypes.create_string_buffer(256)
+        n = ctypes.c_int32()
+        rc = self.lib.fa_token_piece(self.h, int(tid), buf, 256, ctypes.byref(n))
+        if rc != 0 and n.value > 256:
+            buf = ctypes.create_string_buffer(n.value)
+            rc = self.lib.fa_token_piece(self.h, int(tid), buf, n.value, ctypes.byref(n))
+        _check(rc, "fa_token_piece")
+        return buf.raw[:n.value]
+
+
+def gguf_read_tensor(path, name, n_elements, fp16_product=False):
+    """Dequantised GGUF tensor (q8_0 / f16 / f32) as f32 (get_token_embeddings_gguf, llama.py:751-796)."""
+    lib = load()
+    out = np.empty(n_elements, np.float32)
+    _check(lib.fa_gguf_read_tensor(os.fspath(path).encode(), name.encode(), 1 if fp16_product else 0, _ptr(out),
+                                   n_elements), "fa_gguf_read_tensor")
+    return out

@@ -2,9 +2,10 @@
 
 Creates the device-bound native engine and fills its weights:
   * "synthetic" (or a missing path) -> the repo's deterministic synthetic weights (oracle/synth.py spec);
-  * encoder/CTC: a PyTorch/safetensors state dict (model.pt keys audio_encoder.*, audio_adaptor.*,
-    ctc_decoder.*, ctc.ctc_lo.* -> ctc_proj.ctc_lo.*, as HybridSenseVoice.load_weights,
-    model_definition.py:231-238), loaded with weights_only=True;
+  * encoder/CTC: the reference's ONNX files (fun_asr_gguf.onnx_weights: initializers of
+    Fun-ASR-Nano-Encoder-Adaptor.*.onnx and Fun-ASR-Nano-CTC.*.onnx), or a PyTorch/safetensors state dict
+    (model.pt keys audio_encoder.*, audio_adaptor.*, ctc_decoder.*, ctc.ctc_lo.* -> ctc_proj.ctc_lo.*, as
+    HybridSenseVoice.load_weights, model_definition.py:231-238), loaded with weights_only=True;
   * decoder: a GGUF file (q8_0/f16/f32 tensors + tokenizer metadata) through fa_load_gguf.
 Any failure returns False (the reference swallows init exceptions the same way, :98-100).
 """
@@ -48,6 +49,17 @@ def load_encoder_state_dict(engine, path):
     return n
 
 
+def load_encoder_onnx(engine, path):
+    """Initializers of an encoder-adaptor or CTC ONNX file (onnx_weights.state_dict_from_onnx) -> engine tensors."""
+    from ..onnx_weights import state_dict_from_onnx
+    sd = state_dict_from_onnx(path)
+    if not sd:
+        raise ValueError(f"{path}: no encoder / adaptor / CTC initializers found")
+    for k, v in sd.items():
+        engine.set_tensor(k, v)
+    return len(sd)
+
+
 class ModelManager:
     def __init__(self, config):
         self.config = config
@@ -80,13 +92,18 @@ class ModelManager:
                                          max_samples=c.sample_rate * 64, device=c.device)
             self.engine.synthetic_weights(c.synthetic_seed)
             self.engine.set_encoder_fp16(c.encoder_fp16())
-            if not _is_synthetic(c.encoder_onnx_path):
-                if str(c.encoder_onnx_path).endswith(".onnx"):
-                    raise NotImplementedError("ONNX initializer ingestion is not implemented; pass model.pt")
-                load_encoder_state_dict(self.engine, c.encoder_onnx_path)
+            # encoder/adaptor + CTC weights: the reference's ONNX files (initializers read without `onnx`), or a
+            # model.pt / safetensors state dict (HybridSenseVoice.load_weights, model_definition.py:231-238)
+            for p in (c.encoder_onnx_path, getattr(c, "ctc_onnx_path", None)):
+                if _is_synthetic(p) or not os.path.exists(str(p)):
+                    continue
+                if str(p).endswith(".onnx"):
+                    load_encoder_onnx(self.engine, p)
+                else:
+                    load_encoder_state_dict(self.engine, p)
             if gguf_kv is not None:
                 self.engine.load_gguf(c.decoder_gguf_path)
-                self.vocab = GGUFVocab(kv=gguf_kv)
+                self.vocab = GGUFVocab(c.decoder_gguf_path)
             else:
                 self.vocab = SyntheticVocab(self.llm_cfg["n_vocab"])
             self.eos_token = self.vocab.eos

@@ -2,34 +2,13 @@
 (llama.py:738-748 text_to_tokens(add_special=False, parse_special=True), token_to_bytes(special=True);
 ASRStreamDecoder incremental UTF-8 decode llama.py:661-690).
 
-GGUFVocab   byte-level BPE read from GGUF metadata (tokenizer.ggml.tokens/merges/token_type, the
-            layout convert_hf_to_gguf.py writes for Qwen, :1283-1291) with the Qwen2 pre-tokenizer split.
+GGUFVocab   byte-level BPE from GGUF metadata (tokenizer.ggml.tokens/merges/token_type, the layout
+            convert_hf_to_gguf.py writes for Qwen, :1283-1291) with the Qwen2 pre-tokenizer split, run by the
+            native tokenizer (csrc/vocab.cpp).
 SyntheticVocab  deterministic stand-in used with synthetic weights (no tokenizer ships in the reference):
             one token per character, Qwen special-token strings mapped to the top ids.
 """
 import struct
-
-try:
-    import regex as _re
-except ImportError:  # pragma: no cover
-    _re = None
-
-QWEN2_PRETOKENIZE = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*"
-                     r"|\s*[\r\n]+|\s+(?!\S)|\s+")
-TOKEN_TYPE_NORMAL, TOKEN_TYPE_CONTROL, TOKEN_TYPE_USER_DEFINED = 1, 3, 4
-
-
-def bytes_to_unicode():
-    """GPT-2 byte <-> printable-unicode table used by byte-level BPE vocabularies."""
-    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
-    cs = bs[:]
-    n = 0
-    for b in range(256):
-        if b not in bs:
-            bs.append(b)
-            cs.append(256 + n)
-            n += 1
-    return dict(zip(bs, (chr(c) for c in cs)))
 
 
 def read_gguf_metadata(path):
@@ -64,80 +43,20 @@ def read_gguf_metadata(path):
 
 
 class GGUFVocab:
-    def __init__(self, path=None, kv=None):
-        kv = kv if kv is not None else read_gguf_metadata(path)
-        self.tokens = kv["tokenizer.ggml.tokens"]
-        self.types = kv.get("tokenizer.ggml.token_type", [TOKEN_TYPE_NORMAL] * len(self.tokens))
-        merges = kv.get("tokenizer.ggml.merges", [])
-        self.ranks = {tuple(m.split(" ", 1)): i for i, m in enumerate(merges)}
-        self.tok2id = {t: i for i, t in enumerate(self.tokens)}
-        self.eos = int(kv.get("tokenizer.ggml.eos_token_id", -1))
-        self.n_vocab = len(self.tokens)
-        self.b2u = bytes_to_unicode()
-        self.u2b = {v: k for k, v in self.b2u.items()}
-        self.special = sorted((t for t, ty in zip(self.tokens, self.types)
-                               if ty in (TOKEN_TYPE_CONTROL, TOKEN_TYPE_USER_DEFINED)), key=len, reverse=True)
-        self._pat = _re.compile(QWEN2_PRETOKENIZE) if _re is not None else None
-        self._cache = {}
+    """The GGUF's tokenizer, run natively (fa_tokenize / fa_token_piece in libfunasr_hip.so): the llama_tokenize /
+    llama_token_to_piece surface of the reference. The pure-Python restatement is oracle/bpe.py (test only)."""
 
-    def _bpe(self, word):
-        if word in self._cache:
-            return self._cache[word]
-        parts = list(word)
-        while len(parts) > 1:
-            best, bi = None, -1
-            for i in range(len(parts) - 1):
-                r = self.ranks.get((parts[i], parts[i + 1]))
-                if r is not None and (best is None or r < best):
-                    best, bi = r, i
-            if best is None:
-                break
-            parts[bi:bi + 2] = [parts[bi] + parts[bi + 1]]
-        ids = []
-        for p in parts:
-            if p in self.tok2id:
-                ids.append(self.tok2id[p])
-            else:  # unknown merge result: fall back to single byte symbols
-                ids.extend(self.tok2id[c] for c in p if c in self.tok2id)
-        self._cache[word] = ids
-        return ids
-
-    def _encode_plain(self, text):
-        if self._pat is None:
-            raise RuntimeError("the 'regex' module is required for BPE pre-tokenisation")
-        out = []
-        for w in self._pat.findall(text):
-            out.extend(self._bpe("".join(self.b2u[b] for b in w.encode("utf-8"))))
-        return out
+    def __init__(self, path):
+        from ._native import Vocab
+        self._v = Vocab(path)
+        self.n_vocab = self._v.n_vocab
+        self.eos = self._v.eos
 
     def tokenize(self, text, parse_special=True):
-        if not parse_special or not self.special:
-            return self._encode_plain(text)
-        out, i = [], 0
-        while i < len(text):
-            hit = None
-            for s in self.special:
-                if text.startswith(s, i):
-                    hit = s
-                    break
-            if hit is not None:
-                out.append(self.tok2id[hit])
-                i += len(hit)
-                continue
-            j = i + 1
-            while j < len(text) and not any(text.startswith(s, j) for s in self.special):
-                j += 1
-            out.extend(self._encode_plain(text[i:j]))
-            i = j
-        return out
+        return self._v.tokenize(text, parse_special)
 
     def token_to_bytes(self, tid):
-        if tid < 0 or tid >= self.n_vocab:
-            return b""
-        t = self.tokens[tid]
-        if self.types[tid] in (TOKEN_TYPE_CONTROL, TOKEN_TYPE_USER_DEFINED):
-            return t.encode("utf-8")
-        return bytes(self.u2b[c] for c in t if c in self.u2b)
+        return self._v.token_to_bytes(tid)
 
 
 class SyntheticVocab:

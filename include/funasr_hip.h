@@ -75,6 +75,8 @@ int fa_set_tensor_q8_0(fa_engine* e, const char* name, const uint8_t* blocks, in
 int fa_load_gguf(fa_engine* e, const char* path);
 /* Copy a decoder tensor back as ggml q8_0 blocks (test hook). */
 int fa_get_tensor_q8_0(fa_engine* e, const char* name, uint8_t* out, int64_t n_bytes);
+/* Copy an f32 tensor (encoder / norm weights) back (test hook). */
+int fa_get_tensor_f32(fa_engine* e, const char* name, float* out, int64_t n);
 
 /* ---- encoder operator (replaces encoder_sess.run_with_ort_values + ctc_sess.run)
  * pcm: batch clips, clip b at pcm + b*stride with n_samples[b] valid samples (16 kHz f32).
@@ -128,6 +130,24 @@ int fa_llm_generate(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n
 int fa_llm_logits(fa_engine* e, int32_t seq, float* out);
 /* Current length (n_past) of a sequence slot. */
 int fa_llm_n_past(fa_engine* e, int32_t seq, int32_t* out);
+
+/* ---- tokenizer / detokenizer from GGUF metadata (replaces llama_model_get_vocab + llama_tokenize +
+ * llama_token_to_piece, llama.py:738-748; used by PromptBuilder.build_prompt prompt_utils.py:44-52 and the
+ * streamed output ASRStreamDecoder.push llama.py:671-683). Byte-level BPE with the Qwen2 pre-tokenizer
+ * (tokenizer.ggml.pre "qwen2"); control / user-defined tokens are matched in the text when parse_special != 0.
+ * Pure host code (no device). */
+typedef struct fa_vocab fa_vocab;
+int fa_vocab_load_gguf(const char* path, fa_vocab** out);
+int fa_vocab_free(fa_vocab* v);
+int fa_vocab_info(const fa_vocab* v, int32_t* n_tokens, int32_t* eos_id);
+/* text: UTF-8 bytes (add_special = false). *n_out = number of tokens; FA_ERR_ARG when cap is too small. */
+int fa_tokenize(const fa_vocab* v, const char* text, int32_t n_bytes, int32_t parse_special, int32_t* out,
+                int32_t cap, int32_t* n_out);
+/* raw bytes of one token (special = true: control tokens render as their text). */
+int fa_token_piece(const fa_vocab* v, int32_t id, char* buf, int32_t cap, int32_t* n_out);
+/* One GGUF tensor (q8_0 / f16 / f32) dequantised to f32 [n]; fp16_product = 1 reproduces the numpy-f16
+ * product of get_token_embeddings_gguf (llama.py:778-784), 0 = ggml dequantize_row_q8_0. */
+int fa_gguf_read_tensor(const char* path, const char* name, int32_t fp16_product, float* out, int64_t n);
 
 /* ---- host-side char alignment (replaces nano_ctc.align_timestamps, nano_ctc.py:118-232)
  * ctc_keys/llm_keys: per-char integer keys (equal iff the chars' .lower() strings are equal);

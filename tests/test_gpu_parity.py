@@ -49,6 +49,16 @@ def llm_tiny_oracle():
     return oqw.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=512)
 
 
+def test_synthetic_f32_weights_bit_exact(tiny_engine, enc_w_tiny):
+    """Device hash of every f32 encoder / norm tensor == the numpy spec (oracle/synth.py), bit for bit (two IEEE
+    roundings for the offset-1 LayerNorm weights: no fused multiply-add)."""
+    for name, w in enc_w_tiny.items():
+        assert (tiny_engine.get_tensor_f32(name, w.size) == w.ravel()).all(), name
+    for name, shape, scale, off in synth.llm_tensors(synth.LLM_TINY):
+        if len(shape) == 1 and name.startswith(("blk.1.", "output_norm")):
+            assert (tiny_engine.get_tensor_f32(name, shape[0]) == synth.gen(name, shape[0], scale, off, 0)).all(), name
+
+
 def test_synthetic_q8_weights_bit_exact(tiny_engine):
     """Device hash + device ggml quantiser == numpy hash + reference quantiser, byte for byte."""
     cfg = synth.LLM_TINY
