@@ -35,10 +35,15 @@ class FunASREngine:
                                             top_k=top_k, ranks=ranks)
 
     def transcribe_batch(self, clips: List, language=None, context=None, temperature: float = 0.4, top_p=1.0,
-                         top_k=50) -> List[DecodeResult]:
-        """Many independent clips (each <= segment_size + 2 s) as encoder batches + one decoder batch."""
+                         top_k=50, ranks=None) -> Optional[List[DecodeResult]]:
+        """Many independent clips (each <= segment_size + 2 s) as encoder batches + one decoder batch.
+        ranks (an initialised torch.distributed): the clips are assigned longest-first across the ranks, every rank
+        decodes its share, results are gathered to rank 0 (the list there, None on the other ranks)."""
         from .audio import load_audio
         pcm = [load_audio(c, self.sample_rate) for c in clips]
+        if ranks is not None:
+            from .parallel import sharded_decode
+            return sharded_decode(self.orchestrator, pcm, language, context, False, temperature, top_p, top_k, ranks)
         return self.orchestrator.decode_segments(pcm, language, context, False, temperature, top_p, top_k)
 
     def create_stream(self, hotwords: Optional[str] = None) -> RecognitionStream:

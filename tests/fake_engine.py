@@ -1,0 +1,93 @@
+"""Host stand-in for fun_asr_gguf._native.Engine (no GPU): the surface StreamDecoder / TranscriptionOrchestrator use
+(encode, ctc_collapse, embd_rows, llm_reset / llm_prefill / llm_generate), deterministic in each clip's own samples
+and independent of how clips are batched, so a sharded run must equal a single-rank run exactly. Lets the real
+orchestration code (windows, LPT sharding, record gather, merge) run in multi-process CPU tests."""
+import numpy as np
+
+from fun_asr_gguf.core.model_manager import ModelManager
+from fun_asr_gguf.nano_dataclass import ASREngineConfig
+from fun_asr_gguf.prompt_utils import PromptBuilder
+from fun_asr_gguf.vocab import CTCSyntheticTokens, SyntheticVocab
+
+N_VOCAB, CTC_VOCAB = 4096, 3001
+
+
+def _frames(n):
+    return ((max(n, 16000) // 160 + 1) + 5) // 6
+
+
+class FakeEngine:
+    def __init__(self):
+        self.last = []
+        self.seqs = {}
+
+    def encode(self, clips, want_enc=False, resident=None):
+        self.last = [np.asarray(c, np.float32) for c in clips]
+        out = dict(audio_embd=[], ctc_ids=[])
+        for c in self.last:
+            T = _frames(len(c))
+            frames = np.resize(c, T * 160)[: T * 160].reshape(T, 160)
+            key = (np.abs(frames).sum(1) * 1e4).astype(np.int64)
+            ids = np.where(key % 3 == 0, CTC_VOCAB - 1, key % 50).astype(np.int32)  # blanks + 50 symbols
+            tgt = max(1, T // 8)
+            out["audio_embd"].append(np.full((tgt, 1024), float(key.sum() % 97) / 97, np.float32))
+            out["ctc_ids"].append(ids)
+        return out
+
+    def ctc_collapse(self, blank, B):
+        res = []
+        for c in self.last[:B]:
+            ids = self.encode_ids(c)
+            keep = [(int(t), i) for i, t in enumerate(ids) if t != blank and (i == 0 or t != ids[i - 1])]
+            res.append((np.array([k for k, _ in keep], np.int32), np.array([f for _, f in keep], np.int32)))
+        return res
+
+    def encode_ids(self, c):
+        T = _frames(len(c))
+        frames = np.resize(c, T * 160)[: T * 160].reshape(T, 160)
+        key = (np.abs(frames).sum(1) * 1e4).astype(np.int64)
+        return np.where(key % 3 == 0, CTC_VOCAB - 1, key % 50)
+
+    def embd_rows(self, ids, fp16_round=True):
+        return np.repeat(np.asarray(ids, np.float32)[:, None] / N_VOCAB, 1024, 1)
+
+    def llm_reset(self, s):
+        self.seqs.pop(s, None)
+
+    def llm_prefill(self, s, embd, **samp):
+        h = int(np.abs(embd).sum() * 1000) % 100003
+        self.seqs[s] = h
+        return 1000 + h % 20
+
+    def llm_generate(self, seqs, n, **samp):
+        out = np.zeros((len(seqs), n), np.int32)
+        for r, s in enumerate(seqs):
+            for k in range(n):
+                self.seqs[s] = (self.seqs[s] * 1103515245 + 12345) % 2147483647
+                out[r, k] = 1000 + self.seqs[s] % 40
+        return out
+
+
+def fake_models(max_batch=4, n_predict=24):
+    cfg = ASREngineConfig(encoder_onnx_path="synthetic", ctc_onnx_path="synthetic", decoder_gguf_path="synthetic",
+                          tokens_path="synthetic", n_predict=n_predict, max_batch=max_batch, ignore_eos=True)
+    m = ModelManager(cfg)
+    m.engine = FakeEngine()
+    m.vocab = SyntheticVocab(N_VOCAB)
+    m.eos_token = m.vocab.eos
+    m.ctc_id2token = CTCSyntheticTokens(CTC_VOCAB)
+    m.prompt_builder = PromptBuilder(m.vocab, m.engine)
+    m._initialized = True
+    return m
+
+
+def fake_api(max_batch=4, n_predict=24):
+    from fun_asr_gguf import FunASREngine
+    api = FunASREngine("synthetic", "synthetic", "synthetic", "synthetic", n_predict=n_predict, max_batch=max_batch,
+                       ignore_eos=True)
+    m = fake_models(max_batch, n_predict)
+    api.models = m
+    api.orchestrator.models = m
+    api.orchestrator.decoder.models = m
+    api.orchestrator.decoder.llm_decoder.models = m
+    return api

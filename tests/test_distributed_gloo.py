@@ -58,3 +58,52 @@ def test_gather_world2_equals_single():
         assert p.exitcode == 0
     single = [from_record(to_record(d)) for d in _StubOrch().decode_segments([[0.0] * n for n in (960, 960, 960, 960, 960, 320)])]
     assert got == [(r.text, r.aligned, [(t.text, t.start) for t in r.ctc_results]) for r in single]
+
+
+def _api_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "fun-asr-gguf_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fake_engine import fake_api
+    from fun_asr_gguf.synthetic import synth_audio
+    api = fake_api(max_batch=2)
+    audio = synth_audio(16000 * 300, 4000)
+    res = api.transcribe(audio, segment_size=60.0, overlap=4.0, temperature=0.0, verbose=False, ranks=dist)
+    clips = [synth_audio(16000 * s, 100 + i) for i, s in enumerate((60, 12, 45, 60, 3, 33, 59))]
+    batch = api.transcribe_batch(clips, temperature=0.0, ranks=dist)
+    if rank == 0:
+        q.put((res.text, res.segments, res.ctc_text, [(d.text, d.aligned, d.n_gen) for d in batch]))
+    else:
+        assert batch is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_transcribe_and_batch_sharded_world2_through_real_orchestrator():
+    """The real TranscriptionOrchestrator / StreamDecoder / merge on a host fake engine (tests/fake_engine.py):
+    C4-style 300 s file (6 segments, LPT over 2 ranks + gather_object + merge on rank 0) and a 7-clip
+    transcribe_batch(ranks=) both equal the single-rank run exactly."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "tests")]
+    from fake_engine import fake_api
+    from fun_asr_gguf.synthetic import synth_audio
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_api_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    api = fake_api(max_batch=2)
+    audio = synth_audio(16000 * 300, 4000)
+    res = api.transcribe(audio, segment_size=60.0, overlap=4.0, temperature=0.0, verbose=False)
+    clips = [synth_audio(16000 * s, 100 + i) for i, s in enumerate((60, 12, 45, 60, 3, 33, 59))]
+    batch = api.transcribe_batch(clips, temperature=0.0)
+    assert res.text and len(res.segments) > 0
+    assert got == (res.text, res.segments, res.ctc_text, [(d.text, d.aligned, d.n_gen) for d in batch])
