@@ -86,3 +86,35 @@ extern "C" int fa_align_timestamps(const int32_t* ctc_keys, const double* ctc_st
   }
   return FA_OK;
 }
+
+// FastRAG coarse retrieval distance (/root/reference/fun_asr_gguf/hotword/rag_fast.py:35-77, the numba kernel):
+// minimum over end positions j >= 1 of the edit distance between the hotword's phoneme codes (sub) and a
+// substring of the input's codes (main) ending at j, free start (dp[0][j] = 0), unit insert / delete / substitute.
+// Float32 DP as in the reference (all values are small integers: exact).
+extern "C" int fa_fuzzy_substring_distance(const int32_t* main_codes, int32_t m, const int32_t* sub_codes, int32_t n,
+                                           float* dist_out) {
+  if (!dist_out || m < 0 || n < 0) return FA_ERR_ARG;
+  if (n == 0 || m == 0) {
+    *dist_out = (float)n;
+    return FA_OK;
+  }
+  if (!main_codes || !sub_codes) return FA_ERR_ARG;
+  std::vector<float> prev(m + 1, 0.f), cur(m + 1);
+  for (int i = 1; i <= n; ++i) {
+    cur[0] = (float)i;
+    const int32_t s = sub_codes[i - 1];
+    for (int j = 1; j <= m; ++j) {
+      const float cost = s == main_codes[j - 1] ? 0.f : 1.f;
+      float v = prev[j] + 1.f;
+      if (cur[j - 1] + 1.f < v) v = cur[j - 1] + 1.f;
+      if (prev[j - 1] + cost < v) v = prev[j - 1] + cost;
+      cur[j] = v;
+    }
+    prev.swap(cur);
+  }
+  float best = prev[1];
+  for (int j = 2; j <= m; ++j)
+    if (prev[j] < best) best = prev[j];
+  *dist_out = best;
+  return FA_OK;
+}

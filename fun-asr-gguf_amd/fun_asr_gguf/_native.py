@@ -17,7 +17,7 @@ EXPORTS = [
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
     "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
-    "fa_get_tensor_f32", "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
+    "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
 ]
 
 
@@ -89,6 +89,7 @@ def load():
     lib.fa_tokenize.argtypes = [P, ctypes.c_char_p, I32, I32, P, I32, P]
     lib.fa_token_piece.argtypes = [P, I32, ctypes.c_char_p, I32, P]
     lib.fa_gguf_read_tensor.argtypes = [ctypes.c_char_p, ctypes.c_char_p, I32, P, I64]
+    lib.fa_fuzzy_substring_distance.argtypes = [P, I32, P, I32, P]
     _lib = lib
     return lib
 
@@ -346,3 +347,14 @@ def gguf_read_tensor(path, name, n_elements, fp16_product=False):
     _check(lib.fa_gguf_read_tensor(os.fspath(path).encode(), name.encode(), 1 if fp16_product else 0, _ptr(out),
                                    n_elements), "fa_gguf_read_tensor")
     return out
+
+
+def fuzzy_substring_distance(main_codes, sub_codes):
+    """FastRAG coarse distance (rag_fast.py:35-77) on int32 phoneme codes."""
+    lib = load()
+    a = np.ascontiguousarray(main_codes, np.int32)
+    b = np.ascontiguousarray(sub_codes, np.int32)
+    d = ctypes.c_float()
+    _check(lib.fa_fuzzy_substring_distance(_ptr(a), a.size, _ptr(b), b.size, ctypes.byref(d)),
+           "fa_fuzzy_substring_distance")
+    return d.value

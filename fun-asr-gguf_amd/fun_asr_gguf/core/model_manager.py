@@ -69,6 +69,7 @@ class ModelManager:
         self.ctc_id2token = None
         self.prompt_builder = None
         self.hotwords = []
+        self.hotword_source = None
         self.enc_cfg = None
         self.llm_cfg = None
         self._initialized = False
@@ -113,8 +114,10 @@ class ModelManager:
                 self.ctc_id2token = load_ctc_tokens(c.tokens_path)
             self.prompt_builder = PromptBuilder(self.vocab, self.engine)
             if c.hotwords_path and os.path.exists(c.hotwords_path):
-                with open(c.hotwords_path, encoding="utf-8") as f:
-                    self.hotwords = [ln.strip() for ln in f if ln.strip() and not ln.startswith("#")]
+                # phoneme hotword retrieval (hotword/manager.py + hot_phoneme.py), reloaded when hot.txt changes
+                from ..hotword import HotwordSource
+                self.hotword_source = HotwordSource(c.hotwords_path, c.similar_threshold)
+                self.hotwords = list(self.hotword_source.corrector.hotwords)
             self._initialized = True
             if verbose:
                 print(f"✓ 模型加载完成 (耗时: {time.perf_counter() - t0:.2f}s)")
@@ -126,10 +129,11 @@ class ModelManager:
             return False
 
     def match_hotwords(self, ctc_text, k):
-        """Hotwords that occur verbatim in the CTC text (phoneme retrieval is out of scope)."""
-        if not ctc_text or not self.hotwords:
+        """CTCDecoder.decode's hotword step (decoder.py:39-44): PhonemeCorrector.correct(ctc_text, k) -> the
+        hotwords of its matches and similars (fun_asr_gguf.hotword)."""
+        if self.hotword_source is None or not ctc_text:
             return []
-        return [h for h in self.hotwords if h in ctc_text][:k]
+        return self.hotword_source.hotwords_for(ctc_text, k)
 
     def cleanup(self):
         if self.engine is not None:

@@ -157,6 +157,12 @@ int fa_gguf_read_tensor(const char* path, const char* name, int32_t fp16_product
 int fa_align_timestamps(const int32_t* ctc_keys, const double* ctc_starts, int32_t n_ctc, const int32_t* llm_keys,
                         int32_t n_llm, double* starts_out, int32_t* aligned_out);
 
+/* ---- hotword retrieval (host): the FastRAG coarse distance of rag_fast.py:35-77 (numba in the reference):
+ * min over end positions of the edit distance between sub_codes [n] and a substring of main_codes [m] (free
+ * start). *dist_out = n when either is empty. */
+int fa_fuzzy_substring_distance(const int32_t* main_codes, int32_t m, const int32_t* sub_codes, int32_t n,
+                                float* dist_out);
+
 /* ---- timing hooks for bench.py roofline (HIP events on the engine's stream) */
 /* Enable per-kernel-class event timing; fa_profile_read returns accumulated ms and launch counts for
  * class ids: 0 q8 GEMV/GEMM of the decoder layers, 1 f32 GEMM (encoder), 2 encoder attention,
