@@ -138,6 +138,8 @@ struct Engine {
   std::vector<int> n_past, last_tok;
   std::vector<int> logits_row;  // per sequence: its row of `logits` in the most recent forward (-1: none)
   AttnWork attn_wk;
+  FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
+  bool use_fused = true;   // FUNASR_FUSED_DECODE=0: the 5-launch layer at M = 1 too (A/B)
   AttnF32Work enc_attn_wk;
   GemmF32Work enc_gemm_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
@@ -580,6 +582,14 @@ struct Engine {
     attn_wk.counters = alloc<int>((size_t)m_max * KV * CNT_LINE);
     FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * CNT_LINE * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
+    fdw.opart = alloc<float>((size_t)FUSED_PARTS * E);
+    fdw.dpart = alloc<float>((size_t)FUSED_PARTS * E);
+    fdw.act = alloc<float>(lc.n_ff);
+    fdw.xmid = alloc<float>(E);
+    fdw.cnt = alloc<unsigned>((size_t)2 * FUSED_PARTS * CNT_LINE);
+    fdw.err = alloc<int>(1);
+    FA_HIP(hipMemset(fdw.cnt, 0, (size_t)2 * FUSED_PARTS * CNT_LINE * sizeof(unsigned)));
+    FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
     // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)
     gk_cnt_n = 1024;                             // tiles of a split-K launch
     gk_part_n = (int64_t)1024 * 2 * 1024;        // tiles x splits x (1 or 2 matrices) x 32 x 32 partial floats
@@ -762,6 +772,10 @@ struct Engine {
     const int QKV = (H + 2 * KV) * D;
     const bool small = gemv_small(M);
     (void)max_pos;
+    if (decode && M == 1 && use_fused && fused_shape_ok()) {
+      llm_forward_fused();
+      return;
+    }
     for (int l = 0; l < lc.n_layer; ++l) {
       const LlmLayerW& w = layers[l];
       prof_sample = l == 0;  // sampled timing: layer 0's launches stand for every layer (identical shapes)
@@ -826,6 +840,66 @@ struct Engine {
     if (gemv_small(n_rows)) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
     gemv(h, E, 3);
+  }
+
+  bool fused_shape_ok() const {
+    return lc.n_embd == 1024 && lc.n_ff == 3072 && lc.n_head == 16 && lc.n_head_kv == 8 && lc.head_dim == 128;
+  }
+
+  // batch-1 decode step through the fused layer (llm.hip "Fused batch-1 decode layer"): per layer
+  //   A  q|k|v GEMV, prologue x = x_mid + sum dpart (layer > 0; block 0 stores x to lx)
+  //   B  attention + this split's slice of the o projection -> opart
+  //   C  x_mid = lx + sum opart; gate|up + SwiGLU; group fan-in; slice of the down projection -> dpart
+  // then the LM head with the same partial-sum prologue.
+  void llm_forward_fused() {
+    const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
+    const int QKV = (H + 2 * KV) * D;
+    for (int l = 0; l < lc.n_layer; ++l) {
+      const LlmLayerW& w = layers[l];
+      prof_sample = l == 0;
+      __half* kc = kcache + (size_t)l * layer_stride;
+      __half* vc = vcache + (size_t)l * layer_stride;
+      GemvArgs a{};
+      a.M = 1;
+      a.eps = lc.rms_eps;
+      a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
+      a.out = lqkv; a.ldo = QKV; a.ldx = E; a.norm_w = w.attn_norm;
+      if (l == 0) a.x = lx;
+      else { a.x = fdw.xmid; a.psum = fdw.dpart; a.xsum = lx; }
+      gemv(a, E, 0);
+      {
+        hipEvent_t ev;
+        prof_begin(3, &ev);
+        attn_o_fused(lqkv, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
+                     w.o.q, w.o.d, E, attn_wk, fdw, stream);
+        prof_end(3, (double)E * H * D * 34.0 / 32.0, 0);
+      }
+      {
+        hipEvent_t ev;
+        prof_begin(0, &ev);
+        ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream);
+        prof_end(0, 3.0 * F * E * 34.0 / 32.0, 2.0 * 3.0 * F * E);
+      }
+    }
+    prof_sample = true;
+    GemvArgs h{};
+    h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
+    h.rpw = gemv_rows_per_wave(lc.n_vocab);
+    h.out = logits; h.ldo = lc.n_vocab;
+    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, 1);
+    h.x = fdw.xmid; h.ldx = E; h.norm_w = out_norm; h.psum = fdw.dpart;
+    gemv(h, E, 3);
+  }
+
+  // fused-decode fan-in timeouts are reported, never silent (the step's outputs are garbage then)
+  void check_fused_error() {
+    int err = 0;
+    FA_HIP(hipMemcpy(&err, fdw.err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+      FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
+      set_error("fused decode: an in-launch fan-in timed out (a block was not resident?)");
+      throw hip_failure();
+    }
   }
 
   // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
@@ -942,6 +1016,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMV_SMALL")) fa::g_gemv_small_max = std::min(7, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;
     e->build_arenas();
     e->build_constants();
     e->build_encoder();
@@ -1157,6 +1232,18 @@ int fa_set_encoder_fp16(fa_engine* h, int32_t on) {
   FA_API_END
 }
 
+int fa_set_decode_fused(fa_engine* h, int32_t on) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  if (e->use_fused != (on != 0)) {
+    FA_HIP(hipStreamSynchronize(e->stream));
+    for (auto& g : e->step_graphs) FA_HIP(hipGraphExecDestroy(g.second));
+    e->step_graphs.clear();  // captured steps bake the layer structure in
+  }
+  e->use_fused = on != 0;
+  FA_API_END
+}
+
 int fa_set_debug(fa_engine* h, int32_t flags) {
   FA_API_BEGIN
   h->e->debug_flags = flags;
@@ -1262,6 +1349,7 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   FA_HIP(hipMemcpyAsync(hist.data(), e->d_tok_hist, hist.size() * 4, hipMemcpyDeviceToHost, e->stream));
   FA_HIP(hipStreamSynchronize(e->stream));
   e->prof_collect();
+  if (n_seqs == 1) e->check_fused_error();
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
     for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hist[(size_t)i * e->hist_max + st];

@@ -85,6 +85,7 @@ struct GemvArgs {
   float* kpart; int64_t kpart_n;           // MFMA GEMM split-K workspace (floats) + arrival counters
   int* kcnt; int64_t kcnt_n;               //   (counters zeroed once; re-armed by the combining block)
   int8_t* qout; float* dout;               // MFMA GEMM SwiGLU epilogue: also the q8_0 rows of out (next GEMM's input)
+  const float* psum; float* xsum;          // fused decode (M = 1): x += psum[0..7][K] before the norm; block 0 -> xsum
 };
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
@@ -116,6 +117,25 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
                 int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout = nullptr,
                 float* dout = nullptr);
+// Fused batch-1 decode layer (M = 1; llm.hip): attention + split o projection, and gate|up + SwiGLU + split down
+// projection, each with an in-launch group fan-in (see the kernels). FUSED_PARTS = partial vectors summed by the next
+// launch's prologue (8 kv heads for o, 8 groups of 384 act rows for down).
+constexpr int FUSED_PARTS = 8;
+struct FusedDecodeWork {
+  float* opart = nullptr;   // [FUSED_PARTS][E]
+  float* dpart = nullptr;   // [FUSED_PARTS][E]
+  float* act = nullptr;     // [F] act hand-off
+  float* xmid = nullptr;    // [E] residual stream after the attention block
+  unsigned* cnt = nullptr;  // [2 * FUSED_PARTS][CNT_LINE] ticket counters (zeroed once, never re-armed)
+  int* err = nullptr;       // set to 1 by a timed-out fan-in wait
+};
+void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
+                  __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
+                  const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,
+                  hipStream_t s);
+void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
+               const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
+               hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 // Decode-step tail fused into the sampler: embedding row of the sampled token -> x (the next step's input), and

@@ -318,8 +318,11 @@ void gemm_stamps_read(unsigned long long* host, int n) {
 #define KSTAMP(i) do { } while (0)
 #endif
 
-template <int NCH, int MT, bool FUSED, int EPI>
+// PS (fused decode, M = 1, K = 1024): the activation row is first completed as x + psum[0] + ... + psum[7] (the split
+// down projection of the previous fused layer), and block 0 stores that row to a.xsum (the residual stream).
+template <int NCH, int MT, bool FUSED, int EPI, bool PS = false>
 __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
+  static_assert(!PS || (NCH == 1 && MT == 1 && FUSED), "partial-sum prologue: M = 1, K = 1024 only");
   GSTAMP(0);
   constexpr int K = NCH * 1024, NB = K / 32;
   __shared__ int8_t s_q[MT * K];
@@ -339,6 +342,14 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   const bool pro_blk = FUSED && NCH < 3;
   const bool pro_chunk = FUSED && NCH == 3 && !a.norm_w;  // K = 3072, no norm (down projection)
   float xv[MT][NCH < 3 ? PERB : 16], xw[PERB];
+  float pv[PS ? FUSED_PARTS : 1][PS ? PERB : 1];
+  if constexpr (PS) {
+#pragma unroll
+    for (int g = 0; g < FUSED_PARTS; ++g) {
+      const float4 f = *reinterpret_cast<const float4*>(a.psum + g * 1024 + threadIdx.x * PERB);
+      pv[g][0] = f.x; pv[g][1] = f.y; pv[g][2] = f.z; pv[g][3] = f.w;
+    }
+  }
   if constexpr (FUSED && NCH < 3) {
     const float* wr = (a.norm_w ? a.norm_w : a.x) + threadIdx.x * PERB;  // no norm: a valid dummy row, unused
 #pragma unroll
@@ -380,6 +391,17 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   // activations (vmcnt(0)) before the weight stream is even issued
   __builtin_amdgcn_sched_barrier(0);
   // ---- prologue: activation tile -> LDS (int8 q + f32 d)
+  if constexpr (PS) {
+#pragma unroll
+    for (int j = 0; j < PERB; ++j) {
+      float v = xv[0][j];
+#pragma unroll
+      for (int g = 0; g < FUSED_PARTS; ++g) v = v + pv[g][j];
+      xv[0][j] = v;
+    }
+    if (a.xsum && blockIdx.x == 0)
+      *reinterpret_cast<float4*>(a.xsum + threadIdx.x * PERB) = make_float4(xv[0][0], xv[0][1], xv[0][2], xv[0][3]);
+  }
   if (pro_blk) {
     __shared__ float s_red[MT][4];
 #pragma unroll
@@ -442,10 +464,10 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   }
 }
 
-template <int NCH, int MT, bool FUSED, int EPI>
+template <int NCH, int MT, bool FUSED, int EPI, bool PS = false>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   dim3 grid(cdiv(a.O, 4 * a.rpw), cdiv(a.M, MT));
-  hipLaunchKernelGGL((k_gemv_q8<NCH, MT, FUSED, EPI>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_gemv_q8<NCH, MT, FUSED, EPI, PS>), grid, dim3(256), 0, s, a);
 }
 
 template <int MT, bool FUSED, int EPI>
@@ -862,6 +884,12 @@ static void launch_gemv_fused(int K, int epi, const GemvArgs& a, hipStream_t s) 
 
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   const bool fused = a.x != nullptr;
+  if (a.psum) {  // fused decode layer (M = 1): q|k|v (EPI 0) or the LM head (EPI 3) after a split down projection
+    FA_REQUIRE(fused && a.M == 1 && K == 1024 && (epi == 0 || epi == 3), "gemv_q8: partial-sum prologue shape");
+    if (epi == 0) launch_gemv<1, 1, true, 0, true>(a, s);
+    else launch_gemv<1, 1, true, 3, true>(a, s);
+    return;
+  }
   if (gemv_small(a.M) && fused) {
     FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemv_q8: n_part");
     // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens)
@@ -1169,34 +1197,29 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // wait-count pass drain the q loads at the join, before the K/V loads were issued
 // LEAN (batched decode, several blocks per CU): at most 4 groups per wave pass and a 4-partial combine chunk, so
 // the kernel fits 128 VGPRs and 4 blocks share a CU (every block of a batch-32 launch resident at once)
+// The decode / causal attention of one (kv head g, key split sp, token m) block up to the merge of its waves:
+// returns false for a split past the active ones (block-uniform, nothing computed); otherwise wave 0 leaves the
+// split's softmax state in (M, L, o) for lane -> head j = lane >> 5, dims [d0, d0 + 4) (d0 = 4 (lane & 31)).
+// Shared by k_attn_block (partials + last-arriver combine) and k_attn_o (fused decode: every split combines, then
+// multiplies its slice of the o projection).
 template <int DM, int LEAN>
-__global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
-                                                         int nsplit, int decode_mode, int H, int KV,
-                                                         int64_t seq_stride, int64_t head_stride,
-                                                         __half* __restrict__ kc,
-                                                         __half* __restrict__ vc, const float* __restrict__ qsrc,
-                                                         const float* __restrict__ qn, const float* __restrict__ kn,
-                                                         const float* __restrict__ rcos, const float* __restrict__ rsin,
-                                                         float eps, float scale, float* __restrict__ out,
-                                                         int* __restrict__ counters, float* __restrict__ partials,
-                                                         int8_t* __restrict__ qout, float* __restrict__ dout) {
+__device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, int seq, int nsplit, int H, int KV,
+                                                 int64_t seq_stride, int64_t head_stride, __half* __restrict__ kc,
+                                                 __half* __restrict__ vc, const float* __restrict__ qsrc,
+                                                 const float* __restrict__ qn, const float* __restrict__ kn,
+                                                 const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
+                                                 float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
+                                                 float4& o) {
   constexpr int D = 128;
-  const int g = blockIdx.x, sp = blockIdx.y, m = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int pos = tok_pos[m];
-  const int seq = tok_seq[m];
-  // pos "depends" on seq and on the pointer arguments: the two index loads and every kernarg line are
-  // fetched together, before the first use (otherwise each is a serial scalar-load latency)
-  asm volatile("" : "+s"(pos) : "s"(seq), "s"(qsrc), "s"(kc), "s"(vc), "s"(rcos), "s"(rsin), "s"(qn), "s"(kn),
-               "s"(seq_stride), "s"(head_stride), "s"(out), "s"(partials));
-  STAMP(0);
   const int n_keys = pos + 1;
   const int n_groups = (n_keys + 3) >> 2;
   // groups per split = ceil(n_groups / nsplit) without an integer-division sequence (exact below 2^24)
   const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)nsplit));
   // n_active = ceil(n_groups / gps) without an integer-division sequence (gps <= n_groups < 2^24: exact)
   int n_active = (int)ceilf((float)n_groups / (float)gps);
-  if (sp >= n_active) return;                                      // uniform over the block
+  n_active_out = n_active;
+  if (sp >= n_active) return false;                                // uniform over the block
   const int gb = sp * gps, ge = min(n_groups, gb + gps);           // this split's groups [gb, ge)
   STAMP(1);
   __half* kb = kc + (int64_t)seq * seq_stride + g * head_stride;
@@ -1294,15 +1317,16 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   }
   STAMP(7);
   __syncthreads();
-  if (wave != 0) return;
+  if (wave != 0) return true;
   STAMP(8);
   // wave 0 merges the waves: lane -> head j = lane >> 5, dims [4 (lane & 31), +4)
-  const int j = lane >> 5, d0 = (lane & 31) * 4;
-  float M = -INFINITY;
+  j = lane >> 5;
+  d0 = (lane & 31) * 4;
+  M = -INFINITY;
 #pragma unroll
   for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_ml[w][j][0]);
-  float L = 0.f;
-  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  L = 0.f;
+  o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int w = 0; w < AWV; ++w) {
     const float mw = s_ml[w][j][0];
@@ -1314,6 +1338,37 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
     o.z += wt * t.z;
     o.w += wt * t.w;
   }
+  return true;
+}
+
+template <int DM, int LEAN>
+__global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+                                                         int nsplit, int decode_mode, int H, int KV,
+                                                         int64_t seq_stride, int64_t head_stride,
+                                                         __half* __restrict__ kc,
+                                                         __half* __restrict__ vc, const float* __restrict__ qsrc,
+                                                         const float* __restrict__ qn, const float* __restrict__ kn,
+                                                         const float* __restrict__ rcos, const float* __restrict__ rsin,
+                                                         float eps, float scale, float* __restrict__ out,
+                                                         int* __restrict__ counters, float* __restrict__ partials,
+                                                         int8_t* __restrict__ qout, float* __restrict__ dout) {
+  constexpr int D = 128;
+  const int g = blockIdx.x, sp = blockIdx.y, m = blockIdx.z;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int pos = tok_pos[m];
+  const int seq = tok_seq[m];
+  // pos "depends" on seq and on the pointer arguments: the two index loads and every kernarg line are
+  // fetched together, before the first use (otherwise each is a serial scalar-load latency)
+  asm volatile("" : "+s"(pos) : "s"(seq), "s"(qsrc), "s"(kc), "s"(vc), "s"(rcos), "s"(rsin), "s"(qn), "s"(kn),
+               "s"(seq_stride), "s"(head_stride), "s"(out), "s"(partials));
+  STAMP(0);
+  int n_active, j, d0;
+  float M, L;
+  float4 o;
+  if (!attn_split_merge<DM, LEAN>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc, qn, kn, rcos,
+                                  rsin, eps, scale, n_active, j, d0, M, L, o))
+    return;
+  if (wave != 0) return;
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;
   if (n_active == 1) {
     const float4 r = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
@@ -1780,6 +1835,309 @@ __global__ void k_advance(int* __restrict__ tok_pos, int* __restrict__ step_ctr,
 }
 void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s) {
   hipLaunchKernelGGL(k_advance, dim3(cdiv(M, 64)), dim3(64), 0, s, tok_pos, step_ctr, M);
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Fused batch-1 decode layer: three launches per layer instead of five (M = 1; the C2 critical path).
+//   A  q|k|v GEMV (k_gemv_q8 with the PS prologue): x = x_mid + dpart[0] + ... + dpart[7], block 0 stores x;
+//   B  k_attn_o: decode attention of (kv head g, split sp) (attn_split_merge), partial published; EVERY split of head
+//      g waits for all FS splits (in-launch ticket fan-in), combines them itself, quantises the head pair's 256
+//      outputs to q8_0 (ggml's per-32 quantisation of the o projection input) and multiplies them into ITS 64-row
+//      slice of the o projection, whose weights it prefetched at kernel start:
+//      opart[g][rows] = Wo[rows, 256 g : 256 g + 256] . q8(att_g);
+//   C  k_ffn_fused: x_mid = x + opart[0] + ... + opart[7] (block 0 stores it), rmsnorm + q8_0, gate|up GEMV +
+//      SwiGLU for the block's 12 rows, published; the 32 blocks of its group (384 act rows = 12 q8_0 blocks) wait
+//      for each other, quantise the group's act rows and multiply them into the block's 32-row slice of the down
+//      projection (prefetched): dpart[group][rows] = Wdown[rows, 384 group : +384] . q8(act_group).
+// The next layer's A (or the LM head) completes the residual. A kernel boundary between two dependent GEMVs costs
+// 1.5-1.9 us plus the weight stream's first-byte latency (profiles/); the fan-ins here are 16 / 32 blocks
+// deep and the slices' weights are already in registers when their inputs arrive. Every block of a launch is
+// resident (128 / 256 blocks, at most 2 per CU); every spin is bounded: a timeout sets *err and falls through.
+__device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) {
+  __shared__ unsigned s_target;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 payload stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_target = (t / n + 1) * n;  // tickets are consumed n at a time, launch after launch (never re-armed)
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const unsigned target = s_target;
+    unsigned spins = 0;
+    while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        if (threadIdx.x == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+constexpr int FO_ROWS = 64;  // o-projection rows per split block (E / ASPLIT, E = 1024)
+
+struct AttnOArgs {
+  const int* tok_seq;
+  const int* tok_pos;
+  int H, KV;
+  int64_t seq_stride, head_stride;
+  __half* kc;
+  __half* vc;
+  const float* qkv;
+  const float* qn;
+  const float* kn;
+  const float* rcos;
+  const float* rsin;
+  float eps, scale;
+  const int8_t* wo_q;  // o projection [E][H D], engine layout
+  const __half* wo_d;
+  int E;
+  float* opart;        // [KV][E]
+  unsigned* cnt;       // [KV][CNT_LINE]
+  float* partials;     // [KV][ASPLIT][APART]
+  int* err;
+};
+
+__global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
+  constexpr int D = 128, FS = ASPLIT;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int g = blockIdx.x, sp = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int pos = a.tok_pos[0];
+  const int seq = a.tok_seq[0];
+  asm volatile("" : "+s"(pos) : "s"(seq));
+  // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
+  const int tr = threadIdx.x >> 2, tq = threadIdx.x & 3, KO = a.H * D;
+  const int orow = FO_ROWS * sp + tr;
+  const int8_t* wp = a.wo_q + (int64_t)orow * KO + GQ * D * g + 64 * tq;
+  const int4 w0 = ld_nt16(wp), w1 = ld_nt16(wp + 16), w2 = ld_nt16(wp + 32), w3 = ld_nt16(wp + 48);
+  const __half* dp = a.wo_d + (int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + 2 * tq;
+  const float dw0 = __half2float(dp[0]), dw1 = __half2float(dp[1]);
+  __builtin_amdgcn_sched_barrier(0);
+  int n_active = 0, j = 0, d0 = 0;
+  float M = -INFINITY, L = 0.f;
+  float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool active = attn_split_merge<1, 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
+                                             a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
+                                             M, L, o);
+  float* pbase = a.partials + (int64_t)g * FS * APART;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
+  if (active && wave == 0) {
+    const f4v ov = {o.x, o.y, o.z, o.w};
+    st_sc1_f4(ov, rs, (sp * APART + j * D + d0) * 4);
+    const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
+    if (lane == 0) {
+      const f4v ml = {M, L, M1, L1};
+      st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
+    }
+  }
+  fanin_wait(a.cnt + g * CNT_LINE, FS, a.err);
+  // every split combines the n_active partials (the last-arriver combine of k_attn_block, done by all)
+  __shared__ __attribute__((aligned(16))) int8_t s_aq[GQ * D];
+  __shared__ float s_ad[GQ * D / 32];
+  if (wave == 0) {
+    const int jj = lane >> 5, dd = (lane & 31) * 4;
+    float MM = -INFINITY, LL = 0.f;
+    f4v oo = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < n_active; c0 += FS) {
+      f4v pml[FS], po[FS];
+#pragma unroll
+      for (int t = 0; t < FS; ++t) {
+        const int tt = min(c0 + t, n_active - 1);
+        pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
+        po[t] = ld_sc1_f4(rs, (tt * APART + jj * D + dd) * 4);
+      }
+      float mn = MM;
+#pragma unroll
+      for (int t = 0; t < FS; ++t)
+        if (c0 + t < n_active) mn = fmaxf(mn, jj ? pml[t].z : pml[t].x);
+      const float alpha = MM == -INFINITY ? 0.f : __expf(MM - mn);
+      LL *= alpha;
+      oo *= alpha;
+#pragma unroll
+      for (int t = 0; t < FS; ++t) {
+        if (c0 + t < n_active) {
+          const float mt = jj ? pml[t].z : pml[t].x;
+          const float wt = mt == -INFINITY ? 0.f : __expf(mt - mn);
+          LL += wt * (jj ? pml[t].w : pml[t].y);
+          oo += wt * po[t];
+        }
+      }
+      MM = mn;
+    }
+    const float4 r = make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
+    // q8_0 of the o projection's input (lanes 8b..8b+7 hold one 32-dim block), into LDS
+    const float am = group_max<8>(fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w))));
+    const float d = am / 127.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    const int b0 = (int)roundf(__fmul_rn(r.x, id)) & 0xFF, b1 = (int)roundf(__fmul_rn(r.y, id)) & 0xFF;
+    const int b2 = (int)roundf(__fmul_rn(r.z, id)) & 0xFF, b3 = (int)roundf(__fmul_rn(r.w, id)) & 0xFF;
+    *reinterpret_cast<int32_t*>(s_aq + jj * D + dd) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    if ((lane & 7) == 0) s_ad[(jj * D + dd) / 32] = __half2float(__float2half_rn(d));
+  }
+  __syncthreads();
+  const int4 x0 = *reinterpret_cast<const int4*>(s_aq + 64 * tq), x1 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 16);
+  const int4 x2 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 32), x3 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 48);
+  const int s0 = dot16(w1, x1, dot16(w0, x0, 0)), s1 = dot16(w3, x3, dot16(w2, x2, 0));
+  float v = (float)s0 * (dw0 * s_ad[2 * tq]) + (float)s1 * (dw1 * s_ad[2 * tq + 1]);
+  v += dpp_f<DPP_XOR1>(v);  // the row's 4 threads are 4 consecutive lanes: fixed-order quad sum
+  v += dpp_f<DPP_XOR2>(v);
+  if (tq == 0) a.opart[(int64_t)g * a.E + orow] = v;
+}
+
+void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
+                  __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
+                  const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,
+                  hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ && KV == FUSED_PARTS && E == FO_ROWS * ASPLIT, "attn_o_fused: Qwen3-0.6B head layout");
+  FA_REQUIRE(wk.partials && fw.opart && fw.cnt && fw.err, "attn_o_fused: workspace");
+  AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
+              1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err};
+  hipLaunchKernelGGL(k_attn_o, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
+}
+
+struct FfnArgs {
+  const float* x;       // residual stream after A [E]
+  const float* opart;   // [FUSED_PARTS][E]
+  const float* norm_w;
+  float eps;
+  float* xmid;          // out (block 0): x + sum opart
+  const int8_t* gq;
+  const __half* gd;
+  const int8_t* uq;
+  const __half* ud;
+  const int8_t* dq;     // down [E][F]
+  const __half* dd;
+  float* act;           // [F] hand-off
+  float* dpart;         // [FUSED_PARTS][E]
+  unsigned* cnt;        // [FUSED_PARTS][CNT_LINE]
+  int* err;
+  int E, F;
+};
+
+constexpr int FF_ROWS = 12;                        // gate|up rows per block (3 per wave)
+constexpr int FF_GROUP_BLOCKS = 32;                // blocks per down-projection group: 384 act rows = 12 q8_0 blocks
+constexpr int FF_GROUP_ROWS = FF_ROWS * FF_GROUP_BLOCKS;
+constexpr int FD_ROWS = 32;                        // down-projection rows per block (E / FF_GROUP_BLOCKS)
+
+__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
+  constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
+  const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) int8_t s_q[K];
+  __shared__ float s_d[NB];
+  __shared__ float s_red[4];
+  __shared__ float s_act[FF_ROWS];
+  __shared__ __attribute__((aligned(16))) int8_t s_aq[FF_GROUP_ROWS];
+  __shared__ float s_ad[GB];
+  // ---- activation loads (x, the 8 o partials, the norm weights), then every weight load of the block
+  float xv[PER], pv[FUSED_PARTS][PER], wv[PER];
+  {
+    const float4 a4 = *reinterpret_cast<const float4*>(f.x + t * PER);
+    xv[0] = a4.x; xv[1] = a4.y; xv[2] = a4.z; xv[3] = a4.w;
+#pragma unroll
+    for (int g = 0; g < FUSED_PARTS; ++g) {
+      const float4 p4 = *reinterpret_cast<const float4*>(f.opart + g * f.E + t * PER);
+      pv[g][0] = p4.x; pv[g][1] = p4.y; pv[g][2] = p4.z; pv[g][3] = p4.w;
+    }
+    const float4 w4 = *reinterpret_cast<const float4*>(f.norm_w + t * PER);
+    wv[0] = w4.x; wv[1] = w4.y; wv[2] = w4.z; wv[3] = w4.w;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  GemvArgs a{};
+  a.wq = f.gq; a.wd = f.gd; a.wq2 = f.uq; a.wd2 = f.ud; a.O = f.F; a.rpw = 3;
+  const int row_base = (b * 4 + wave) * 3;
+  RowGroup<1, 2> G;
+  load_group<1, 2>(a, row_base, 0, lane, G);
+  // down slice: rows [FD_ROWS bi, +FD_ROWS), K columns [FF_GROUP_ROWS grp, +FF_GROUP_ROWS); thread -> row dr, q8_0
+  // blocks dk and (dk < 4) dk + 8 of the group's 12
+  const int dr = t >> 3, dk = t & 7;
+  const int drow = FD_ROWS * bi + dr;
+  const int8_t* wdp = f.dq + (int64_t)drow * f.F + FF_GROUP_ROWS * grp + 32 * dk;
+  const int4 da0 = ld_nt16(wdp), da1 = ld_nt16(wdp + 16);
+  const int8_t* wdp2 = wdp + 32 * 8 * (dk < 4 ? 1 : 0);
+  const int4 db0 = ld_nt16(wdp2), db1 = ld_nt16(wdp2 + 16);
+  const __half* ddp = f.dd + (int64_t)drow * (f.F / 32) + GB * grp + dk;
+  const float ds0 = __half2float(ddp[0]), ds1 = __half2float(ddp[dk < 4 ? 8 : 0]);
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- x_mid = x + sum_g opart[g]; rmsnorm + q8_0 into LDS
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    float v = xv[j];
+#pragma unroll
+    for (int g = 0; g < FUSED_PARTS; ++g) v = v + pv[g][j];
+    xv[j] = v;
+  }
+  if (b == 0) *reinterpret_cast<float4*>(f.xmid + t * PER) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+  norm_quant_block_regs<PER>(xv, wv, true, f.eps, K, s_q, s_d, s_red);
+  __syncthreads();
+  // ---- gate|up + SwiGLU for this wave's 3 rows (compute_group's arithmetic)
+  {
+    float acc[3] = {0.f, 0.f, 0.f}, acc2[3] = {0.f, 0.f, 0.f};
+    const int4 xq = *reinterpret_cast<const int4*>(s_q + lane * 16);
+    const float xdv = s_d[lane >> 1];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      int si = dot16(G.w[rr][0], xq, 0);
+      si += dpp_i<DPP_XOR1>(si);
+      if (!(lane & 1)) acc[rr] += (float)si * (G.dw[rr][0] * xdv);
+      int su = dot16(G.u[rr][0], xq, 0);
+      su += dpp_i<DPP_XOR1>(su);
+      if (!(lane & 1)) acc2[rr] += (float)su * (G.du[rr][0] * xdv);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const float y = wave_sum(acc[rr]), y2 = wave_sum(acc2[rr]);
+      if (lane == 0) s_act[wave * 3 + rr] = (y / (1.0f + expf(-y))) * y2;
+    }
+  }
+  __syncthreads();
+  // ---- publish the block's 12 act rows (write-through), group fan-in
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act, f.F * 4);
+  if (t < FF_ROWS / 4) {
+    const f4v v = {s_act[4 * t], s_act[4 * t + 1], s_act[4 * t + 2], s_act[4 * t + 3]};
+    st_sc1_f4(v, ra, (FF_ROWS * b + 4 * t) * 4);
+  }
+  fanin_wait(f.cnt + grp * CNT_LINE, FF_GROUP_BLOCKS, f.err);
+  // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
+  if (t < FF_GROUP_ROWS / 4) {
+    const f4v v = ld_sc1_f4(ra, (FF_GROUP_ROWS * grp + 4 * t) * 4);
+    const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    const float d = am / 127.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    const int q0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, q1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
+    const int q2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, q3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
+    *reinterpret_cast<int32_t*>(s_aq + 4 * t) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
+    if ((t & 7) == 0) s_ad[t >> 3] = __half2float(__float2half_rn(d));
+  }
+  __syncthreads();
+  // ---- down slice: row dr over the group's 12 q8_0 blocks (thread: blocks dk, dk + 8), 8-lane fixed-order sum
+  const int4 xa0 = *reinterpret_cast<const int4*>(s_aq + 32 * dk), xa1 = *reinterpret_cast<const int4*>(s_aq + 32 * dk + 16);
+  float v = (float)dot16(da1, xa1, dot16(da0, xa0, 0)) * (ds0 * s_ad[dk]);
+  if (dk < 4) {
+    const int4 xb0 = *reinterpret_cast<const int4*>(s_aq + 32 * (dk + 8));
+    const int4 xb1 = *reinterpret_cast<const int4*>(s_aq + 32 * (dk + 8) + 16);
+    v = v + (float)dot16(db1, xb1, dot16(db0, xb0, 0)) * (ds1 * s_ad[dk + 8]);
+  }
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_HALF_MIRROR>(v);
+  if (dk == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
+}
+
+void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
+               const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
+               hipStream_t s) {
+  FA_REQUIRE(E == 1024 && F == FF_GROUP_ROWS * FUSED_PARTS && E == FD_ROWS * FF_GROUP_BLOCKS,
+             "ffn_fused: Qwen3-0.6B FFN shape (E 1024, F 3072)");
+  FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
+  FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart, fw.cnt + FUSED_PARTS * CNT_LINE,
+            fw.err, E, F};
+  hipLaunchKernelGGL(k_ffn_fused, dim3(F / FF_ROWS), dim3(256), 0, s, f);
 }
 
 }  // namespace fa

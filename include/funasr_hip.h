@@ -106,6 +106,10 @@ int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* f
  * graphs of 02-Quantize-ONNX.py:13-27 (fp16 weights and op outputs, LayerNorm in fp32, fp16 input audio;
  * replaces the dtype switch of nano_onnx.py:84,101). The fp16 weight copies are built on the next encode. */
 int fa_set_encoder_fp16(fa_engine* e, int32_t on);
+/* Batch-1 decode layer structure: 1 (default) = 3 launches per layer (attention fused with a split o projection,
+ * gate|up fused with a split down projection, in-launch group fan-ins); 0 = the 5-launch layer every batch width
+ * uses. Same numerics contract (ggml q8_0), different f32 summation order of the o / down projections. */
+int fa_set_decode_fused(fa_engine* e, int32_t on);
 int fa_set_debug(fa_engine* e, int32_t flags);
 int fa_encode_tap(fa_engine* e, int32_t which, float* out, int64_t n);
 

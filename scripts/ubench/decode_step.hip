@@ -62,7 +62,30 @@ int main(int argc, char** argv) {
     GemvArgs a{}; a.M = 1; a.eps = 1e-6f; a.wq = q; a.wd = d; a.O = O; a.rpw = gemv_rows_per_wave(O);
     a.x = xin; a.ldx = ldx; a.norm_w = nrm; a.out = o; a.ldo = O; a.res = res; a.ldr = O; return a; };
   int mask = 63;  // 1 qkv, 2 attn, 4 o, 8 gate/up, 16 down, 32 lm_head (ablation: time a subset of the chain)
+  // "fused": the 3-launch batch-1 layer (A = qkv with the partial-sum prologue, B = attention + o slice, C = gate|up +
+  // down slice); masks: 1 A, 2 B, 8 C, 32 lm_head
+  const bool fused = argc > 1 && !strcmp(argv[1], "fused");
+  FusedDecodeWork fw;
+  fw.opart = dalloc<float>(8 * E); fw.dpart = dalloc<float>(8 * E); fw.act = dalloc<float>(F); fw.xmid = dalloc<float>(E);
+  fw.cnt = dalloc<unsigned>(16 * CNT_LINE); fw.err = dalloc<int>(1);
+  CK(hipMemset(fw.cnt, 0, 16 * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
+  CK(hipMemset(fw.opart, 0, 8 * E * 4)); CK(hipMemset(fw.dpart, 0, 8 * E * 4)); CK(hipMemset(fw.xmid, 0, E * 4));
+  wk.max_tokens = 1;
+  auto step_fused = [&]() {
+    for (int l = 0; l < L; ++l) {
+      auto& w = lw[l % n_distinct];
+      auto a = G(w.qkv, w.dqkv, QKV, fw.xmid, E, nw, qkv, nullptr); a.psum = fw.dpart; a.xsum = x;
+      if (mask & 1) gemv_q8(a, E, 0, s);
+      if (mask & 2) attn_o_fused(qkv, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D,
+                                 H, KV, seq, pos, (int64_t)NCTX * KV * D, w.o, w.dO, E, wk, fw, s);
+      if (mask & 8) ffn_fused(x, nw, 1e-6f, w.g, w.dg, w.u, w.du, w.d, w.dd, E, F, fw, s);
+    }
+    auto h = G(wemb, demb, V, fw.xmid, E, nw, logits, nullptr); h.pval = pval; h.pidx = pidx; h.psum = fw.dpart;
+    h.n_part = (V + 4 * h.rpw - 1) / (4 * h.rpw) * 4;
+    if (mask & 32) gemv_q8(h, E, 3, s);
+  };
   auto step = [&]() {
+    if (fused) { step_fused(); return; }
     for (int l = 0; l < L; ++l) {
       auto& w = lw[l % n_distinct];
       if (mask & 1) gemv_q8(G(w.qkv, w.dqkv, QKV, x, E, nw, qkv, nullptr), E, 0, s);
@@ -86,8 +109,14 @@ int main(int argc, char** argv) {
   const char* names[] = {"full step", "qkv x28", "attn x28", "o x28", "gate/up x28", "down x28", "lm_head", "layers w/o attn",
                          "qkv+attn x28"};
   const int masks[] = {63, 1, 2, 4, 8, 16, 32, 29, 3};
+  const char* fnames[] = {"full step", "A qkv+psum x28", "B attn+o x28", "", "C ffn+down x28", "", "lm_head", "A+C x28",
+                          "A+B x28"};
+  const int fmasks[] = {63, 1, 2, 0, 8, 0, 32, 9, 3};
+  if (fused) { for (int t = 0; t < 9; ++t) { names[t] = fnames[t]; } }
   for (int t = 0; t < 9; ++t) {
-    mask = masks[t];
+    if (fused && fmasks[t] == 0) continue;
+    if (fused) mask = fmasks[t];
+    if (!fused) mask = masks[t];
     hipGraph_t g; hipGraphExec_t ex;
     CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)); step(); CK(hipStreamEndCapture(s, &g));
     CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
@@ -101,8 +130,10 @@ int main(int argc, char** argv) {
              ms * 1e3 / R, bytes / (ms * 1e-3 / R) / 1e9, bytes / 1e6);
     else
       printf("  %-18s %8.1f us  (%.2f us per launch)\n", names[t], ms * 1e3 / R,
-             ms * 1e3 / R / (t == 6 ? 1 : (t == 7 ? 4 * L : (t == 8 ? 2 * L : L))));
+             ms * 1e3 / R / (t == 6 ? 1 : (t == 7 ? (fused ? 2 : 4) * L : (t == 8 ? 2 * L : L))));
     CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
   }
+  int err = 0; CK(hipMemcpy(&err, fw.err, 4, hipMemcpyDeviceToHost));
+  if (err) printf("FUSED FAN-IN TIMEOUT\n");
   return 0;
 }

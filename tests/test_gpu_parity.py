@@ -294,13 +294,19 @@ def test_llm_batch20_lean_attention_chunked_combine(llm_tiny_oracle):
 
 
 def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
+    """A sequence decoded inside a batch (M = 3: the 5-launch layer) gives the tokens it gives alone on the same
+    layer structure (the fused batch-1 layer is switched off for the single runs; it is checked below)."""
     rng = np.random.default_rng(4)
     prompts = [llm_tiny_oracle.embed_prompt(rng.integers(0, 4096, n)) for n in (9, 17, 5)]
     singles = []
-    for p in prompts:
-        tiny_engine.llm_reset(0)
-        t = tiny_engine.llm_prefill(0, p)
-        singles.append([t] + list(tiny_engine.llm_generate([0], 10)[0]))
+    tiny_engine.set_decode_fused(False)
+    try:
+        for p in prompts:
+            tiny_engine.llm_reset(0)
+            t = tiny_engine.llm_prefill(0, p)
+            singles.append([t] + list(tiny_engine.llm_generate([0], 10)[0]))
+    finally:
+        tiny_engine.set_decode_fused(True)
     firsts = []
     for s, p in enumerate(prompts):
         tiny_engine.llm_reset(s)
@@ -323,3 +329,36 @@ def test_encoder_full_10s_vs_reference_golden():
     assert _rel(out["audio_embd"][0], g["adaptor"]) < ENC_ATOL_FULL
     nontie = g["ctc_margin"] > 1e-3
     assert ((out["ctc_ids"][0] != g["ctc_ids"]) & nontie).sum() == 0
+
+
+def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
+    """The fused batch-1 layer (attention + split o projection, gate|up + split down projection, in-launch fan-ins)
+    against the 5-launch layer on the same steps: logits equal up to f32 summation order, same greedy token where the
+    margin is not a tie; teacher-forced against the oracle too; over a long context (12 active key splits)."""
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(12)
+    prompt = np.concatenate([m.embed_prompt(rng.integers(0, 4096, 40)),
+                             (rng.standard_normal((330, 1024)) * 0.5).astype(np.float32)], 0)
+    runs = []
+    for fused in (True, False):
+        tiny_engine.set_decode_fused(fused)
+        tiny_engine.llm_reset(0)
+        tok = tiny_engine.llm_prefill(0, prompt)
+        lgs, toks = [], [tok]
+        for _ in range(8):
+            toks.append(int(tiny_engine.llm_generate([0], 1)[0][0]))
+            lgs.append(tiny_engine.llm_logits(0))
+        runs.append((toks, lgs))
+    tiny_engine.set_decode_fused(True)
+    (tf, lf), (tu, lu) = runs
+    m.reset()
+    m.forward(prompt, 0)
+    for k in range(8):
+        if tf[:k + 1] != tu[:k + 1]:
+            break  # a tie flipped the fed token: later steps are different sequences
+        assert _cos(lf[k], lu[k]) > 0.99999
+        ref = m.forward(m.embed_tokens([tf[k]]), prompt.shape[0] + k)
+        _check_step(lf[k], ref)
+        s = np.sort(lu[k])
+        if s[-1] - s[-2] > 1e-3:
+            assert tf[k + 1] == tu[k + 1]
