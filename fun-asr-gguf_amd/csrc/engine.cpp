@@ -294,6 +294,38 @@ struct Engine {
   }
   int r16() const { return enc_fp16 ? 1 : 0; }
 
+  // ---- f32 mode on the bf16x3 split GEMM (enc_gemm 1, default; 0 = exact-f32 MFMA): every GEMM weight split once into
+  // bf16 hi / lo planes (hi plane then lo plane, registration order in each, so contiguous sub-matrices stay
+  // contiguous), built on the first f32 encode after weights change.
+  int enc_gemm = 1;
+  bool wb_stale = true;
+  uint16_t* wb_arena = nullptr;
+  std::unordered_map<const float*, WSplit> wb;
+
+  void prepare_bf3() {
+    if (!wb_stale) return;
+    int64_t total = 0;
+    for (const WRegion& r : gemm_w) total += r.n;
+    if (!wb_arena) wb_arena = alloc<uint16_t>((size_t)2 * total);
+    int64_t off = 0;
+    for (const WRegion& r : gemm_w) {
+      WSplit s;
+      s.hi = wb_arena + off;
+      s.lo = wb_arena + total + off;
+      launch_split_bf16(r.w, wb_arena + off, wb_arena + total + off, r.n, stream);
+      wb[r.w] = s;
+      off += r.n;
+    }
+    wb_stale = false;
+  }
+  WSplit WB(const float* W) const {
+    if (enc_fp16 || !enc_gemm) return WSplit{};
+    auto it = wb.find(W);
+    FA_REQUIRE(it != wb.end(), "bf16x3 encoder: GEMM weight without a split copy");
+    return it->second;
+  }
+  void weights_changed() { w16_stale = wb_stale = true; }
+
   EncBlockW sanm_block(const std::string& p, int d_in) {
     const int d = ec.d_model, f = ec.d_ffn, k = ec.fsmn_k;
     EncBlockW w{};
@@ -643,7 +675,7 @@ struct Engine {
                int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0) {
     hipEvent_t ev;
     prof_begin(1, &ev);
-    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W), &enc_gemm_wk);
+    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W), &enc_gemm_wk, WB(W));
     prof_end(1, 0, 2.0 * M * N * K);
   }
 
@@ -726,6 +758,7 @@ struct Engine {
     FA_HIP(hipMemcpyAsync(d_ctclen, h_ctclen.data(), batch * 4, hipMemcpyHostToDevice, stream));
     // F1-F4
     if (enc_fp16) prepare_fp16();
+    else if (enc_gemm) prepare_bf3();
     frontend_preemph(pcm, stride, d_nsamp, batch, mean_part, xp, xps, stream, r16());
     {
       hipEvent_t ev;
@@ -758,7 +791,8 @@ struct Engine {
     {
       hipEvent_t ev;
       prof_begin(1, &ev);
-      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, rows, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w));
+      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, rows, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w),
+                      WB(ctc_w));
       prof_end(1, 0, 2.0 * rows * (double)ec.ctc_vocab * d);
     }
   }
@@ -1017,6 +1051,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ENC_GEMM")) e->enc_gemm = strcmp(g, "f32") == 0 ? 0 : 1;
     e->build_arenas();
     e->build_constants();
     e->build_encoder();
@@ -1040,7 +1075,7 @@ int fa_engine_destroy(fa_engine* h) {
 int fa_weights_synthetic(fa_engine* h, uint32_t seed) {
   FA_API_BEGIN
   h->e->synthetic(seed);
-  h->e->w16_stale = true;
+  h->e->weights_changed();
   FA_API_END
 }
 
@@ -1051,7 +1086,7 @@ int fa_set_tensor_f32(fa_engine* h, const char* name, const float* host, int64_t
   FA_REQUIRE(n == s.n, std::string("size mismatch for ") + name);
   if (s.kind == 0) {
     FA_HIP(hipMemcpyAsync(s.f, host, n * 4, hipMemcpyHostToDevice, e->stream));
-    e->w16_stale = true;
+    e->weights_changed();
   } else {
     float* tmp = nullptr;
     FA_HIP(hipMalloc(&tmp, n * 4));
@@ -1229,6 +1264,13 @@ int fa_ctc_collapse(fa_engine* h, int32_t blank_id, int32_t* ids_out, int32_t* f
 int fa_set_encoder_fp16(fa_engine* h, int32_t on) {
   FA_API_BEGIN
   h->e->enc_fp16 = on != 0;
+  FA_API_END
+}
+
+int fa_set_encoder_gemm(fa_engine* h, int32_t mode) {
+  FA_API_BEGIN
+  FA_REQUIRE(mode == 0 || mode == 1, "encoder GEMM mode must be 0 (exact f32) or 1 (bf16x3)");
+  h->e->enc_gemm = mode;
   FA_API_END
 }
 

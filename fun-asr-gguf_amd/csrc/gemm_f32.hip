@@ -247,7 +247,54 @@ inline dim3 xcd_grid(int nbx, int nby, int ks = 1) { return dim3(((nbx * nby + 7
 
 // gridDim.z = KS > 1 (64x64 tiles only): split z covers k in [z kper, (z + 1) kper); each split publishes its
 // accumulators (sc1), counts its arrival on the tile's counter, and the last one sums all KS partials in split order
-// (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1)
+// (deterministic) and runs the epilogue (MI355X_MICROARCH.md hand-off table, row 1). Returns false in every block
+// but that last one; there acc holds the sum and the counter is re-armed.
+__device__ __forceinline__ bool split_combine(f32x16& acc, float* __restrict__ part, int* __restrict__ cnt, int tile) {
+  __shared__ int s_last;
+  const int KS = gridDim.z;
+  float* base = part + (int64_t)tile * KS * 256 * 16;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * 256 * 16 * 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    st_sc1_f4(f32x4_t{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]}, rs,
+              ((blockIdx.z * 4 + q) * 256 + threadIdx.x) * 16);  // one 4-KB run per (split, q): full lines
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+  __syncthreads();
+  if (!s_last) return false;
+  f32x4_t pv[GEMM_F32_KS_MAX][4];
+#pragma unroll
+  for (int z = 0; z < GEMM_F32_KS_MAX; ++z)  // all in flight; clamped duplicates past KS are not summed
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pv[z][q] = ld_sc1_f4(rs, ((min(z, KS - 1) * 4 + q) * 256 + threadIdx.x) * 16);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4_t t = pv[0][q];
+#pragma unroll
+    for (int z = 1; z < GEMM_F32_KS_MAX; ++z)
+      if (z < KS) t += pv[z][q];
+    acc[4 * q] = t.x; acc[4 * q + 1] = t.y; acc[4 * q + 2] = t.z; acc[4 * q + 3] = t.w;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// K-split factor of a 64x64-tile launch: up to 4 splits while the tiles leave most CUs idle, >= kmin of k per split
+// (measured on the f32 kernel: ffn2 of one clip, N 512 K 2048, 60.7 -> 55.8 us; the K = 512 projections lose with 2)
+int g_gemm_ks_force = 0;  // microbenchmark hook: K splits of 64x64-tile launches with a workspace (1, 2 or 4)
+static int k_splits(int64_t tiles, int K, const GemmF32Work* wk, int kmin) {
+  int ks = 1;
+  if (wk && wk->part && g_gemm_ks_force && tiles <= wk->cnt_n && tiles * g_gemm_ks_force * 256 * 16 <= wk->part_n)
+    return g_gemm_ks_force;
+  if (wk && wk->part && g_gemm_f32_split)
+    while (ks < GEMM_F32_KS_MAX && tiles * ks * 2 <= 512 && K / (2 * ks) >= kmin && tiles <= wk->cnt_n &&
+           tiles * ks * 2 * 256 * 16 <= wk->part_n)
+      ks *= 2;
+  return ks;
+}
+
 template <class AL, class EPI, int WM, int WN, int KB, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
                                                   EPI epi, float* __restrict__ part, int* __restrict__ cnt) {
@@ -293,38 +340,8 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
     if (kt + 1 < nk) store_tiles<WM, WN, KB>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
     __syncthreads();
   }
-  if constexpr (SPLIT && WM == 1 && WN == 1) {
-    {
-      __shared__ int s_last;
-      const int tile = tm * ((N + T::BN - 1) / T::BN) + tn;
-      float* base = part + (int64_t)tile * KS * 256 * 16;
-      const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * 256 * 16 * 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        st_sc1_f4(f32x4_t{acc[0][0][4 * q], acc[0][0][4 * q + 1], acc[0][0][4 * q + 2], acc[0][0][4 * q + 3]}, rs,
-                  ((blockIdx.z * 256 + threadIdx.x) * 16 + 4 * q) * 4);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
-      __syncthreads();
-      if (!s_last) return;
-      f32x4_t pv[GEMM_F32_KS_MAX][4];
-#pragma unroll
-      for (int z = 0; z < GEMM_F32_KS_MAX; ++z)  // all in flight; clamped duplicates past KS are not summed
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pv[z][q] = ld_sc1_f4(rs, ((min(z, KS - 1) * 256 + threadIdx.x) * 16 + 4 * q) * 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        f32x4_t t = pv[0][q];
-#pragma unroll
-        for (int z = 1; z < GEMM_F32_KS_MAX; ++z)
-          if (z < KS) t += pv[z][q];
-        acc[0][0][4 * q] = t.x; acc[0][0][4 * q + 1] = t.y; acc[0][0][4 * q + 2] = t.z; acc[0][0][4 * q + 3] = t.w;
-      }
-      if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if constexpr (SPLIT && WM == 1 && WN == 1)
+    if (!split_combine(acc[0][0], part, cnt, tm * ((N + T::BN - 1) / T::BN) + tn)) return;
 #pragma unroll
   for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -335,19 +352,14 @@ template <class AL, class EPI, int WM, int WN, int KB = BK>
 static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
                         const GemmF32Work* wk = nullptr) {
   using T = Tile<WM, WN, KB>;
-  // K splits (64x64 tiles, workspace given) while the tiles leave most CUs idle: up to 4, >= 512 of k per split
-  // (measured: ffn2 of one clip, N 512 K 2048, 60.7 -> 55.8 us; the K = 512 projections lose with 2 splits)
-  int ks = 1;
-  const int64_t tiles = (int64_t)cdiv(N, T::BN) * cdiv(M, T::BM);
-  if (WM == 1 && WN == 1 && wk && wk->part && g_gemm_f32_split)
-    while (ks < GEMM_F32_KS_MAX && tiles * ks * 2 <= 512 && K / (2 * ks) >= 512 && tiles <= wk->cnt_n &&
-           tiles * ks * 2 * 256 * 16 <= wk->part_n)
-      ks *= 2;
+  const int ks = WM == 1 && WN == 1 ? k_splits((int64_t)cdiv(N, T::BN) * cdiv(M, T::BM), K, wk, 512) : 1;
   const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM), ks);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   static bool attr = false;
   if (!attr && lds > 65536) {
     (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
@@ -497,12 +509,192 @@ static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N,
   else launch_gemm16<AL, EPI, 1, 1>(al, W, ldw, M, N, K, epi, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16x3 split GEMM (f32 mode, the default encoder path): x = xh + xl with xh = bf16_rn(x) and xl = bf16_rn(x - xh)
+// (x - xh is exact in f32), so x w ~= xh wh + xh wl + xl wh in the f32 accumulator; the dropped xl wl and the rounding
+// of xl leave ~2^-16 relative error per product (numpy simulation over the full 10 s encoder golden: 1.7e-5 of the
+// output range, CTC ids unchanged on non-tie frames; the GPU tests hold it to the f32 goldens' bars). Three
+// v_mfma_f32_32x32x16_bf16 (32 cycles) replace eight v_mfma_f32_32x32x2_f32 (64 cycles) per 16 of k: 5.3x the
+// exact-f32 MFMA rate. W is split once when the weights change (hi and lo planes [N][K], launch_split_bf16); A is
+// split while it is staged. One LDS stage holds the four planes in rows of KB + 8 bf16 (80 or 144 B): the 16 rows
+// one 16-lane group reads start in 16 distinct 4-bank groups, conflict-free. Operand maps and accumulator layout are
+// the f16 kernel's, so the same epilogues apply.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64
+
+template <int WM, int WN, int KB>
+struct TileB3 {
+  static constexpr int BM = 64 * WM, BN = 64 * WN;
+  static constexpr int LDK = KB + 8;                    // bf16 per LDS row
+  static constexpr int R4 = KB / 4, R8 = KB / 8;        // float4 of A / 8-bf16 chunks of W per tile row
+  static constexpr int NA = BM * KB / 4 / 256;          // float4 of A per thread
+  static constexpr int NB = BN * KB / 8 / 256;          // 8-bf16 chunks of each W plane per thread
+  static constexpr int PA = BM * LDK, PB = BN * LDK;    // bf16 per plane
+  static constexpr int STAGE = 2 * (PA + PB);           // [Ah][Al][Bh][Bl]
+};
+
+template <class AL, int WM, int WN, int KB>
+__device__ __forceinline__ void load_b3(const AL& al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                        int64_t ldw, int m0, int n0, int k0, int M, int N, int K,
+                                        float4 (&ra)[TileB3<WM, WN, KB>::NA], uint4 (&rh)[TileB3<WM, WN, KB>::NB],
+                                        uint4 (&rl)[TileB3<WM, WN, KB>::NB]) {
+  using T = TileB3<WM, WN, KB>;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < T::NA; ++i) {
+    const int idx = t + i * 256;
+    ra[i] = al.load4(m0 + idx / T::R4, k0 + 4 * (idx % T::R4), M, K);
+  }
+#pragma unroll
+  for (int i = 0; i < T::NB; ++i) {
+    const int idx = t + i * 256;  // K % 8 == 0
+    const int n = n0 + idx / T::R8, k = k0 + 8 * (idx % T::R8);
+    const bool in = n < N && k < K;
+    const int64_t o = (int64_t)n * ldw + k;
+    rh[i] = in ? *reinterpret_cast<const uint4*>(Wh + o) : make_uint4(0, 0, 0, 0);
+    rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int WM, int WN, int KB>
+__device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<WM, WN, KB>::NA],
+                                         const uint4 (&rh)[TileB3<WM, WN, KB>::NB],
+                                         const uint4 (&rl)[TileB3<WM, WN, KB>::NB]) {
+  using T = TileB3<WM, WN, KB>;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < T::NA; ++i) {
+    const int idx = t + i * 256;
+    const float4 v = ra[i];
+    const bf16x4 h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    const bf16x4 l = {(__bf16)(v.x - (float)h[0]), (__bf16)(v.y - (float)h[1]), (__bf16)(v.z - (float)h[2]),
+                      (__bf16)(v.w - (float)h[3])};
+    const int o = (idx / T::R4) * T::LDK + 4 * (idx % T::R4);
+    *reinterpret_cast<bf16x4*>(st + o) = h;
+    *reinterpret_cast<bf16x4*>(st + T::PA + o) = l;
+  }
+#pragma unroll
+  for (int i = 0; i < T::NB; ++i) {
+    const int idx = t + i * 256;
+    const int o = (idx / T::R8) * T::LDK + 8 * (idx % T::R8);
+    *reinterpret_cast<uint4*>(st + 2 * T::PA + o) = rh[i];
+    *reinterpret_cast<uint4*>(st + 2 * T::PA + T::PB + o) = rl[i];
+  }
+}
+
+template <class AL, class EPI, int WM, int WN, int KB>
+__global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                                  int64_t ldw, int M, int N, int K, EPI epi) {
+  using T = TileB3<WM, WN, KB>;
+  constexpr int LDK = T::LDK;
+  extern __shared__ float smem[];  // 2 stages; the epilogue reuses it
+  __bf16* sh = reinterpret_cast<__bf16*>(smem);
+  int tm, tn;
+  if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
+  const int m0 = tm * T::BM, n0 = tn * T::BN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  float4 ra[T::NA];
+  uint4 rh[T::NB], rl[T::NB];
+  load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl);
+  store_b3<WM, WN, KB>(sh, ra, rh, rl);
+  __syncthreads();
+  const int nk = (K + KB - 1) / KB;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, (kt + 1) * KB, M, N, K, ra, rh, rl);
+    const __bf16* a = sh + cur * T::STAGE + (wr * 32 * WM + r) * LDK + 8 * h;
+    const __bf16* b = sh + cur * T::STAGE + 2 * T::PA + (wc * 32 * WN + r) * LDK + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < KB / 16; ++kk) {
+      bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(a + 32 * i * LDK + 16 * kk);
+        alo[i] = *reinterpret_cast<const bf16x8*>(a + T::PA + 32 * i * LDK + 16 * kk);
+      }
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(b + 32 * j * LDK + 16 * kk);
+        blo[j] = *reinterpret_cast<const bf16x8*>(b + T::PB + 32 * j * LDK + 16 * kk);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], blo[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+}
+
+// No K splits: the bf16x3 body is fast enough that the split-K seam (publish + ticket + combine, 5-13 us:
+// MI355X_MICROARCH.md splitk-seam) costs more than it saves (one clip, measured: out N 512 K 512 10.8 -> 19.8 us,
+// ffn2 N 512 K 2048 32.6 -> 57 us with 2-4 splits).
+template <class AL, class EPI, int WM, int WN, int KB>
+static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                           hipStream_t s) {
+  using T = TileB3<WM, WN, KB>;
+  FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3: K and ldw must be multiples of 8");
+  const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM));
+  const size_t lds = std::max<size_t>(2 * T::STAGE * 2, 1024);  // >= EpiArgmax scratch
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB>), grid, dim3(256), lds, s, al,
+                     reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+}
+
+template <class AL, class EPI>
+static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
+  const int f = g_gemm_bf3_force;
+  const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
+  if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32>(al, w, ldw, M, N, K, epi, s);
+  else launch_gemm_b3<AL, EPI, 1, 1, 64>(al, w, ldw, M, N, K, epi, s);
+}
+
+__global__ void k_split_bf16(const float* __restrict__ w, __bf16* __restrict__ hi, __bf16* __restrict__ lo, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = w[i];
+    const __bf16 h = (__bf16)v;
+    hi[i] = h;
+    lo[i] = (__bf16)(v - (float)h);
+  }
+}
+
+void launch_split_bf16(const float* w, uint16_t* hi, uint16_t* lo, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int blocks = (int)std::min<int64_t>(cdiv(n, 256), 4096);
+  hipLaunchKernelGGL(k_split_bf16, dim3(blocks), dim3(256), 0, s, w, reinterpret_cast<__bf16*>(hi),
+                     reinterpret_cast<__bf16*>(lo), n);
+}
+
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16, const GemmF32Work* wk) {
+                 hipStream_t s, const __half* W16, const GemmF32Work* wk, WSplit wb) {
   ALoadPlain al{A, lda};
   EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
   if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
+  else if (wb.hi) run_gemm_b3(al, wb, ldw, M, N, K, epi, s);
   else run_gemm(al, W, ldw, M, N, K, epi, s, true, wk);
 }
 
@@ -538,12 +730,13 @@ __global__ void k_argmax_final(const float* __restrict__ pval, const int* __rest
 }
 
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
-                     int* pidx, int* out, hipStream_t s, const __half* W16) {
+                     int* pidx, int* out, hipStream_t s, const __half* W16, WSplit wb) {
   int n_tiles = cdiv(N, 64);
   ALoadPlain al{A, lda};
   EpiArgmax epi{bias, pval, pidx, n_tiles, W16 ? 1 : 0};
   // the argmax epilogue reduces 64-column blocks
   if (W16) launch_gemm16<ALoadPlain, EpiArgmax, 1, 1>(al, W16, K, M, N, K, epi, s);
+  else if (wb.hi) launch_gemm_b3<ALoadPlain, EpiArgmax, 1, 1, 64>(al, wb, K, M, N, K, epi, s);
   else run_gemm(al, W, K, M, N, K, epi, s, false);
   hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
 }

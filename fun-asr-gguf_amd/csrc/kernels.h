@@ -32,16 +32,23 @@ struct GemmF32Work {
   int64_t cnt_n = 0;
 };
 extern int g_gemm_f32_split;  // 1 (default): K splits where the tiles leave the chip idle; 0: none
-// W16 != nullptr: fp16 mode (C5) on the f16 MFMA kernel with the fp16 weight copy W16, every op output rounded to fp16
+// bf16x3 split of an f32 weight (raw bf16 bits): hi = bf16_rn(w), lo = bf16_rn(w - hi), planes laid out as w
+struct WSplit {
+  const uint16_t* hi = nullptr;
+  const uint16_t* lo = nullptr;
+};
+void launch_split_bf16(const float* w, uint16_t* hi, uint16_t* lo, int64_t n, hipStream_t s);
+// W16 != nullptr: fp16 mode (C5) on the f16 MFMA kernel with the fp16 weight copy W16, every op output rounded to fp16;
+// else wb.hi != nullptr: f32 mode on the bf16x3 split kernel; else the exact-f32 MFMA kernel
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16 = nullptr, const GemmF32Work* wk = nullptr);
+                 hipStream_t s, const __half* W16 = nullptr, const GemmF32Work* wk = nullptr, WSplit wb = {});
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
                      int64_t ldp, hipStream_t s, int r16 = 0);
 void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
                   int n_freq, hipStream_t s, int r16 = 0);
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
-                     int* pidx, int* out, hipStream_t s, const __half* W16 = nullptr);
+                     int* pidx, int* out, hipStream_t s, const __half* W16 = nullptr, WSplit wb = {});
 
 // attn_f32.hip
 // Key-split workspace of the encoder attention (used only while (query tile, head, clip) blocks leave the

@@ -17,7 +17,8 @@ EXPORTS = [
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
     "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
-    "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
+    "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
+    "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
 ]
 
 
@@ -72,6 +73,7 @@ def load():
     lib.fa_set_debug.argtypes = [P, I32]
     lib.fa_set_encoder_fp16.argtypes = [P, I32]
     lib.fa_set_decode_fused.argtypes = [P, I32]
+    lib.fa_set_encoder_gemm.argtypes = [P, I32]
     lib.fa_encode_tap.argtypes = [P, I32, P, I64]
     lib.fa_embd_rows.argtypes = [P, P, I32, I32, P]
     lib.fa_llm_reset.argtypes = [P, I32]
@@ -143,6 +145,10 @@ class Engine:
     def set_encoder_fp16(self, on=True):
         """fp16 encoder graph (the reference's *.fp16.onnx, 02-Quantize-ONNX.py:13-27); fp32 when off."""
         _check(self.lib.fa_set_encoder_fp16(self.h, 1 if on else 0), "fa_set_encoder_fp16")
+
+    def set_encoder_gemm(self, mode="bf16x3"):
+        """fp32-graph GEMM arithmetic: "bf16x3" (default, split operands on the bf16 matrix cores) or "f32"."""
+        _check(self.lib.fa_set_encoder_gemm(self.h, {"f32": 0, "bf16x3": 1}[mode]), "fa_set_encoder_gemm")
 
     def set_decode_fused(self, on=True):
         """Batch-1 decode layer: fused 3-launch structure (default) or the 5-launch layer."""

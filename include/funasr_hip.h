@@ -106,6 +106,11 @@ int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* f
  * graphs of 02-Quantize-ONNX.py:13-27 (fp16 weights and op outputs, LayerNorm in fp32, fp16 input audio;
  * replaces the dtype switch of nano_onnx.py:84,101). The fp16 weight copies are built on the next encode. */
 int fa_set_encoder_fp16(fa_engine* e, int32_t on);
+/* fp32-graph GEMM arithmetic: 1 (default) = bf16x3 split operands on the bf16 matrix cores (x w ~= xh wh + xh wl +
+ * xl wh, f32 accumulate; ~2^-16 relative error per product, held to the fp32 goldens' tolerances by the tests);
+ * 0 = exact-f32 MFMA (v_mfma_f32_32x32x2_f32). Env FUNASR_ENC_GEMM=f32 selects 0 at engine creation. The split
+ * weight copies are built on the next encode. No effect in fp16 mode. */
+int fa_set_encoder_gemm(fa_engine* e, int32_t mode);
 /* Batch-1 decode layer structure: 1 (default) = 3 launches per layer (attention fused with a split o projection,
  * gate|up fused with a split down projection, in-launch group fan-ins); 0 = the 5-launch layer every batch width
  * uses. Same numerics contract (ggml q8_0), different f32 summation order of the o / down projections. */

@@ -1,5 +1,5 @@
 """Encoder-only runs (full Fun-ASR-Nano encoder/adaptor/CTC dims, synthetic weights) for kernel profiling:
-  rocprofv3 --kernel-trace --stats -d gpurun_out/pe -o run -- python scripts/prof_encode.py [batch] [reps] [fp16]"""
+  rocprofv3 --kernel-trace --stats -d gpurun_out/pe -o run -- python scripts/prof_encode.py [batch] [reps] [fp16|f32|bf16x3]"""
 import os
 import sys
 import time
@@ -13,9 +13,11 @@ from fun_asr_gguf.synthetic import synth_audio  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 fp16 = len(sys.argv) > 3 and sys.argv[3] == "fp16"
+gemm = sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] in ("f32", "bf16x3") else "bf16x3"
 eng = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=B, max_samples=16000 * 60)
 eng.synthetic_weights(0)
 eng.set_encoder_fp16(fp16)
+eng.set_encoder_gemm(gemm)
 clips = [synth_audio(16000 * 60, i) for i in range(B)]
 h = eng.upload(clips)
 eng.encode(clips, resident=h)
@@ -25,5 +27,5 @@ for _ in range(reps):
     eng.encode(clips, resident=h)
 eng.synchronize()
 dt = (time.perf_counter() - t) / reps
-print(f"encode batch {B} x 60 s ({'fp16' if fp16 else 'fp32'}): {dt * 1e3:.2f} ms per call, {dt * 1e3 / B:.2f} ms per clip")
+print(f"encode batch {B} x 60 s ({'fp16' if fp16 else 'fp32 ' + gemm}): {dt * 1e3:.2f} ms per call, {dt * 1e3 / B:.2f} ms per clip")
 eng.close()

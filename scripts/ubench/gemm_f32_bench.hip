@@ -8,6 +8,8 @@
 #include "../../fun-asr-gguf_amd/csrc/kernels.h"
 namespace fa {
 extern int g_gemm_f32_force;
+extern int g_gemm_bf3_force;
+extern int g_gemm_ks_force;
 void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
 void log(int, const std::string&) {}
 }
@@ -27,7 +29,8 @@ static double time_graph(std::function<void()> f, int reps) {
   return ms * 1e3 / (3.0 * reps);
 }
 int main(int argc, char** argv) {
-  const int pad = argc > 1 ? atoi(argv[1]) : 0;  // extra floats per A / W row (stride study)
+  const bool ksmode = argc > 1 && std::string(argv[1]) == "ks";  // K-split study on the single-clip shapes
+  const int pad = argc > 1 && !ksmode ? atoi(argv[1]) : 0;  // extra floats per A / W row (stride study)
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int Mmax = 32032, Kmax = 2048 + 128, Nmax = 2048;
   float *A, *W, *bias, *C;
@@ -71,8 +74,61 @@ int main(int argc, char** argv) {
     }
     printf("check split-K: max|err| %.3g %s\n", err, err < 1e-3 ? "ok" : "FAIL");
   }
+  uint16_t *Wh, *Wl;
+  CK(hipMalloc(&Wh, (size_t)Nmax * Kmax * 2)); CK(hipMalloc(&Wl, (size_t)Nmax * Kmax * 2));
+  launch_split_bf16(W, Wh, Wl, (int64_t)Nmax * Kmax, s);
+  WSplit wb; wb.hi = Wh; wb.lo = Wl;
+  for (int sk = 0; sk < 2; ++sk) {  // bf16x3 spot checks (M=100 N=96 K=72; split-K M=70 N=64 K=2048): relative to sum |a w|
+    const int M = sk ? 70 : 100, N = sk ? 64 : 96, K = sk ? 2048 : 72;
+    for (int v : {1, 2, 3}) {
+      if (sk && v == 2) continue;
+      g_gemm_bf3_force = v;
+      gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s, nullptr, sk ? &wk : nullptr, wb);
+      CK(hipStreamSynchronize(s));
+      std::vector<float> a((size_t)M * K), w((size_t)N * K), b(N), c((size_t)M * N);
+      CK(hipMemcpy(a.data(), A, a.size() * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(w.data(), W, w.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), bias, N * 4, hipMemcpyDeviceToHost)); CK(hipMemcpy(c.data(), C, c.size() * 4, hipMemcpyDeviceToHost));
+      double err = 0, mag = 0;
+      for (int i = 0; i < M; ++i) for (int j = 0; j < N; ++j) {
+        double r = b[j], m = std::fabs(b[j]);
+        for (int k = 0; k < K; ++k) { r += (double)a[i * K + k] * w[j * K + k]; m += std::fabs((double)a[i * K + k] * w[j * K + k]); }
+        err = std::max(err, std::fabs(r - c[i * N + j]) / m);
+      }
+      printf("check bf16x3 variant %d%s: max|err|/sum|aw| %.3g %s\n", v, sk ? " split-K" : "", err, err < 3e-5 ? "ok" : "FAIL");
+    }
+  }
+  g_gemm_bf3_force = 0;
   struct Sh { const char* name; int N, K; };
   const Sh shapes[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
+  if (ksmode) {
+    for (const Sh& sh : shapes) {
+      std::vector<float> ref;
+      for (int f32 : {1, 0})
+        for (int v : {1, 3}) {
+          printf("M=1001 %-9s %s %s:", sh.name, f32 ? "f32" : "bf3", v == 1 ? "64x64x32" : "64x64x64");
+          for (int ks : {1, 2, 4}) {
+            g_gemm_ks_force = ks;
+            g_gemm_f32_force = v;
+            g_gemm_bf3_force = v;
+            const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, 1001, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
+                                                           nullptr, &wk, f32 ? WSplit{} : wb); }, 50);
+            CK(hipGetLastError());
+            CK(hipMemsetAsync(C, 0, (size_t)1001 * sh.N * 4, s));
+            gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, 1001, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s, nullptr, &wk,
+                        f32 ? WSplit{} : wb);
+            CK(hipStreamSynchronize(s));
+            std::vector<float> c((size_t)1001 * sh.N);
+            CK(hipMemcpy(c.data(), C, c.size() * 4, hipMemcpyDeviceToHost));
+            if (ref.size() != c.size()) ref = c;
+            double e = 0, mx = 0;
+            for (size_t i = 0; i < c.size(); ++i) { e = std::max(e, (double)std::fabs(c[i] - ref[i])); mx = std::max(mx, (double)std::fabs(ref[i])); }
+            printf("  ks %d %6.1f us (dev %.1e)", ks, us, e / mx);
+          }
+          printf("\n");
+        }
+    }
+    return 0;
+  }
   printf("row stride pad %d floats\n", pad);
   for (int M : {1001, 32032}) {
     if (pad && M > 2000) break;
@@ -86,6 +142,15 @@ int main(int argc, char** argv) {
         const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K", "engine default"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
+      for (int v : {1, 3, 2, 0}) {
+        g_gemm_bf3_force = v;
+        const double us = time_graph([&] { gemm_linear(A, sh.K + pad, W, sh.K + pad, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
+                                                       nullptr, &wk, wb); },
+                                     M > 2000 ? 10 : 50);
+        const char* nm[] = {"bf3 default", "bf3 64x64x32", "bf3 128x128x32", "bf3 64x64x64"};
+        printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
+      }
+      g_gemm_bf3_force = 0;
       printf("\n");
     }
   }

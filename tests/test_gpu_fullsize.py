@@ -96,8 +96,25 @@ def test_encoder_60s_vs_reference_golden(eng, g60):
                    g60["ctc_ids"], g60["ctc_margin"], "60 s")
 
 
+def test_encoder_60s_exact_f32_gemm_mode(eng, g60):
+    """fa_set_encoder_gemm(0): the exact-f32 MFMA GEMMs (v_mfma_f32_32x32x2_f32, K-split few-tile shapes) against the
+    same golden as the default bf16x3 split-operand GEMMs above; both modes agree to the golden bar."""
+    eng.set_encoder_gemm("f32")
+    try:
+        out = eng.encode([g60["audio"]], want_enc=True)
+    finally:
+        eng.set_encoder_gemm("bf16x3")
+    out3 = eng.encode([g60["audio"]], want_enc=True)
+    rows = g60["enc_rows"]
+    _check_encoder(out["enc"][0][rows], out["audio_embd"][0], out["ctc_ids"][0], g60["enc"], g60["adaptor"],
+                   g60["ctc_ids"], g60["ctc_margin"], "60 s exact f32")
+    e32, e3 = _rel(out["enc"][0][rows], g60["enc"]), _rel(out3["enc"][0][rows], g60["enc"])
+    print(f"60 s encoder max-abs/max vs golden: exact f32 {e32:.2e}, bf16x3 {e3:.2e}")
+    assert e3 < ENC_ATOL and _rel(out3["audio_embd"][0], out["audio_embd"][0]) < ENC_ATOL
+
+
 def test_encoder_batch32_vs_oracle(eng, cenc):
-    """configs[2]: 32 clips in one encoder batch (32 x 1001 rows: the 128x128-tile f32 GEMM path), ragged lengths
+    """configs[2]: 32 clips in one encoder batch (32 x 1001 rows: the 128x128-tile GEMM path), ragged lengths
     included; clips 0, 5, 17 and 31 against the oracle run of each clip alone (CPU-EP policy, unpadded)."""
     from fun_asr_gguf.synthetic import synth_audio
     lens = [960000] * 32
