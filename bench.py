@@ -331,7 +331,7 @@ def headline(args, world, dt, dt_prof, prof, stage):
     ms_step = dt / args.steps * 1e3
     # dominant kernel class by estimated device time: decoder layer classes are timed on layer 0 only
     # (identical shapes in all layers), so their sampled ms stand for n_layer x as much device time
-    names = {0: "q8_0 GEMV/GEMM (decoder layers)", 1: "f32 MFMA GEMM (encoder)", 2: "f32 MFMA attention (encoder)",
+    names = {0: "q8_0 GEMV/GEMM (decoder layers)", 1: "bf16x3 MFMA GEMM (f32 encoder)", 2: "f32 MFMA attention (encoder)",
              3: "decode attention", 4: "q8_0 LM head GEMV + argmax"}
     n_layer = 28 if args.model == "full" else 2
     weight = {0: n_layer, 1: 1, 2: 1, 3: n_layer, 4: 1}
@@ -365,7 +365,7 @@ def headline(args, world, dt, dt_prof, prof, stage):
     out = {"metric": "audio-sec/s (RTF = 1/value per GPU) on 60 s 16 kHz clips", "value": round(value, 3),
            "unit": "audio_s/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "f32 encoder / q8_0 x q8_0 int-dot decoder", "data": "synthetic (seeded chirps; synthetic weights)",
+           "dtype": "f32 encoder (bf16x3 split-operand MFMA GEMMs, f32 accumulate) / q8_0 x q8_0 int-dot decoder", "data": "synthetic (seeded chirps; synthetic weights)",
            "rtf": round(1.0 / (value / world), 6),
            "config": {"workload": "configs[1]: single 60 s clip per GPU per step, fp32 encoder + CTC + q8_0 LLM "
                                   "(73+126+5 prefill, 253 greedy steps, EOS ignored)",
