@@ -15,6 +15,14 @@ ggml rms_norm accumulates sum(x*x) in double and scales by 1/sqrtf(mean+eps) (f3
 are quantised per 32-block with the reference q8_0 quantiser (q8.py). Embedding rows: prompt rows are
 fp16(d*q) as produced by numpy in llama.py:778-784; generated-token rows are f32(d)*q (ggml get_rows).
 "Parity unpinned" w.r.t. llama.cpp itself (absent); anchored on HF Qwen3 in tests.
+
+Attention arithmetic. The reference creates its context with flash_attn_type = 1 (llama.py:404, 475), so llama.cpp
+runs flash_attn_ext; its CPU kernel (ggml-cpu ops.cpp, ggml_compute_forward_flash_attn_ext_f16 on an f16 cache)
+rounds Q to f16 for the K dot and accumulates P.V in f16 with an online softmax (y = f16(f32(y) * ms) on a new
+max, y = f16(f32(y) + f32(v) * vs) per key, S in f32), while GPU backends differ again. attn="f32" (default, what
+the HIP engine computes: f32 Q, f32 softmax and P.V over the fp16 cache) is the backend-neutral form;
+attn="ggml_cpu_fa" restates the CPU kernel; tests/test_oracle_golden.py::test_attention_mode_below_q8_noise_floor
+shows the two differ by less than the q8_0 activation noise floor the GPU tolerances are set on.
 """
 import numpy as np
 from . import q8
@@ -53,8 +61,36 @@ def silu(x):
     return (x / (np.float32(1.0) + np.exp(-x))).astype(np.float32)
 
 
+def attn_ggml_cpu_fa(q, k16, v16, scale, pos):
+    """ggml-cpu flash_attn_ext over an f16 cache (see the module docstring): q [N, H, D] f32, k16 / v16 [T, KV, D]
+    f16, query row n attends keys 0..pos[n]."""
+    N, H, D = q.shape
+    g = H // k16.shape[1]
+    q16 = q.astype(np.float16).astype(np.float32)
+    o = np.empty((N, H, D), np.float32)
+    for n in range(N):
+        T = int(pos[n]) + 1
+        for hh in range(H):
+            kk = k16[:T, hh // g].astype(np.float32)
+            vv = v16[:T, hh // g].astype(np.float32)
+            s = ((kk @ q16[n, hh]).astype(np.float32) * scale).astype(np.float32)
+            M, S = np.float32(-np.inf), np.float32(0.0)
+            acc = np.zeros(D, np.float16)
+            for t in range(T):
+                if s[t] > M:
+                    ms = np.float32(np.exp(np.float32(M - s[t]))) if M != -np.inf else np.float32(0.0)
+                    M, vs = s[t], np.float32(1.0)
+                    acc = (acc.astype(np.float32) * ms).astype(np.float16)
+                else:
+                    ms, vs = np.float32(1.0), np.float32(np.exp(np.float32(s[t] - M)))
+                acc = (acc.astype(np.float32) + vv[t] * vs).astype(np.float16)
+                S = np.float32(S * ms + vs)
+            o[n, hh] = acc.astype(np.float32) * np.float32(1.0 / S)
+    return o
+
+
 class Qwen3Q8:
-    def __init__(self, weights, cfg, n_ctx=2048):
+    def __init__(self, weights, cfg, n_ctx=2048, attn="f32"):
         """weights: name -> f32 array (GGUF names); 2-D tensors are q8_0-quantised here, exactly as
         the GGUF converter does (convert_hf_to_gguf.py:622-623 -> gguf/quants.py:378-393)."""
         self.cfg = cfg
@@ -67,6 +103,8 @@ class Qwen3Q8:
                 self.f[k] = v.astype(np.float32)
         self.cos, self.sin = rope_table(n_ctx, cfg["head_dim"], cfg["rope_theta"])
         self.n_ctx = n_ctx
+        assert attn in ("f32", "ggml_cpu_fa")
+        self.attn = attn
         self.reset()
 
     def reset(self):
@@ -112,11 +150,15 @@ class Qwen3Q8:
             o = np.empty((N, H, D), np.float32)
             causal = np.where(np.arange(T)[None, :] <= pos[:, None], 0.0, -np.inf).astype(np.float32)
             g = H // KV
-            for hh in range(H):
-                s = (q[:, hh, :] @ K[:, hh // g, :].T) * scale + causal
-                s = s - s.max(-1, keepdims=True)
-                e = np.exp(s)
-                o[:, hh, :] = (e / e.sum(-1, keepdims=True)) @ V[:, hh // g, :]
+            if self.attn == "ggml_cpu_fa":
+                o = attn_ggml_cpu_fa(q, self.kc[l][:T].reshape(T, KV, D), self.vc[l][:T].reshape(T, KV, D), scale,
+                                     pos)
+            else:
+                for hh in range(H):
+                    s = (q[:, hh, :] @ K[:, hh // g, :].T) * scale + causal
+                    s = s - s.max(-1, keepdims=True)
+                    e = np.exp(s)
+                    o[:, hh, :] = (e / e.sum(-1, keepdims=True)) @ V[:, hh // g, :]
             x = (x + self.mm(b + "attn_output.weight", o.reshape(N, H * D))).astype(np.float32)
             h = rms_norm(x, self.f[b + "ffn_norm.weight"], eps)
             a = (silu(self.mm(b + "ffn_gate.weight", h)) * self.mm(b + "ffn_up.weight", h)).astype(np.float32)
