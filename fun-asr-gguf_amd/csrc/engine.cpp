@@ -140,6 +140,8 @@ struct Engine {
   AttnWork attn_wk;
   FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
   bool use_fused = true;   // FUNASR_FUSED_DECODE=0: the 5-launch layer at M = 1 too (A/B)
+  bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
+  float* d_ssp = nullptr;  // batched decode: per-token sum-of-squares partials [max_seqs][32] of the residual stream
   AttnF32Work enc_attn_wk;
   GemmF32Work enc_gemm_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
@@ -600,6 +602,7 @@ struct Engine {
     n_part = std::max(lm_head_parts(lc.n_vocab, 1), lm_head_parts(lc.n_vocab, lc.max_seqs));
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
+    d_ssp = alloc<float>((size_t)lc.max_seqs * 32);
 
     d_tok_seq = alloc<int>(m_max);
     d_tok_pos = alloc<int>(m_max);
@@ -805,6 +808,10 @@ struct Engine {
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
     const bool small = gemv_small(M);
+    // batched decode: the residual GEMMs (o, down) quantise their new rows times the next RMSNorm weight and leave
+    // per-token sum-of-squares partials; q|k|v, gate|up and the LM head apply rstd to those rows' block scales
+    // (no k_prep_q8 launches but layer 0's)
+    const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm;
     (void)max_pos;
     if (decode && M == 1 && use_fused && fused_shape_ok()) {
       llm_forward_fused();
@@ -822,6 +829,7 @@ struct Engine {
       a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
       a.out = lqkv; a.ldo = QKV;
       if (small) { a.x = lx; a.ldx = E; a.norm_w = w.attn_norm; }
+      else if (nrm && l > 0) { a.xq = lxq; a.xd = lxd; a.ssp = d_ssp; }  // rows from the previous down epilogue
       else { prep_q8(lx, E, w.attn_norm, lc.rms_eps, M, E, lxq, lxd, stream); a.xq = lxq; a.xd = lxd; }
       gemv(a, E, 0);
       {
@@ -842,6 +850,7 @@ struct Engine {
       o.out = lx; o.ldo = E; o.res = lx; o.ldr = E;
       if (small) { o.x = latt; o.ldx = H * D; }
       else { o.xq = lxq2; o.xd = lxd2; }
+      if (nrm) { o.ssp_out = d_ssp; o.qout = lxq; o.dout = lxd; o.qn_w = w.ffn_norm; }
       gemv(o, H * D, 1);
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
       GemvArgs g{};
@@ -849,8 +858,8 @@ struct Engine {
       g.rpw = gemv_rows_per_wave(F); g.out = lact; g.ldo = F;
       if (small) { g.x = lx; g.ldx = E; g.norm_w = w.ffn_norm; }
       else {
-        prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream);
-        g.xq = lxq; g.xd = lxd;
+        if (nrm) { g.xq = lxq; g.xd = lxd; g.ssp = d_ssp; }  // rows from the o epilogue
+        else { prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream); g.xq = lxq; g.xd = lxd; }
         g.qout = lxq2; g.dout = lxd2;  // SwiGLU epilogue quantises act for the down GEMM (no prep launch)
       }
       gemv(g, E, 2);
@@ -860,6 +869,10 @@ struct Engine {
       dn.out = lx; dn.ldo = E; dn.res = lx; dn.ldr = E;
       if (small) { dn.x = lact; dn.ldx = F; }
       else { dn.xq = lxq2; dn.xd = lxd2; }
+      if (nrm) {
+        dn.ssp_out = d_ssp; dn.qout = lxq; dn.dout = lxd;
+        dn.qn_w = l + 1 < lc.n_layer ? layers[l + 1].attn_norm : out_norm;
+      }
       gemv(dn, F, 1);
     }
     prof_sample = true;
@@ -872,6 +885,7 @@ struct Engine {
     h.out = logits; h.ldo = lc.n_vocab;
     h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows);
     if (gemv_small(n_rows)) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
+    else if (nrm) { h.xq = lxq; h.xd = lxd; h.ssp = d_ssp; }  // rows from the last down epilogue
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
     gemv(h, E, 3);
   }
@@ -1051,6 +1065,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ENC_GEMM")) e->enc_gemm = strcmp(g, "f32") == 0 ? 0 : 1;
     e->build_arenas();
     e->build_constants();

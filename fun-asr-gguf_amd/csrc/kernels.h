@@ -93,6 +93,11 @@ struct GemvArgs {
   int* kcnt; int64_t kcnt_n;               //   (counters zeroed once; re-armed by the combining block)
   int8_t* qout; float* dout;               // MFMA GEMM SwiGLU epilogue: also the q8_0 rows of out (next GEMM's input)
   const float* psum; float* xsum;          // fused decode (M = 1): x += psum[0..7][K] before the norm; block 0 -> xsum
+  // batched decode (8 <= M <= 32, no k_prep_q8 launches): a residual GEMM (epi 1, O = 1024) with ssp_out also
+  // quantises its new rows times qn_w (the next RMSNorm's weight) per 32-block into qout / dout (unscaled f32 block
+  // scales) and writes per-token sum-of-squares partials ssp_out [M][32]; a GEMM with ssp != nullptr reads such rows
+  // (xq / xd) and applies rstd = 1/sqrtf(sum ssp / K + eps) to the block scales
+  const float* ssp; float* ssp_out; const float* qn_w;
 };
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);

@@ -538,10 +538,18 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
 // loads before its MFMAs (one memory round trip), and the residual is fetched before the hop. Splits merge by last
 // arriver (sc1 partials, MI355X_MICROARCH.md hand-off table row 1) with the KSM partial loads in flight together,
 // summed in split order (deterministic).
-template <int EPI, int NBW, int KSM>
+//
+// NRM (batched decode, K = 1024): the input rows come from the previous residual GEMM's epilogue (ssp_out below),
+// which quantised z = x * norm_w per 32-block (its tile is one q8_0 block of every token: xq, and the unscaled
+// f32 block scales d_z in xd) and left the per-token sum-of-squares partials ssp [M][32]. RMSNorm's per-token factor
+// rstd = 1/sqrtf(sum/K + eps) scales every block uniformly, so the q8_0 rows of y = (x * rstd) * w are the same
+// integers (up to float rounding at .5 ties) with scale f16(rstd * d_z): this GEMM only applies rstd, and the two
+// k_prep_q8 launches per layer (with their kernel boundaries) disappear.
+template <int EPI, int NBW, int KSM, bool NRM = false>
 __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
   constexpr int NS = EPI == 2 ? 2 : 1;
+  static_assert(!NRM || EPI != 1, "k_gemm_q8_sk: NRM inputs feed q|k|v, gate|up and the LM head");
   const int nb = K >> 5;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32, ks = blockIdx.z;
@@ -553,6 +561,11 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   const int t_b = min(t0 + r, a.M - 1);
   const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + bw0 * 32;
   KSTAMP(0);
+  float4 sv[NRM ? 8 : 1];
+  if constexpr (NRM) {  // this lane's token's 32 partials, issued first (vmcnt retires in issue order)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = *reinterpret_cast<const float4*>(a.ssp + (int64_t)t_b * 32 + 4 * i);
+  }
   i32x4_t A[NBW], B[NBW];
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
@@ -566,6 +579,17 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   float2 dx2[NBW / 2];
 #pragma unroll
   for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + bw0 + 2 * q);
+  if constexpr (NRM) {
+    float ss = 0.f;  // the producer's 32 tile partials in tile order
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss = (((ss + sv[i].x) + sv[i].y) + sv[i].z) + sv[i].w;
+    const float rstd = 1.0f / sqrtf(ss / (float)K + a.eps);
+#pragma unroll
+    for (int q = 0; q < NBW / 2; ++q) {
+      dx2[q].x = __half2float(__float2half_rn(rstd * dx2[q].x));
+      dx2[q].y = __half2float(__float2half_rn(rstd * dx2[q].y));
+    }
+  }
   // this thread finalises regs [4 g, 4 g + 4) of lane l (token col, rows rrow): residual fetched now, used after the hop
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6, col = l & 31, tok = t0 + col;
   float rv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -648,6 +672,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
     if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  float nv[4];  // EPI 1: the new residual values of this thread's 4 consecutive rows [8 g + 4 (l >> 5), +4)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int reg = 4 * g + q;
@@ -662,6 +687,40 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     }
     if (EPI == 2) s_act[col][rrow] = v;
     if (EPI == 3) s_act[col][rrow] = row < a.O ? v : -INFINITY;
+    nv[q] = rv[q] + y[q];
+  }
+  if (EPI == 1 && a.ssp_out) {
+    // the next NRM GEMM's input (its K = this GEMM's O = 1024): the tile is one q8_0 block of every token, so it
+    // quantises z = x_new * qn_w (block scale d_z = amax / 127 left unrounded in f32, dout) into qout, and leaves the
+    // rows' sum of squares (lane halves pair up, then the 4 waves in order) in ssp_out[tok][tile]
+    __shared__ float s_ssq[4][32], s_am[4][32];
+    const int rb = 8 * g + 4 * (l >> 5);
+    float z[4], am = 0.f, ssq = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ssq += nv[q] * nv[q];
+      z[q] = nv[q] * a.qn_w[o0 + rb + q];
+      am = fmaxf(am, fabsf(z[q]));
+    }
+    ssq += __shfl_xor(ssq, 32, 64);
+    am = fmaxf(am, __shfl_xor(am, 32, 64));
+    if (l < 32) {
+      s_ssq[g][l] = ssq;
+      s_am[g][l] = am;
+    }
+    __syncthreads();
+    const float amx = fmaxf(fmaxf(s_am[0][col], s_am[1][col]), fmaxf(s_am[2][col], s_am[3][col]));
+    const float d = amx / 127.0f;
+    const float id = d != 0.0f ? 1.0f / d : 0.0f;
+    const int b0 = (int)roundf(__fmul_rn(z[0], id)) & 0xFF, b1 = (int)roundf(__fmul_rn(z[1], id)) & 0xFF;
+    const int b2 = (int)roundf(__fmul_rn(z[2], id)) & 0xFF, b3 = (int)roundf(__fmul_rn(z[3], id)) & 0xFF;
+    if (tok < a.M) {
+      *reinterpret_cast<int32_t*>(a.qout + (int64_t)tok * 1024 + o0 + rb) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      if (threadIdx.x < 32) {
+        a.dout[(int64_t)tok * 32 + blockIdx.x] = d;
+        a.ssp_out[(int64_t)tok * 32 + blockIdx.x] = ((s_ssq[0][col] + s_ssq[1][col]) + s_ssq[2][col]) + s_ssq[3][col];
+      }
+    }
   }
   if (EPI == 3) {
     __syncthreads();
@@ -883,7 +942,7 @@ static void launch_gemv_fused(int K, int epi, const GemvArgs& a, hipStream_t s) 
 }
 
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
-  const bool fused = a.x != nullptr;
+  const bool fused = a.x != nullptr && a.ssp == nullptr;
   if (a.psum) {  // fused decode layer (M = 1): q|k|v (EPI 0) or the LM head (EPI 3) after a split down projection
     FA_REQUIRE(fused && a.M == 1 && K == 1024 && (epi == 0 || epi == 3), "gemv_q8: partial-sum prologue shape");
     if (epi == 0) launch_gemv<1, 1, true, 0, true>(a, s);
@@ -901,16 +960,28 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
-  if (g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
+  if (!a.ssp && g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
   int NBW, KS;
   gemm_sk_shape(a.O, a.M, K, epi, &NBW, &KS);
   FA_REQUIRE(NBW > 0, "gemm_q8: no split-K shape");
+  FA_REQUIRE(!a.ssp || (K == 1024 && epi != 1 && a.xq && a.xd),
+             "gemm_q8: rows normalised by their producer's epilogue need K 1024 (a residual GEMM cannot take them)");
+  FA_REQUIRE(!a.ssp_out || (epi == 1 && a.O == 1024 && a.qout && a.dout && a.qn_w),
+             "gemm_q8: the normalising residual epilogue needs O 1024, qout / dout and qn_w");
   if (KS > 1)
     FA_REQUIRE(a.kpart && a.kcnt && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) <= a.kcnt_n &&
                    (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) * KS * (epi == 2 ? 2 : 1) * 1024 <= a.kpart_n,
                "gemm_q8: split-K workspace too small");
   const dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
   const int ksm = KS == 1 ? 1 : KS <= 4 ? 4 : 16;
+  if (a.ssp) {  // batched decode (M <= 32): inputs quantised by the previous residual epilogue, rstd applied here
+    switch (epi * 1000 + NBW * 100 + ksm) {
+#define SKN(E, N, Q) case E * 1000 + N * 100 + Q: hipLaunchKernelGGL((k_gemm_q8_sk<E, N, Q, true>), grid, dim3(256), 0, s, a, K, KS); return;
+      SKN(0, 4, 4) SKN(0, 8, 1) SKN(2, 4, 4) SKN(3, 8, 1)
+#undef SKN
+      default: FA_REQUIRE(false, "gemm_q8: normalised-input shape not instantiated");
+    }
+  }
   switch (epi * 1000 + NBW * 100 + ksm) {
 #define SK(E, N, Q) case E * 1000 + N * 100 + Q: hipLaunchKernelGGL((k_gemm_q8_sk<E, N, Q>), grid, dim3(256), 0, s, a, K, KS); break;
     SK(0, 2, 1) SK(0, 2, 4) SK(0, 2, 16) SK(0, 4, 1) SK(0, 4, 4) SK(0, 4, 16) SK(0, 8, 1) SK(0, 8, 4) SK(0, 8, 16)
