@@ -125,6 +125,7 @@ struct Engine {
   __half *kcache = nullptr, *vcache = nullptr;
   int64_t seq_stride = 0, layer_stride = 0;
   int m_max = 0, n_part = 0, n_part_cur = 0;  // partial stride allocated / written by the last lm_head
+  int chunk_cur = 1;                            // rows per partial of the last lm_head
   float *lx = nullptr, *lqkv = nullptr, *lq = nullptr, *latt = nullptr, *lact = nullptr, *logits = nullptr;
   int8_t *lxq = nullptr, *lxq2 = nullptr;
   float *lxd = nullptr, *lxd2 = nullptr;
@@ -884,6 +885,7 @@ struct Engine {
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
     h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows);
+    chunk_cur = lm_head_chunk(lc.n_vocab, n_rows);
     if (gemv_small(n_rows)) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
     else if (nrm) { h.xq = lxq; h.xd = lxd; h.ssp = d_ssp; }  // rows from the last down epilogue
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
@@ -935,6 +937,7 @@ struct Engine {
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
     h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, 1);
+    chunk_cur = lm_head_chunk(lc.n_vocab, 1);
     h.x = fdw.xmid; h.ldx = E; h.norm_w = out_norm; h.psum = fdw.dpart;
     gemv(h, E, 3);
   }
@@ -1001,7 +1004,7 @@ struct Engine {
   }
   void sample(int M, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out, int* hist,
               const EmbedNext* en = nullptr) {
-    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, M, d_samp, row_seq, row_pos, step_ctr, tok_out,
+    sample_tokens(logits, lc.n_vocab, lc.n_vocab, pval, pidx, n_part_cur, chunk_cur, M, d_samp, row_seq, row_pos, step_ctr, tok_out,
                   hist, hist_max, en, stream);
   }
 };

@@ -165,10 +165,12 @@ struct SampleParams {
   int top_k;
   uint32_t seed;
 };
-// row_seq / row_pos [M]: sequence id and position of each row's token (the draw's counter: (seed, seq, pos))
-void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out,
-                   int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s);
+// row_seq / row_pos [M]: sequence id and position of each row's token (the draw's counter: (seed, seq, pos));
+// partial t of a row covers logits [chunk t, chunk (t + 1)) (the lm_head launch's rows per partial)
+void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int chunk,
+                   int M, const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr,
+                   int* tok_out, int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s);
+int lm_head_chunk(int O, int M);  // rows per argmax partial of the lm_head launch for M tokens
 void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s);
 void gpu_delay_us(int us, hipStream_t s);
 

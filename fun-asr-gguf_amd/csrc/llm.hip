@@ -994,6 +994,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
 }
 
 int lm_head_parts(int O, int M) { return gemv_small(M) ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
+int lm_head_chunk(int O, int M) { return gemv_small(M) ? gemv_rows_per_wave(O) : 32; }
 
 // ------------------------------------------------------------------------------------------------
 // q/k RMSNorm per head (attn_q_norm/attn_k_norm) + NEOX RoPE + KV-cache store (fp16).
@@ -1690,8 +1691,13 @@ __device__ uint32_t radix_select_desc(Get get, int n, T need, T* hist, int* s_di
   return prefix;
 }
 
+constexpr int SAMPLE_QCAP = 1024;  // fast path: chunks whose maximum reaches tau, scanned (else the whole row)
+constexpr int SAMPLE_RANK = 256;   // fast path: candidate lists up to this long are rank-sorted (else bitonic)
+
 struct SampleShared {
   unsigned long long list[SAMPLE_CAP];  // fast path: (~key << 32 | id), sorted ascending = logit desc, id asc
+  int qch[SAMPLE_QCAP];
+  int nq;
   float hist_f[256];
   int hist_i[256];
   float wf[SAMPLE_T / 64];
@@ -1704,7 +1710,7 @@ struct SampleShared {
 
 __global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ logits, int64_t ldl, int V,
                                                      const float* __restrict__ pval, const int* __restrict__ pidx,
-                                                     int n_part, const SampleParams* __restrict__ sp,
+                                                     int n_part, int chunk, const SampleParams* __restrict__ sp,
                                                      const int* __restrict__ row_seq, const int* __restrict__ row_pos,
                                                      int* __restrict__ step_ctr, int* __restrict__ tok_out,
                                                      int* __restrict__ tok_hist, int hist_stride, EmbedNext en) {
@@ -1756,17 +1762,38 @@ __global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ l
       // tau = k-th largest chunk maximum (keys staged in LDS, reusing the candidate list's space)
       uint32_t* pk = reinterpret_cast<uint32_t*>(S.list);
       for (int i = tid; i < n_part; i += SAMPLE_T) pk[i] = fkey(pval[(int64_t)m * n_part + i]);
-      if (tid == 0) S.cnt = 0;
+      if (tid == 0) { S.cnt = 0; S.nq = 0; }
       __syncthreads();
       const uint32_t tau = radix_select_desc<int>(
           [&](int i, uint32_t& key, int& w) { key = pk[i]; w = 1; return true; }, n_part, k, S.hist_i, &S.dig,
           &S.need_i);
-      // one pass over the row: every logit >= tau into the list (a superset of the top-k)
-      for (int i = tid; i < V; i += SAMPLE_T) {
-        const uint32_t key = fkey(lg[i]);
-        if (key >= tau) {
-          const int slot = atomicAdd(&S.cnt, 1);
-          if (slot < SAMPLE_CAP) S.list[slot] = ((unsigned long long)(~key) << 32) | (uint32_t)i;
+      // every logit >= tau lies in a chunk (rows [chunk t, chunk (t + 1)) of partial t) whose maximum is >= tau:
+      // gather those chunks (at least k of them, usually about k) and scan only their rows
+      for (int i = tid; i < n_part; i += SAMPLE_T)
+        if (pk[i] >= tau) {
+          const int slot = atomicAdd(&S.nq, 1);
+          if (slot < SAMPLE_QCAP) S.qch[slot] = i;
+        }
+      __syncthreads();
+      const int nq = S.nq;  // the chunk keys (in the list's space) are dead from here on
+      if (nq <= SAMPLE_QCAP) {
+        for (int p = tid; p < nq * chunk; p += SAMPLE_T) {
+          const int i = S.qch[p / chunk] * chunk + p % chunk;
+          if (i < V) {
+            const uint32_t key = fkey(lg[i]);
+            if (key >= tau) {
+              const int slot = atomicAdd(&S.cnt, 1);
+              if (slot < SAMPLE_CAP) S.list[slot] = ((unsigned long long)(~key) << 32) | (uint32_t)i;
+            }
+          }
+        }
+      } else {  // many tied chunk maxima: one pass over the row
+        for (int i = tid; i < V; i += SAMPLE_T) {
+          const uint32_t key = fkey(lg[i]);
+          if (key >= tau) {
+            const int slot = atomicAdd(&S.cnt, 1);
+            if (slot < SAMPLE_CAP) S.list[slot] = ((unsigned long long)(~key) << 32) | (uint32_t)i;
+          }
         }
       }
       __syncthreads();
@@ -1774,18 +1801,31 @@ __global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ l
     }
     if (fast) {
       const int c = S.cnt;
-      int P = 2;
-      while (P < c) P <<= 1;
-      for (int i = c + tid; i < P; i += SAMPLE_T) S.list[i] = ~0ull;
-      __syncthreads();
-      for (int size = 2; size <= P; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int i = tid; i < (P >> 1); i += SAMPLE_T) {
-            const int pos = 2 * i - (i & (stride - 1));
-            const unsigned long long x = S.list[pos], y = S.list[pos + stride];
-            if ((x > y) == ((pos & size) == 0)) { S.list[pos] = y; S.list[pos + stride] = x; }
+      if (c <= SAMPLE_RANK) {
+        // rank sort (entries are distinct: ids differ): entry t moves to its rank among the c entries, in one pass
+        unsigned long long x = 0;
+        int rank = 0;
+        if (tid < c) {
+          x = S.list[tid];
+          for (int j = 0; j < c; ++j) rank += S.list[j] < x;
+        }
+        __syncthreads();
+        if (tid < c) S.list[rank] = x;
+        __syncthreads();
+      } else {
+        int P = 2;
+        while (P < c) P <<= 1;
+        for (int i = c + tid; i < P; i += SAMPLE_T) S.list[i] = ~0ull;
+        __syncthreads();
+        for (int size = 2; size <= P; size <<= 1) {
+          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < (P >> 1); i += SAMPLE_T) {
+              const int pos = 2 * i - (i & (stride - 1));
+              const unsigned long long x = S.list[pos], y = S.list[pos + stride];
+              if ((x > y) == ((pos & size) == 0)) { S.list[pos] = y; S.list[pos + stride] = x; }
+            }
+            __syncthreads();
           }
-          __syncthreads();
         }
       }
       int nk = min(k, c);
@@ -1913,12 +1953,13 @@ __global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ l
   }
 }
 
-void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int M,
-                   const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr, int* tok_out,
-                   int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s) {
+void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int chunk,
+                   int M, const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr,
+                   int* tok_out, int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s) {
   FA_REQUIRE(!en || (step_ctr && en->tok_pos && en->qs && en->d && en->E % 32 == 0), "sample_tokens: embed-next args");
   FA_REQUIRE(d_params && row_seq && row_pos, "sample_tokens: params / row ids");
-  hipLaunchKernelGGL(k_sample, dim3(M), dim3(SAMPLE_T), 0, s, logits, ldl, V, pval, pidx, n_part, d_params, row_seq,
+  FA_REQUIRE(chunk >= 1 && (int64_t)chunk * n_part >= V, "sample_tokens: partial chunks must cover the row");
+  hipLaunchKernelGGL(k_sample, dim3(M), dim3(SAMPLE_T), 0, s, logits, ldl, V, pval, pidx, n_part, chunk, d_params, row_seq,
                      row_pos, step_ctr, tok_out, tok_hist, hist_stride, en ? *en : EmbedNext{});
 }
 

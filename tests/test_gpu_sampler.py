@@ -121,3 +121,28 @@ def test_fresh_draws_across_calls_and_sequences(eng, prompt):
     assert not np.array_equal(a[0], b[0]) and not np.array_equal(a[1], b[1])
     assert not np.array_equal(a[0], a[1])  # same seed, same positions, different sequences
     assert len(set(a[0].tolist() + b[0].tolist())) > 48
+
+
+def test_batched_membership_mfma_lm_head(prompt):
+    """8 sequences per step: the LM head runs on the MFMA GEMM (32-row argmax partials), so the fast path's chunk
+    gather walks 32-row chunks instead of the GEMV's; every row's draw stays in its own top-k / top-p set."""
+    from fun_asr_gguf import _native
+    e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=8), max_batch=1, max_samples=16000)
+    try:
+        e.synthetic_weights(0)
+        rng = np.random.default_rng(4)
+        for s in range(8):
+            e.llm_reset(s)
+            e.llm_prefill(s, prompt[: 4 + s] + (rng.standard_normal((4 + s, 1024)) * 0.05).astype(np.float32),
+                          temperature=0.0)
+        for step in range(6):
+            k, p = (5, 1.0) if step % 2 == 0 else (50, 0.3)
+            toks = e.llm_generate(list(range(8)), 1, temperature=1.3, top_k=k, top_p=p, seed=300 + step)
+            for s in range(8):
+                lg = e.llm_logits(s)
+                t = int(toks[s][0])
+                assert t in _topk_set(lg, k), (step, s, t)
+                if p < 1:
+                    assert t in _topp_set(lg, k, p), (step, s, t)
+    finally:
+        e.close()
