@@ -72,6 +72,110 @@ __device__ __forceinline__ void attn_store_tile(float* lds, int stage, const f4v
   }
 }
 
+// The block's epilogue, shared by the exact-f32 and the bf16x3 kernels: O^T (d on registers, q on lanes) -> LDS [q][d]
+// for row-contiguous stores; with key splits, publish (m, l, O) and let the last split merge.
+template <int D>
+__device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m_run, float l_run, float* lds,
+                                              float* __restrict__ O, int64_t ldo, int64_t row_base, int head, int q0,
+                                              int qt, int n_qt, int clip, int t_stride, int KS, int ks, int r16,
+                                              float* __restrict__ part, int* __restrict__ cnt, int lds_bytes) {
+  using L = AttnLds<D>;
+  constexpr int NDT = D / 32;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  float* s_m = lds + (lds_bytes - 2 * AQ * 4 - 16) / 4;  // [AQ] merged row max / sum (split path), past the O staging
+  float* s_l = s_m + AQ;
+  int* s_flag = reinterpret_cast<int*>(s_l + AQ);
+  float* so = lds;
+#pragma unroll
+  for (int i = 0; i < NDT; ++i)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int d = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h;
+      so[(wave * 32 + r) * L::OS + d] = o[i][t];
+    }
+  if (h == 0) {
+    s_m[wave * 32 + r] = m_run;
+    s_l[wave * 32 + r] = l_run;
+  }
+  __syncthreads();
+  constexpr int D4 = D / 4;
+  if (KS == 1) {
+    for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+      const int q = f / D4, d4 = f % D4;
+      if (q0 + q < t_stride) {
+        const float inv = 1.0f / s_l[q];
+        float4 v = *reinterpret_cast<const float4*>(so + q * L::OS + 4 * d4);
+        v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+        if (r16) v = round_f16x4(v);
+        *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+      }
+    }
+    return;
+  }
+  // ---- key split: publish (m, l, O) of this split; the last split merges
+  constexpr int PSZ = AQ * D + 2 * AQ;  // floats per split partial
+  const int tile = (clip * gridDim.y + head) * n_qt + qt;
+  float* pbase = part + (int64_t)tile * KS * PSZ;
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, KS * PSZ * 4);
+  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+    const int q = f / D4, d4 = f % D4;
+    const f4v v = *reinterpret_cast<const f4v*>(so + q * L::OS + 4 * d4);
+    st_sc1_f4(v, rs, (ks * PSZ + q * D + 4 * d4) * 4);
+  }
+  if (threadIdx.x < AQ / 2) {
+    const int q = threadIdx.x * 2;
+    const f4v v = {s_m[q], s_l[q], s_m[q + 1], s_l[q + 1]};
+    st_sc1_f4(v, rs, (ks * PSZ + AQ * D + 2 * q) * 4);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *s_flag = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
+  __syncthreads();
+  if (!*s_flag) return;
+  // merged max / sum per query and each split's weight exp(m_k - m) -> LDS (the O staging area is free now), with
+  // every split's (m, l) load in flight at once; then the weighted sum of the splits' O, KSM loads per output in
+  // flight (clamped duplicates past KS carry weight 0)
+  constexpr int KSM = 8;
+  float* s_w = lds;  // [KSM][AQ]
+  if (threadIdx.x < AQ) {
+    const int q = threadIdx.x;
+    f4v ml[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) ml[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + AQ * D + 2 * (q & ~1)) * 4);
+    float mm = -INFINITY;
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2)
+      if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
+    float ll = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) {
+      const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
+      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
+      ll += w * lk;
+      s_w[k2 * AQ + q] = w;
+    }
+    s_l[q] = ll;
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
+    const int q = f / D4, d4 = f % D4;
+    if (q0 + q >= t_stride) continue;
+    f4v pv[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
+    f4v acc = s_w[q] * pv[0];
+#pragma unroll
+    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
+    const float inv = 1.0f / s_l[q];
+    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (r16) v = round_f16x4(v);
+    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
@@ -83,9 +187,6 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
   constexpr int NDT = D / 32;  // output d-tiles
   constexpr int F4 = AK * D / 4 / 256;  // float4 per thread per tile (K or V)
   extern __shared__ float lds[];
-  float* s_m = lds + (L::BYTES - 2 * AQ * 4 - 16) / 4;  // [AQ] merged row max / sum (split path)
-  float* s_l = s_m + AQ;
-  int* s_flag = reinterpret_cast<int*>(s_l + AQ);
 
   const int n_qt = (t_stride + AQ - 1) / AQ;
   // splits of one (query tile, head, clip) sit 8*k block ids apart: the dispatcher deals blocks round-robin
@@ -181,95 +282,175 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
     __syncthreads();
   }
 
-  // ---- O^T (d on registers, q on lanes) -> LDS [q][d] for row-contiguous stores
-  float* so = lds;
+  attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, r16, part, cnt,
+                   L::BYTES);
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16x3 attention (f32 graph in the default bf16x3 GEMM mode): the same flash structure with both products on
+// v_mfma_f32_32x32x16_bf16 in split form (x y ~= xh yh + xh yl + xl yh, f32 accumulate, ~2^-16 relative per product;
+// 3 x 32 cycles per 32x32x16 step instead of 8 x 64 for the exact-f32 form):
+//   S^T = K . Q^T: A = K fragment (lane: key r, dims 16 s + 8 h + 0..7 of k-step s), B = Q^T (lane: query r, the same
+//     dims); Q is split once per block, K while staged (planes Kh, Kl [AK][D + 8]);
+//   O^T += V^T . P^T: B = P^T straight from the S accumulator (registers 8 s .. 8 s + 7 of lane half h are the keys
+//     16 s + 8 (j >> 2) + 4 h + (j & 3): cdna_hip_programming.md "accumulator tile as the next MFMA's operand"), split
+//     in registers; A = V^T fragment (lane: dim r, the same 8 keys) read as 8 f32 values from the exact kernel's V tile
+//     image (conflict-free, as there) and split in registers: a transposed bf16 V image costs 16-way conflicted
+//     2-byte LDS writes in the staging pass (measured at batch 32: 516 vs 412 us per call; exact f32: 679).
+//   Softmax, masking, key splits and the epilogue are the exact-f32 kernel's.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+template <int D>
+struct AttnLds3 {
+  static constexpr int SK = D + 8;                   // K plane row (bf16): 16-B reads of 16 rows, distinct bank groups
+  static constexpr int KP = AK * SK;                 // bf16 per K plane
+  static constexpr int VOFF = 2 * KP / 2;            // V tile offset (floats) after the Kh, Kl planes
+  static constexpr int STAGE = VOFF + AttnLds<D>::TILE;  // floats per stage
+  static constexpr int BYTES_PIPE = 2 * STAGE * 4;
+  static constexpr int BYTES_OUT = AttnLds<D>::BYTES_OUT;
+  static constexpr int BYTES = (BYTES_PIPE > BYTES_OUT ? BYTES_PIPE : BYTES_OUT) + 2 * AQ * 4 + 16;
+};
+
+template <int D>
+__device__ __forceinline__ void attn3_store_tile(float* st, const f4v (&pk)[AK * D / 1024], const f4v (&pv)[AK * D / 1024]) {
+  using L = AttnLds3<D>;
+  __bf16* kb = reinterpret_cast<__bf16*>(st);
+  float* vs_ = st + L::VOFF;
 #pragma unroll
-  for (int i = 0; i < NDT; ++i)
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int d = i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h;
-      so[(wave * 32 + r) * L::OS + d] = o[i][t];
-    }
-  if (h == 0) {
-    s_m[wave * 32 + r] = m_run;
-    s_l[wave * 32 + r] = l_run;
+  for (int c = 0; c < AK * D / 1024; ++c) {
+    const int f = threadIdx.x + 256 * c;
+    const int key = f / (D / 4), d4 = f % (D / 4);
+    const f4v v = pk[c];
+    const bf16x4 hi = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    const bf16x4 lo = {(__bf16)(v.x - (float)hi[0]), (__bf16)(v.y - (float)hi[1]), (__bf16)(v.z - (float)hi[2]),
+                       (__bf16)(v.w - (float)hi[3])};
+    *reinterpret_cast<bf16x4*>(kb + key * L::SK + 4 * d4) = hi;
+    *reinterpret_cast<bf16x4*>(kb + L::KP + key * L::SK + 4 * d4) = lo;
+    *reinterpret_cast<f4v*>(vs_ + key * AttnLds<D>::S + 4 * d4) = pv[c];
   }
-  __syncthreads();
-  constexpr int D4 = D / 4;
-  if (KS == 1) {
-    for (int f = threadIdx.x; f < AQ * D4; f += 256) {
-      const int q = f / D4, d4 = f % D4;
-      if (q0 + q < t_stride) {
-        const float inv = 1.0f / s_l[q];
-        float4 v = *reinterpret_cast<const float4*>(so + q * L::OS + 4 * d4);
-        v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
-        if (r16) v = round_f16x4(v);
-        *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, const float* __restrict__ Kp,
+                                                  const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
+                                                  float* __restrict__ O, int64_t ldo, int t_stride,
+                                                  const int* __restrict__ lens, float scale, int KS,
+                                                  float* __restrict__ part, int* __restrict__ cnt) {
+  using L = AttnLds3<D>;
+  constexpr int NDT = D / 32;
+  constexpr int NKS = D / 16;  // k-steps of the S product
+  extern __shared__ float lds[];
+  const int n_qt = (t_stride + AQ - 1) / AQ;
+  const int n_qt8 = (n_qt + 7) & ~7;
+  const int qt = blockIdx.x % n_qt8, ks = blockIdx.x / n_qt8, head = blockIdx.y, clip = blockIdx.z;
+  if (qt >= n_qt) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t row_base = (int64_t)clip * t_stride;
+  const int len = lens ? lens[clip] : t_stride;
+  const int q0 = qt * AQ;
+  const int n_kt = (t_stride + AK - 1) / AK;
+  const int tpk = (n_kt + KS - 1) / KS;
+  const int kt0 = ks * tpk, kt1 = min(n_kt, kt0 + tpk);
+  // this wave's 32 queries, pre-scaled (python: q * d_k**-0.5 before the dot), split into bf16 fragments
+  bf16x8 qh[NKS], ql[NKS];
+  {
+    const int q = min(q0 + wave * 32 + r, t_stride - 1);
+    const float* p = Q + (row_base + q) * ldq + head * D + 8 * h;
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      const float4 a = *reinterpret_cast<const float4*>(p + 16 * st);
+      const float4 b = *reinterpret_cast<const float4*>(p + 16 * st + 4);
+      const float x[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale, b.x * scale, b.y * scale, b.z * scale,
+                          b.w * scale};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qh[st][j] = (__bf16)x[j];
+        ql[st][j] = (__bf16)(x[j] - (float)qh[st][j]);
       }
     }
-    return;
   }
-  // ---- key split: publish (m, l, O) of this split; the last split merges
-  constexpr int PSZ = AQ * D + 2 * AQ;  // floats per split partial
-  const int tile = (clip * gridDim.y + head) * n_qt + qt;
-  float* pbase = part + (int64_t)tile * KS * PSZ;
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, KS * PSZ * 4);
-  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
-    const int q = f / D4, d4 = f % D4;
-    const f4v v = *reinterpret_cast<const f4v*>(so + q * L::OS + 4 * d4);
-    st_sc1_f4(v, rs, (ks * PSZ + q * D + 4 * d4) * 4);
+  f32x16 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.f;
+  f4v pk[AK * D / 1024], pv[AK * D / 1024];
+  if (kt0 < kt1) {
+    attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt0, pk, pv);
+    attn3_store_tile<D>(lds, pk, pv);
   }
-  if (threadIdx.x < AQ / 2) {
-    const int q = threadIdx.x * 2;
-    const f4v v = {s_m[q], s_l[q], s_m[q + 1], s_l[q + 1]};
-    st_sc1_f4(v, rs, (ks * PSZ + AQ * D + 2 * q) * 4);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    *s_flag = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
-  __syncthreads();
-  if (!*s_flag) return;
-  // merged max / sum per query and each split's weight exp(m_k - m) -> LDS (the O staging area is free now), with
-  // every split's (m, l) load in flight at once; then the weighted sum of the splits' O, KSM loads per output in
-  // flight (clamped duplicates past KS carry weight 0)
-  constexpr int KSM = 8;
-  float* s_w = lds;  // [KSM][AQ]
-  if (threadIdx.x < AQ) {
-    const int q = threadIdx.x;
-    f4v ml[KSM];
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int stage = (kt - kt0) & 1;
+    if (kt + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 1, pk, pv);  // in flight
+    const __bf16* kh_ = reinterpret_cast<const __bf16*>(lds + stage * L::STAGE);
+    const float* vs_ = lds + stage * L::STAGE + L::VOFF;
+    const int k0 = kt * AK;
+    f32x16 s = {};
 #pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) ml[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + AQ * D + 2 * (q & ~1)) * 4);
-    float mm = -INFINITY;
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2)
-      if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
-    float ll = 0.f;
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) {
-      const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
-      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
-      ll += w * lk;
-      s_w[k2 * AQ + q] = w;
+    for (int st = 0; st < NKS; ++st) {
+      const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kh_ + r * L::SK + 16 * st + 8 * h);
+      const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kh_ + L::KP + r * L::SK + 16 * st + 8 * h);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], s, 0, 0, 0);
     }
-    s_l[q] = ll;
-  }
-  __syncthreads();
-  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
-    const int q = f / D4, d4 = f % D4;
-    if (q0 + q >= t_stride) continue;
-    f4v pv[KSM];
+    // mask + online softmax (as k_attn_f32)
+    float mt = -INFINITY;
 #pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
-    f4v acc = s_w[q] * pv[0];
+    for (int t = 0; t < 16; ++t) {
+      const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
+      float v = s[t];
+      if (key >= t_stride) v = -INFINITY;
+      else if (key >= len) v = v + -10000.0f;
+      s[t] = v;
+      mt = fmaxf(mt, v);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+    float ls = 0.f;
 #pragma unroll
-    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
-    const float inv = 1.0f / s_l[q];
-    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
-    if (r16) v = round_f16x4(v);
-    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+    for (int t = 0; t < 16; ++t) {
+      const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
+      s[t] = p;
+      ls += p;
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) o[i] *= alpha;
+    // O^T[d][q] += V^T[d][key] P^T[key][q]: P^T k-step s2 = registers 8 s2 .. 8 s2 + 7 (keys 16 s2 + kl(j))
+#pragma unroll
+    for (int s2 = 0; s2 < AK / 16; ++s2) {
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ph[j] = (__bf16)s[8 * s2 + j];
+        pl[j] = (__bf16)(s[8 * s2 + j] - (float)ph[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) {
+        bf16x8 vh, vl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int key = 16 * s2 + 8 * (j >> 2) + 4 * h + (j & 3);
+          const float x = vs_[key * AttnLds<D>::S + i * 32 + r];
+          vh[j] = (__bf16)x;
+          vl[j] = (__bf16)(x - (float)vh[j]);
+        }
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o[i], 0, 0, 0);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o[i], 0, 0, 0);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o[i], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < kt1) attn3_store_tile<D>(lds + (stage ^ 1) * L::STAGE, pk, pv);
+    __syncthreads();
   }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, 0, part, cnt,
+                   L::BYTES);
 }
 
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
@@ -285,7 +466,7 @@ int attn_f32_splits(int batch, int t_stride, int n_heads) {
 
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s, int r16) {
+              const AttnF32Work& wk, hipStream_t s, int r16, int bf3) {
   const int KS = attn_f32_splits(batch, t_stride, n_heads);
   FA_REQUIRE(KS >= 1 && KS <= 8, "attn_f32: 1-8 key splits (16 measured slower: 60 vs 39 us at T = 1001)");
   const int n_tiles = cdiv(t_stride, AQ) * n_heads * batch;
@@ -297,9 +478,21 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
   const float scale = (float)std::pow((double)head_dim, -0.5);  // python d_k ** -0.5 rounded to f32
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<128>::BYTES);
-    hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<64>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<128>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<64>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<128>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<64>::BYTES);
     attr_set = true;
+  }
+  if (bf3 && !r16) {
+    FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
+    if (head_dim == 128)
+      hipLaunchKernelGGL(k_attn_bf3<128>, grid, dim3(256), AttnLds3<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    else
+      hipLaunchKernelGGL(k_attn_bf3<64>, grid, dim3(256), AttnLds3<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    return;
   }
   if (head_dim == 128) {
     hipLaunchKernelGGL(k_attn_f32<128>, grid, dim3(256), AttnLds<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,

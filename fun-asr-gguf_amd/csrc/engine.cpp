@@ -328,6 +328,7 @@ struct Engine {
     return it->second;
   }
   void weights_changed() { w16_stale = wb_stale = true; }
+  int bf3_attn() const { return !enc_fp16 && enc_gemm ? 1 : 0; }  // encoder attention products in the same mode
 
   EncBlockW sanm_block(const std::string& p, int d_in) {
     const int d = ec.d_model, f = ec.d_ffn, k = ec.fsmn_k;
@@ -695,7 +696,7 @@ struct Engine {
       hipEvent_t ev;
       prof_begin(2, &ev);
       attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.n_heads, d / ec.n_heads, lens,
-               enc_attn_wk, stream, r16());
+               enc_attn_wk, stream, r16(), bf3_attn());
       prof_end(2, 0, 4.0 * rows * (double)ts * d);
     }
     if (first) {
@@ -720,7 +721,7 @@ struct Engine {
         hipEvent_t ev;
         prof_begin(2, &ev);
         attn_f32(qkv, qkv + d_out, qkv + 2 * d_out, 3 * d_out, 3 * d_out, 3 * d_out, att, d_out, rows / ts, ts, n_heads,
-                 d_out / n_heads, lens, enc_attn_wk, stream, r16());
+                 d_out / n_heads, lens, enc_attn_wk, stream, r16(), bf3_attn());
         prof_end(2, 0, 4.0 * rows * (double)ts * d_out);
       }
       enc_lin(att, d_out, b.o_w, b.o_b, out, d_out, rows, d_out, d_out, 0, out, d_out);

@@ -65,7 +65,7 @@ constexpr int64_t ATTN_F32_COUNTERS = 512;
 int attn_f32_splits(int batch, int t_stride, int n_heads);
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s, int r16 = 0);
+              const AttnF32Work& wk, hipStream_t s, int r16 = 0, int bf3 = 0);  // bf3: bf16x3 split MFMA products
 
 // enc_misc.hip
 void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,

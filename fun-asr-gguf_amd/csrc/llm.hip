@@ -912,11 +912,12 @@ int gemm_k_splits(int O, int M, int K, int epi) {
   return ks;
 }
 
+int g_lm_rpw = 40;  // rows per wave of the vocabulary-wide GEMV (the LM head); multiple of 4
 int gemv_rows_per_wave(int O) {
   // target ~256-1024 blocks of 4 waves
   int rpw = (O + 4 * 256 - 1) / (4 * 256);
   if (rpw > 4) rpw = ((rpw + 3) / 4) * 4;
-  if (O >= 65536) rpw = 40;
+  if (O >= 65536) rpw = g_lm_rpw;
   return rpw < 1 ? 1 : rpw;
 }
 

@@ -15,7 +15,9 @@ void log(int, const std::string&) {}
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 using namespace fa;
 template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T))); return (T*)p; }
+namespace fa { extern int g_lm_rpw; }
 int main(int argc, char** argv) {
+  if (const char* g = getenv("FUNASR_LM_RPW")) fa::g_lm_rpw = atoi(g);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
   CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
