@@ -126,6 +126,7 @@ struct EpiLinear {
   int64_t ld2;
   int relu;
   int r16;            // fp16 mode: Gemm (+bias) output, then each Add, rounded to fp16
+  __device__ __forceinline__ void finish(int, int, int, int, float*) const {}  // after every apply of the block
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
@@ -150,6 +151,7 @@ struct EpiPower {
   float* P;
   int64_t ldp;
   int r16;
+  __device__ __forceinline__ void finish(int, int, int, int, float*) const {}  // after every apply of the block
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
@@ -171,6 +173,7 @@ struct EpiLog {
   float* C;
   int64_t ldc;
   int r16;
+  __device__ __forceinline__ void finish(int, int, int, int, float*) const {}  // after every apply of the block
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
@@ -190,6 +193,7 @@ struct EpiArgmax {
   int* pidx;
   int n_tiles;
   int r16;  // fp16 mode: argmax over fp16 logits (ties resolve to the first index, as on the rounded values)
+  __device__ __forceinline__ void finish(int, int, int, int, float*) const {}  // after every apply of the block
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int col = col0 + (lane & 31);
@@ -225,6 +229,54 @@ struct EpiArgmax {
         pval[(int64_t)row * n_tiles + tile] = v;
         pidx[(int64_t)row * n_tiles + tile] = i;
       }
+    }
+  }
+};
+
+// CTC projection + bias + row argmax over a 128x128 block's columns (2x2 waves x 2x2 accumulators): every apply
+// leaves its 32-column winners in LDS, finish merges the block's 4 column slices per row in column order ->
+// partial (value, index) per (row, 128-column tile).
+struct EpiArgmax128 {
+  const float* bias;
+  float* pval;   // [M][n_tiles]
+  int* pidx;
+  int n_tiles;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    const int lane = threadIdx.x & 63;
+    const int col = col0 + (lane & 31);
+    const float b = col < N ? bias[col] : 0.f;
+    float* sv = lds;                              // [128 rows][4 slices]
+    int* si = reinterpret_cast<int*>(lds + 512);  // [128][4]
+    const int slice = (col0 & 127) >> 5, rb = row0 & 127;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = col < N ? acc[r] + b : -INFINITY;
+      int i = col < N ? col : 0x7fffffff;
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) {
+        const float v2 = __shfl_xor(v, o, 32);
+        const int i2 = __shfl_xor(i, o, 32);
+        argmax_combine(v, i, v2, i2);
+      }
+      if ((lane & 31) == 0) {
+        const int lr = rb + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        sv[lr * 4 + slice] = v;
+        si[lr * 4 + slice] = i;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(int m0, int n0, int M, int N, float* lds) const {
+    const float* sv = lds;
+    const int* si = reinterpret_cast<const int*>(lds + 512);
+    __syncthreads();
+    if (threadIdx.x < 128 && m0 + (int)threadIdx.x < M) {
+      const int lr = threadIdx.x;
+      float v = sv[lr * 4];
+      int i = si[lr * 4];
+#pragma unroll
+      for (int c = 1; c < 4; ++c) argmax_combine(v, i, sv[lr * 4 + c], si[lr * 4 + c]);
+      pval[(int64_t)(m0 + lr) * n_tiles + n0 / 128] = v;
+      pidx[(int64_t)(m0 + lr) * n_tiles + n0 / 128] = i;
     }
   }
 };
@@ -346,6 +398,7 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+  epi.finish(m0, n0, M, N, smem);
 }
 
 template <class AL, class EPI, int WM, int WN, int KB = BK>
@@ -490,6 +543,7 @@ __global__ __launch_bounds__(256) void k_gemm_f16(AL al, const __half* __restric
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+  epi.finish(m0, n0, M, N, smem);
 }
 
 template <class AL, class EPI, int WM, int WN>
@@ -641,6 +695,7 @@ __global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restric
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+  epi.finish(m0, n0, M, N, smem);
 }
 
 // No K splits: the bf16x3 body is fast enough that the split-K seam (publish + ticket + combine, 5-13 us:
@@ -731,13 +786,18 @@ __global__ void k_argmax_final(const float* __restrict__ pval, const int* __rest
 
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
                      int* pidx, int* out, hipStream_t s, const __half* W16, WSplit wb) {
-  int n_tiles = cdiv(N, 64);
   ALoadPlain al{A, lda};
-  EpiArgmax epi{bias, pval, pidx, n_tiles, W16 ? 1 : 0};
-  // the argmax epilogue reduces 64-column blocks
-  if (W16) launch_gemm16<ALoadPlain, EpiArgmax, 1, 1>(al, W16, K, M, N, K, epi, s);
-  else if (wb.hi) launch_gemm_b3<ALoadPlain, EpiArgmax, 1, 1, 64>(al, wb, K, M, N, K, epi, s);
-  else run_gemm(al, W, K, M, N, K, epi, s, false);
+  int n_tiles = cdiv(N, 64);
+  if (wb.hi) {  // bf16x3: 128x128 blocks (one clip: 1001 x 60515 = 3784 tiles; 64x64 measured 606 us)
+    n_tiles = cdiv(N, 128);
+    EpiArgmax128 epi{bias, pval, pidx, n_tiles};
+    launch_gemm_b3<ALoadPlain, EpiArgmax128, 2, 2, 32>(al, wb, K, M, N, K, epi, s);
+  } else {
+    EpiArgmax epi{bias, pval, pidx, n_tiles, W16 ? 1 : 0};
+    // the argmax epilogue reduces 64-column blocks
+    if (W16) launch_gemm16<ALoadPlain, EpiArgmax, 1, 1>(al, W16, K, M, N, K, epi, s);
+    else run_gemm(al, W, K, M, N, K, epi, s, false);
+  }
   hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
 }
 
