@@ -575,7 +575,7 @@ static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N,
 // the f16 kernel's, so the same epilogues apply.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64
+int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves
 
 template <int WM, int WN, int KB>
 struct TileB3 {
@@ -592,9 +592,8 @@ template <class AL, int WM, int WN, int KB>
 __device__ __forceinline__ void load_b3(const AL& al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
                                         int64_t ldw, int m0, int n0, int k0, int M, int N, int K,
                                         float4 (&ra)[TileB3<WM, WN, KB>::NA], uint4 (&rh)[TileB3<WM, WN, KB>::NB],
-                                        uint4 (&rl)[TileB3<WM, WN, KB>::NB]) {
+                                        uint4 (&rl)[TileB3<WM, WN, KB>::NB], int t) {
   using T = TileB3<WM, WN, KB>;
-  const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
@@ -614,9 +613,8 @@ __device__ __forceinline__ void load_b3(const AL& al, const __bf16* __restrict__
 template <int WM, int WN, int KB>
 __device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<WM, WN, KB>::NA],
                                          const uint4 (&rh)[TileB3<WM, WN, KB>::NB],
-                                         const uint4 (&rl)[TileB3<WM, WN, KB>::NB]) {
+                                         const uint4 (&rl)[TileB3<WM, WN, KB>::NB], int t) {
   using T = TileB3<WM, WN, KB>;
-  const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
@@ -637,17 +635,21 @@ __device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<W
   }
 }
 
-template <class AL, class EPI, int WM, int WN, int KB>
-__global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                                  int64_t ldw, int M, int N, int K, EPI epi) {
+// KW = 2 (few-tile shapes): two groups of 4 waves per block split K in halves, each with its own LDS stages; group 1
+// hands its accumulators to group 0 through LDS (fixed order) and group 0 runs the epilogue. Twice the waves per CU
+// and half the dependent k-steps per wave, with no cross-block split-K seam.
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1>
+__global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                                       int64_t ldw, int M, int N, int K, EPI epi) {
   using T = TileB3<WM, WN, KB>;
   constexpr int LDK = T::LDK;
-  extern __shared__ float smem[];  // 2 stages; the epilogue reuses it
-  __bf16* sh = reinterpret_cast<__bf16*>(smem);
+  extern __shared__ float smem[];  // KW x 2 stages; the epilogue reuses it
   int tm, tn;
   if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
   const int m0 = tm * T::BM, n0 = tn * T::BN;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = KW > 1 ? (int)(threadIdx.x >> 8) : 0, t = threadIdx.x & 255;
+  __bf16* sh = reinterpret_cast<__bf16*>(smem) + grp * 2 * T::STAGE;
+  const int wave = t >> 6, lane = t & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[WM][WN];
@@ -657,13 +659,14 @@ __global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restric
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
   float4 ra[T::NA];
   uint4 rh[T::NB], rl[T::NB];
-  load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl);
-  store_b3<WM, WN, KB>(sh, ra, rh, rl);
+  const int kq = K / KW, kb0 = grp * kq, ke = kb0 + kq;  // host: K % (KW * KB) == 0 when KW > 1
+  load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0, M, N, ke, ra, rh, rl, t);
+  store_b3<WM, WN, KB>(sh, ra, rh, rl, t);
   __syncthreads();
-  const int nk = (K + KB - 1) / KB;
+  const int nk = (kq + KB - 1) / KB;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, (kt + 1) * KB, M, N, K, ra, rh, rl);
+    if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
     const __bf16* a = sh + cur * T::STAGE + (wr * 32 * WM + r) * LDK + 8 * h;
     const __bf16* b = sh + cur * T::STAGE + 2 * T::PA + (wc * 32 * WN + r) * LDK + 8 * h;
 #pragma unroll
@@ -688,8 +691,29 @@ __global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restric
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl);
+    if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
     __syncthreads();
+  }
+  if constexpr (KW > 1) {
+    float* xs = smem;  // [wave][i][j][16][64]: group 1's accumulators
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (grp == 1) xs[(((wave * WM + i) * WN + j) * 16 + q) * 64 + lane] = acc[i][j][q];
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[i][j][q] += xs[(((wave * WM + i) * WN + j) * 16 + q) * 64 + lane];
+    }
+    __syncthreads();  // the epilogue may reuse the LDS
+    if (grp == 1) return;
   }
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -701,20 +725,21 @@ __global__ __launch_bounds__(256) void k_gemm_bf3(AL al, const __bf16* __restric
 // No K splits: the bf16x3 body is fast enough that the split-K seam (publish + ticket + combine, 5-13 us:
 // MI355X_MICROARCH.md splitk-seam) costs more than it saves (one clip, measured: out N 512 K 512 10.8 -> 19.8 us,
 // ffn2 N 512 K 2048 32.6 -> 57 us with 2-4 splits).
-template <class AL, class EPI, int WM, int WN, int KB>
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1>
 static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                            hipStream_t s) {
   using T = TileB3<WM, WN, KB>;
   FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3: K and ldw must be multiples of 8");
+  FA_REQUIRE(KW == 1 || K % (KW * KB) == 0, "gemm_bf3: K groups need K % (KW * KB) == 0");
   const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM));
-  const size_t lds = std::max<size_t>(2 * T::STAGE * 2, 1024);  // >= EpiArgmax scratch
+  const size_t lds = std::max<size_t>(KW * 2 * T::STAGE * 2, 1024);  // >= EpiArgmax scratch
   static bool attr = false;
   if (!attr && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB>), grid, dim3(256), lds, s, al,
+  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW>), grid, dim3(256 * KW), lds, s, al,
                      reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
@@ -722,8 +747,11 @@ template <class AL, class EPI>
 static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
   const int f = g_gemm_bf3_force;
   const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
+  const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
   else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) launch_gemm_b3<AL, EPI, 1, 1, 64, 2>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2>(al, w, ldw, M, N, K, epi, s);
   else launch_gemm_b3<AL, EPI, 1, 1, 64>(al, w, ldw, M, N, K, epi, s);
 }
 

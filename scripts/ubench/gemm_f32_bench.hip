@@ -78,10 +78,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&Wh, (size_t)Nmax * Kmax * 2)); CK(hipMalloc(&Wl, (size_t)Nmax * Kmax * 2));
   launch_split_bf16(W, Wh, Wl, (int64_t)Nmax * Kmax, s);
   WSplit wb; wb.hi = Wh; wb.lo = Wl;
-  for (int sk = 0; sk < 2; ++sk) {  // bf16x3 spot checks (M=100 N=96 K=72; split-K M=70 N=64 K=2048): relative to sum |a w|
-    const int M = sk ? 70 : 100, N = sk ? 64 : 96, K = sk ? 2048 : 72;
-    for (int v : {1, 2, 3}) {
-      if (sk && v == 2) continue;
+  for (int sk = 0; sk < 3; ++sk) {  // bf16x3 spot checks (M=100 N=96 K=72; M=70 N=64 K=2048; K halves M=100 N=96 K=256)
+    const int M = sk == 1 ? 70 : 100, N = sk == 1 ? 64 : 96, K = sk == 1 ? 2048 : sk == 2 ? 256 : 72;
+    for (int v : {1, 2, 3, 4, 5}) {
+      if ((sk == 1 && v == 2) || (sk < 2 && v >= 4) || (sk == 2 && v < 4)) continue;
       g_gemm_bf3_force = v;
       gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s, nullptr, sk ? &wk : nullptr, wb);
       CK(hipStreamSynchronize(s));
@@ -94,7 +94,8 @@ int main(int argc, char** argv) {
         for (int k = 0; k < K; ++k) { r += (double)a[i * K + k] * w[j * K + k]; m += std::fabs((double)a[i * K + k] * w[j * K + k]); }
         err = std::max(err, std::fabs(r - c[i * N + j]) / m);
       }
-      printf("check bf16x3 variant %d%s: max|err|/sum|aw| %.3g %s\n", v, sk ? " split-K" : "", err, err < 3e-5 ? "ok" : "FAIL");
+      printf("check bf16x3 variant %d%s: max|err|/sum|aw| %.3g %s\n", v, sk == 1 ? " K 2048" : sk == 2 ? " K halves" : "", err,
+             err < 3e-5 ? "ok" : "FAIL");
     }
   }
   g_gemm_bf3_force = 0;
@@ -142,12 +143,13 @@ int main(int argc, char** argv) {
         const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K", "engine default"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
-      for (int v : {1, 3, 2, 0}) {
+      for (int v : {1, 3, 4, 5, 2, 0}) {
+        if ((v == 4 || v == 5) && (M > 2000 || sh.K % 128)) continue;
         g_gemm_bf3_force = v;
         const double us = time_graph([&] { gemm_linear(A, sh.K + pad, W, sh.K + pad, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
                                                        nullptr, &wk, wb); },
                                      M > 2000 ? 10 : 50);
-        const char* nm[] = {"bf3 default", "bf3 64x64x32", "bf3 128x128x32", "bf3 64x64x64"};
+        const char* nm[] = {"bf3 default", "bf3 64x64x32", "bf3 128x128x32", "bf3 64x64x64", "bf3 64x64x64 K/2", "bf3 64x64x32 K/2"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
       g_gemm_bf3_force = 0;
