@@ -142,7 +142,9 @@ void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* 
 // A lane owns one channel for FR consecutive rows: the FR + K - 1 input rows it needs are loaded once into
 // registers (a wave reads 64 consecutive channels = 256 B per row), the K taps stay in registers, and each output
 // row sums only inputs of its own clip that are inside the clip's valid length (the v*m mask + per-clip zero pad).
-constexpr int FSMN_K = 11, FSMN_R = 32;
+// FSMN_R rows per wave: 32 for batched encodes; 8 for one clip (T 1001 x 512 channels: 64 -> 256 blocks, 14 -> 5 us)
+constexpr int FSMN_K = 11;
+template <int FSMN_R>
 __global__ __launch_bounds__(256) void k_fsmn(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w,
                                               float* __restrict__ out, int64_t ldo, int rows, int C,
                                               const int* __restrict__ lens, int t_stride, int r16) {
@@ -177,8 +179,12 @@ __global__ __launch_bounds__(256) void k_fsmn(const float* __restrict__ v, int64
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
           const int* lens, int t_stride, hipStream_t s, int r16) {
   FA_REQUIRE(ksize == FSMN_K, "fsmn: kernel size 11 (SenseVoiceSmall sanm_shfit 0, kernel_size 11)");
-  dim3 grid(cdiv(C, 64), cdiv(rows, 4 * FSMN_R));
-  hipLaunchKernelGGL(k_fsmn, grid, dim3(256), 0, s, v, ldv, w, out, ldo, rows, C, lens, t_stride, r16);
+  if ((int64_t)cdiv(C, 64) * cdiv(rows, 4 * 32) >= 512)
+    hipLaunchKernelGGL(k_fsmn<32>, dim3(cdiv(C, 64), cdiv(rows, 4 * 32)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
+                       lens, t_stride, r16);
+  else
+    hipLaunchKernelGGL(k_fsmn<8>, dim3(cdiv(C, 64), cdiv(rows, 4 * 8)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
+                       lens, t_stride, r16);
 }
 
 // ---------------- C2: CTC greedy collapse (nano_ctc.py:65-104): keep frame i iff id != blank and
