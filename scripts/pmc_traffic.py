@@ -10,14 +10,26 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-# algorithmic q8_0 weight bytes per launch for the Qwen3-0.6B decode GEMVs (34 B per 32 weights)
+# algorithmic q8_0 weight bytes per launch for the Qwen3-0.6B decode launches (34 B per 32 weights). The batch-1
+# step runs the fused 3-launch layer: A = q|k|v GEMV with the partial-sum prologue, B = attention + o slice
+# (k_attn_o: Wo only here, its K/V bytes are not weights), C = gate|up + SwiGLU + down slice (k_ffn_fused); the
+# 5-launch layer's GEMVs (fa_set_decode_fused(0)) are listed too. Names as rocprofv3 prints them.
+QKV, O, GU, DOWN = 4096 * 1024 * 34 / 32, 1024 * 2048 * 34 / 32, 2 * 3072 * 1024 * 34 / 32, 1024 * 3072 * 34 / 32
 ALGO = {
-    "k_gemv_q8<1, 1, true, 0>": 4096 * 1024 * 34 / 32,        # q|k|v
-    "k_gemv_q8<2, 1, true, 1>": 1024 * 2048 * 34 / 32,        # o-proj
-    "k_gemv_q8<1, 1, true, 2>": 2 * 3072 * 1024 * 34 / 32,    # gate|up
-    "k_gemv_q8<3, 1, true, 1>": 1024 * 3072 * 34 / 32,        # down
-    "k_gemv_q8<1, 1, true, 3>": 151936 * 1024 * 34 / 32,      # lm_head
+    "k_gemv_q8<1, 1, true, 0, true>": QKV,      # A: q|k|v (fused layer)
+    "k_ffn_fused(": GU + DOWN,                 # C: gate|up + down (fused layer)
+    "k_attn_o(": O,                            # B: o projection slice weights
+    "k_gemv_q8<1, 1, true, 0, false>": QKV,     # 5-launch layer
+    "k_gemv_q8<2, 1, true, 1, false>": O,
+    "k_gemv_q8<1, 1, true, 2, false>": GU,
+    "k_gemv_q8<3, 1, true, 1, false>": DOWN,
+    "k_gemv_q8<1, 1, true, 3, true>": 151936 * 1024 * 34 / 32,   # lm_head (fused layer's partial-sum prologue)
+    "k_gemv_q8<1, 1, true, 3, false>": 151936 * 1024 * 34 / 32,  # lm_head
 }
+# the bench's dominant class "q8_0 GEMV/GEMM (decoder layers)" = the weight-streaming layer launches A and C
+# (B is the "decode attention" class): their mean is what roofline.traffic reports
+LAYER_CLASS = ("k_gemv_q8<1, 1, true, 0, true>", "k_ffn_fused(", "k_gemv_q8<1, 1, true, 0, false>",
+               "k_gemv_q8<1, 1, true, 2, false>", "k_gemv_q8<2, 1, true, 1, false>", "k_gemv_q8<3, 1, true, 1, false>")
 
 
 def main():
@@ -36,9 +48,10 @@ def main():
         m = sum(vals) / len(vals)
         res[key] = {"launches": len(vals), "fetch_kb_mean": m, "traffic_bytes": 2 * m * 1024,
                     "algorithmic_bytes": ALGO[key], "traffic_over_algorithmic": 2 * m * 1024 / ALGO[key]}
-    tot_t = sum(v["traffic_bytes"] * v["launches"] for k, v in res.items() if "true, 3" not in k)
-    tot_n = sum(v["launches"] for k, v in res.items() if "true, 3" not in k)
-    tot_a = sum(v["algorithmic_bytes"] * v["launches"] for k, v in res.items() if "true, 3" not in k)
+    cls = {k: v for k, v in res.items() if k in LAYER_CLASS}
+    tot_t = sum(v["traffic_bytes"] * v["launches"] for v in cls.values())
+    tot_n = sum(v["launches"] for v in cls.values())
+    tot_a = sum(v["algorithmic_bytes"] * v["launches"] for v in cls.values())
     res["decode_layer_gemv_mean"] = {"launches": tot_n, "traffic_bytes": tot_t / max(1, tot_n),
                                      "algorithmic_bytes": tot_a / max(1, tot_n)}
     json.dump(res, open(out, "w"), indent=1)
