@@ -125,6 +125,9 @@ struct Engine {
   __half *kcache = nullptr, *vcache = nullptr;
   int64_t seq_stride = 0, layer_stride = 0;
   int m_max = 0, n_part = 0, n_part_cur = 0;  // partial stride allocated / written by the last lm_head
+  int pf_max = 0;                               // row capacity of one forward (multi-sequence prefill batches)
+  float* lxg = nullptr;                         // gathered last rows of a prefill batch
+  int* d_lastrow = nullptr;
   int chunk_cur = 1;                            // rows per partial of the last lm_head
   float *lx = nullptr, *lqkv = nullptr, *lq = nullptr, *latt = nullptr, *lact = nullptr, *logits = nullptr;
   int8_t *lxq = nullptr, *lxq2 = nullptr;
@@ -586,38 +589,44 @@ struct Engine {
     // decoder
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim;
     m_max = std::max(lc.n_ctx, lc.max_seqs);
+    // rows of one forward: a single prefill (n_ctx), a decode step (max_seqs), or a multi-sequence prefill batch
+    // (fa_llm_prefill_batch: up to 8192 rows, ~55 KB of activations per row)
+    pf_max = lc.max_seqs > 1 ? std::max(m_max, std::min(lc.max_seqs * lc.n_ctx, 8192)) : m_max;
     seq_stride = (int64_t)lc.n_ctx * KV * D;
     layer_stride = seq_stride * lc.max_seqs;
     kcache = alloc<__half>((size_t)layer_stride * lc.n_layer);
     vcache = alloc<__half>((size_t)layer_stride * lc.n_layer);
-    lx = alloc<float>((size_t)m_max * E);
-    lqkv = alloc<float>((size_t)m_max * (H + 2 * KV) * D);
-    lq = alloc<float>((size_t)m_max * H * D);
-    latt = alloc<float>((size_t)m_max * H * D);
-    lact = alloc<float>((size_t)m_max * lc.n_ff);
+    lx = alloc<float>((size_t)pf_max * E);
+    lqkv = alloc<float>((size_t)pf_max * (H + 2 * KV) * D);
+    lq = alloc<float>((size_t)pf_max * H * D);
+    latt = alloc<float>((size_t)pf_max * H * D);
+    lact = alloc<float>((size_t)pf_max * lc.n_ff);
     const int kmax = std::max({E, H * D, lc.n_ff});
-    lxq = alloc<int8_t>((size_t)m_max * kmax);
-    lxd = alloc<float>((size_t)m_max * kmax / 32);
-    lxq2 = alloc<int8_t>((size_t)m_max * kmax);  // q8_0 rows produced by epilogues (attention out, SwiGLU act)
-    lxd2 = alloc<float>((size_t)m_max * kmax / 32);
+    lxq = alloc<int8_t>((size_t)pf_max * kmax);
+    lxd = alloc<float>((size_t)pf_max * kmax / 32);
+    lxq2 = alloc<int8_t>((size_t)pf_max * kmax);  // q8_0 rows produced by epilogues (attention out, SwiGLU act)
+    lxd2 = alloc<float>((size_t)pf_max * kmax / 32);
+    lxg = alloc<float>((size_t)lc.max_seqs * E);   // prefill batch: the last row of each sequence (LM head input)
+    d_lastrow = alloc<int>(lc.max_seqs);
     logits = alloc<float>((size_t)lc.max_seqs * lc.n_vocab);
     n_part = std::max(lm_head_parts(lc.n_vocab, 1), lm_head_parts(lc.n_vocab, lc.max_seqs));
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
     d_ssp = alloc<float>((size_t)lc.max_seqs * 32);
 
-    d_tok_seq = alloc<int>(m_max);
-    d_tok_pos = alloc<int>(m_max);
+    d_tok_seq = alloc<int>(pf_max);
+    d_tok_pos = alloc<int>(pf_max);
     d_step = alloc<int>(m_max);
     d_tok_cur = alloc<int>(lc.max_seqs);
     hist_max = 4096;
     d_tok_hist = alloc<int>((size_t)lc.max_seqs * hist_max);
     d_ids = alloc<int>(m_max);
     d_samp = alloc<SampleParams>(1);
-    attn_wk.max_tokens = m_max;
+    attn_wk.max_tokens = pf_max;
+    attn_wk.max_split_tokens = m_max;
     attn_wk.max_kv = KV;
-    attn_wk.counters = alloc<int>((size_t)m_max * KV * CNT_LINE);
-    FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)m_max * KV * CNT_LINE * sizeof(int)));
+    attn_wk.counters = alloc<int>((size_t)pf_max * KV * CNT_LINE);
+    FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)pf_max * KV * CNT_LINE * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
     fdw.opart = alloc<float>((size_t)FUSED_PARTS * E);
     fdw.dpart = alloc<float>((size_t)FUSED_PARTS * E);
@@ -804,7 +813,8 @@ struct Engine {
 
   // ---------------------------------------------------------------------------------------------
   // decoder forward over M token rows (embeddings already in lx, positions in d_tok_pos)
-  void llm_forward(int M, bool decode, int max_pos) {
+  // n_last > 0 (prefill batch): logits for rows d_lastrow[0 .. n_last) (each sequence's last prompt row)
+  void llm_forward(int M, bool decode, int max_pos, int n_last = 0) {
     // decode: every row is a different sequence (continuous batch), logits for all rows;
     // prefill: rows are consecutive positions of one sequence, logits for the last row only.
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
@@ -878,9 +888,14 @@ struct Engine {
       gemv(dn, F, 1);
     }
     prof_sample = true;
-    // lm_head (tied token_embd) with fused argmax partials: all rows (decode) or the last row (prefill)
-    const int n_rows = decode ? M : 1;
+    // lm_head (tied token_embd) with fused argmax partials: all rows (decode), the last row (prefill) or each
+    // sequence's last row (prefill batch)
+    const int n_rows = decode ? M : n_last > 0 ? n_last : 1;
     const float* xrow = decode ? lx : lx + (size_t)(M - 1) * E;
+    if (!decode && n_last > 0) {
+      gather_rows(lx, d_lastrow, n_last, E, lxg, stream);
+      xrow = lxg;
+    }
     GemvArgs h{};
     h.M = n_rows; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
@@ -1370,6 +1385,66 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   e->logits_row[seq] = 0;
   if (tok_out) *tok_out = tok;
+  FA_API_END
+}
+
+int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, const float* embd, const int32_t* n_tokens,
+                         const fa_sampling* s, int32_t* tok_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs, "prefill batch: n_seqs out of range");
+  const int E = e->lc.n_embd;
+  std::vector<char> seen(e->lc.max_seqs, 0);
+  int64_t total = 0;
+  for (int i = 0; i < n_seqs; ++i) {
+    const int q = seqs[i];
+    FA_REQUIRE(q >= 0 && q < e->lc.max_seqs && !seen[q], "prefill batch: sequence ids must be distinct and in range");
+    seen[q] = 1;
+    FA_REQUIRE(n_tokens[i] >= 1 && n_tokens[i] <= e->pf_max && e->n_past[q] + n_tokens[i] <= e->lc.n_ctx,
+               "prefill batch: prompt exceeds n_ctx or the row capacity");
+    total += n_tokens[i];
+  }
+  e->set_sampling(s);
+  // sequences in order, as many per forward as the row capacity holds; one weight pass per forward
+  int64_t off = 0;
+  for (int i0 = 0; i0 < n_seqs;) {
+    int i1 = i0, rows = 0;
+    while (i1 < n_seqs && rows + n_tokens[i1] <= e->pf_max) rows += n_tokens[i1++];
+    const int n = i1 - i0;
+    std::vector<int> sq(rows), ps(rows), last(n), lseq(n), lpos(n);
+    for (int i = i0, r = 0; i < i1; ++i) {
+      for (int t = 0; t < n_tokens[i]; ++t, ++r) {
+        sq[r] = seqs[i];
+        ps[r] = e->n_past[seqs[i]] + t;
+      }
+      last[i - i0] = r - 1;
+      lseq[i - i0] = seqs[i];
+      lpos[i - i0] = ps[r - 1];
+    }
+    FA_HIP(hipMemcpyAsync(e->lx, embd + off * E, (size_t)rows * E * 4, hipMemcpyHostToDevice, e->stream));
+    FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
+    FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
+    FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    e->llm_forward(rows, false, 0, n);
+    // each first token's draw is keyed by its sequence's last prompt row (seq, position), as fa_llm_prefill's
+    FA_HIP(hipMemcpyAsync(e->d_ids, lseq.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    FA_HIP(hipMemcpyAsync(e->d_step, lpos.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    e->sample(n, e->d_ids, e->d_step, nullptr, e->d_tok_cur, nullptr);
+    std::vector<int> tok(n);
+    FA_HIP(hipMemcpyAsync(tok.data(), e->d_tok_cur, n * 4, hipMemcpyDeviceToHost, e->stream));
+    FA_HIP(hipStreamSynchronize(e->stream));
+    e->prof_collect();
+    std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
+    for (int i = i0; i < i1; ++i) {
+      e->n_past[seqs[i]] += n_tokens[i];
+      e->last_tok[seqs[i]] = tok[i - i0];
+      e->logits_row[seqs[i]] = i - i0;
+      if (tok_out) tok_out[i] = tok[i - i0];
+    }
+    off += rows;
+    i0 = i1;
+  }
+  (void)total;
   FA_API_END
 }
 

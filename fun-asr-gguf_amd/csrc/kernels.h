@@ -121,8 +121,9 @@ void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const floa
 
 struct AttnWork {
   int* counters = nullptr;    // [max_tokens][max_kv][CNT_LINE]
-  float* partials = nullptr;  // [max_tokens][max_kv][ATTN_SPLITS][ATTN_PART_FLOATS]
+  float* partials = nullptr;  // [max_split_tokens][max_kv][ATTN_SPLITS][ATTN_PART_FLOATS]
   int max_tokens = 0, max_kv = 0;
+  int max_split_tokens = 0;   // launches with more rows than this run unsplit (large prefill batches always do)
 };
 // qout/dout (optional): the output rows also as q8_0 blocks (the o GEMM's pre-quantised input, no prep launch)
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
@@ -148,6 +149,8 @@ void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps,
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s);
+// dst[i] = src[rows[i]] (n rows of E floats; row stride E both sides)
+void gather_rows(const float* src, const int* rows, int n, int E, float* dst, hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 // Decode-step tail fused into the sampler: embedding row of the sampled token -> x (the next step's input), and

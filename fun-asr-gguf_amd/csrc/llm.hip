@@ -1547,6 +1547,7 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // K/V stream of 512 (sequence, kv head) pairs comes in at ~2.8 TB/s whatever the block shape.
   int ns = 1;
   while (ns < ASPLIT && (ns + 1) * M * KV <= g_attn_blocks) ++ns;
+  FA_REQUIRE(ns == 1 || M <= wk.max_split_tokens, "attn_block: split partials workspace too small");
   const bool lean = g_attn_lean >= 0 ? g_attn_lean != 0 : M * KV * ns > 3 * 256;
   auto kern = lean ? (decode_mode ? k_attn_block<1, 1> : k_attn_block<0, 1>)
                    : (decode_mode ? k_attn_block<1, 0> : k_attn_block<0, 0>);
@@ -1567,6 +1568,18 @@ __global__ void k_embed(const int8_t* __restrict__ qs, const __half* __restrict_
   float v = dv * (float)qs[row * E + i];
   if (fp16_round) v = __half2float(__float2half_rn(v));
   out[(int64_t)m * E + i] = v;
+}
+
+__global__ void k_gather_rows(const float* __restrict__ src, const int* __restrict__ rows, int E, float* __restrict__ dst) {
+  const int m = blockIdx.y;
+  const int64_t r = rows[m];
+  for (int i = (blockIdx.x * blockDim.x + threadIdx.x) * 4; i < E; i += gridDim.x * blockDim.x * 4)
+    *reinterpret_cast<float4*>(dst + (int64_t)m * E + i) = *reinterpret_cast<const float4*>(src + r * E + i);
+}
+
+void gather_rows(const float* src, const int* rows, int n, int E, float* dst, hipStream_t s) {
+  FA_REQUIRE(E % 4 == 0, "gather_rows: E % 4");
+  if (n > 0) hipLaunchKernelGGL(k_gather_rows, dim3(1, n), dim3(256), 0, s, src, rows, E, dst);
 }
 
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,

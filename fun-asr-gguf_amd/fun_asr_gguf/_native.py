@@ -15,7 +15,7 @@ EXPORTS = [
     "fa_engine_create", "fa_engine_destroy", "fa_last_error", "fa_set_log_callback", "fa_weights_synthetic",
     "fa_set_tensor_f32", "fa_set_tensor_q8_0", "fa_load_gguf", "fa_get_tensor_q8_0", "fa_encode",
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
-    "fa_llm_reset", "fa_llm_prefill", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
+    "fa_llm_reset", "fa_llm_prefill", "fa_llm_prefill_batch", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
@@ -79,6 +79,7 @@ def load():
     lib.fa_llm_reset.argtypes = [P, I32]
     lib.fa_llm_prefill.argtypes = [P, I32, P, I32, ctypes.POINTER(Sampling), P, P]
     lib.fa_llm_generate.argtypes = [P, P, I32, I32, ctypes.POINTER(Sampling), P]
+    lib.fa_llm_prefill_batch.argtypes = [P, P, I32, P, P, ctypes.POINTER(Sampling), P]
     lib.fa_llm_logits.argtypes = [P, I32, P]
     lib.fa_llm_n_past.argtypes = [P, I32, P]
     lib.fa_profile_enable.argtypes = [P, I32]
@@ -273,6 +274,17 @@ class Engine:
         _check(self.lib.fa_llm_prefill(self.h, seq, _ptr(e), e.shape[0], ctypes.byref(s), ctypes.byref(tok), _ptr(lg)),
                "fa_llm_prefill")
         return (tok.value, lg) if want_logits else tok.value
+
+    def llm_prefill_batch(self, seqs, embds, **samp):
+        """Prefill several sequences in shared forwards (fa_llm_prefill_batch); -> first tokens, one per sequence."""
+        seqs = np.ascontiguousarray(seqs, dtype=np.int32)
+        n = np.array([e.shape[0] for e in embds], np.int32)
+        e = np.ascontiguousarray(np.concatenate(embds, 0), dtype=np.float32)
+        tok = np.zeros(len(seqs), np.int32)
+        s = self._sampling(**samp)
+        _check(self.lib.fa_llm_prefill_batch(self.h, _ptr(seqs), len(seqs), _ptr(e), _ptr(n), ctypes.byref(s), _ptr(tok)),
+               "fa_llm_prefill_batch")
+        return tok.tolist()
 
     def llm_generate(self, seqs, n_steps, **samp):
         sq = np.ascontiguousarray(seqs, dtype=np.int32)

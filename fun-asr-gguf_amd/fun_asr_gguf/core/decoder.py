@@ -97,12 +97,16 @@ class LLMDecoder:
         cfg = self.models.config
         samp = self._sampling(temperature, top_p, top_k)
         states, res = [], []
-        for s, e in enumerate(embds):
-            r = LLMDecodeResult()
-            t0 = time.perf_counter()
+        t0 = time.perf_counter()
+        for s in range(len(embds)):
             eng.llm_reset(s)
-            first = eng.llm_prefill(s, e, **samp)
-            r.t_inject = time.perf_counter() - t0
+        # one prompt: llama_decode of its batch; several: their prompts share forwards (one weight pass per forward)
+        firsts = [eng.llm_prefill(0, embds[0], **samp)] if len(embds) == 1 else \
+            eng.llm_prefill_batch(list(range(len(embds))), embds, **samp)
+        t_inject = (time.perf_counter() - t0) / len(embds)
+        for s, first in enumerate(firsts):
+            r = LLMDecodeResult()
+            r.t_inject = t_inject
             st = _SeqState(self.models.vocab, n_predict, self.models.eos_token, cfg.ignore_eos,
                            reporter if stream_output and len(embds) == 1 else None)
             st.feed([first])

@@ -129,6 +129,13 @@ int fa_llm_reset(fa_engine* e, int32_t seq);
  * token with `s`. logits_out (nullable) receives the last-row logits [n_vocab]. */
 int fa_llm_prefill(fa_engine* e, int32_t seq, const float* embd, int32_t n_tokens, const fa_sampling* s,
                    int32_t* tok_out, float* logits_out);
+/* fa_llm_prefill for n_seqs sequences (distinct ids) at once: embd holds their prompts back to back
+ * [sum n_tokens, n_embd], n_tokens[i] rows for seqs[i]. As many sequences as fit the row capacity share one
+ * forward (one pass over the weights instead of one per sequence; each row attends its own sequence's keys), then
+ * every sequence samples its first token keyed on its own (seq, last position): tok_out [n_seqs]. Replaces the
+ * per-sequence llama_decode of a prompt batch (decoder.py:70-80 run per stream). */
+int fa_llm_prefill_batch(fa_engine* e, const int32_t* seqs, int32_t n_seqs, const float* embd, const int32_t* n_tokens,
+                         const fa_sampling* s, int32_t* tok_out);
 /* Run n_steps decode steps for n_seqs sequences (distinct ids) in one continuous batch: each step feeds
  * every sequence's last sampled token at its next position and samples the next one on device
  * (decoder.py:91-98). tokens_out [n_seqs, n_steps]. No host round trip inside the call. */

@@ -17,7 +17,7 @@ template <class T> T* dalloc(size_t n) { void* p; CK(hipMalloc(&p, n * sizeof(T)
 int main(int argc, char** argv) {
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int M = 32, H = 16, KV = 8, D = 128, NCTX = argc > 1 ? atoi(argv[1]) : 1024, L = 28, QKV = (H + 2 * KV) * D;
-  AttnWork wk; wk.max_tokens = M; wk.max_kv = KV;
+  AttnWork wk; wk.max_tokens = M; wk.max_split_tokens = M; wk.max_kv = KV;
   CK(hipMalloc(&wk.counters, (size_t)M * KV * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, (size_t)M * KV * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, (size_t)M * KV * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int64_t seq_stride = (int64_t)NCTX * KV * D;  // per sequence per layer

@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
   if (const char* e = getenv("FUNASR_ATTN_LEAN")) g_attn_lean = atoi(e);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int H = 16, KV = 8, D = 128, NCTX = 1024, QKV = 4096;
-  AttnWork wk; wk.max_tokens = M; wk.max_kv = KV;
+  AttnWork wk; wk.max_tokens = M; wk.max_split_tokens = M; wk.max_kv = KV;
   CK(hipMalloc(&wk.counters, (size_t)M * KV * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, (size_t)M * KV * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, (size_t)M * KV * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int64_t seq_stride = (int64_t)NCTX * KV * D;

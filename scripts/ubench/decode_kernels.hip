@@ -30,7 +30,7 @@ static double time_graph(const char* name, std::function<void()> f, int reps = 2
 }
 int main() {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
+  AttnWork wk; wk.max_tokens = 1; wk.max_split_tokens = 1; wk.max_kv = 8;
   CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048;
@@ -120,7 +120,7 @@ int main() {
   }
   {  // batch-32 decode attention: 32 sequences at n_past 330
     const int M = 32;
-    AttnWork wb; wb.max_tokens = M; wb.max_kv = 8;
+    AttnWork wb; wb.max_tokens = M; wb.max_split_tokens = M; wb.max_kv = 8;
     CK(hipMalloc(&wb.counters, M * 8 * 4)); CK(hipMemset(wb.counters, 0, M * 8 * 4));
     CK(hipMalloc(&wb.partials, (size_t)M * 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
     __half* kb = dalloc<__half>((size_t)M * NCTX * KV * D); __half* vb = dalloc<__half>((size_t)M * NCTX * KV * D);

@@ -19,7 +19,7 @@ namespace fa { extern int g_lm_rpw; }
 int main(int argc, char** argv) {
   if (const char* g = getenv("FUNASR_LM_RPW")) fa::g_lm_rpw = atoi(g);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  AttnWork wk; wk.max_tokens = 1; wk.max_kv = 8;
+  AttnWork wk; wk.max_tokens = 1; wk.max_split_tokens = 1; wk.max_kv = 8;
   CK(hipMalloc(&wk.counters, 8 * CNT_LINE * 4)); CK(hipMemset(wk.counters, 0, 8 * CNT_LINE * 4));
   CK(hipMalloc(&wk.partials, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 4));
   const int E = 1024, H = 16, KV = 8, D = 128, F = 3072, V = 151936, QKV = (H + 2 * KV) * D, NCTX = 2048, L = 28;

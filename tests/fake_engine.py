@@ -1,5 +1,5 @@
 """Host stand-in for fun_asr_gguf._native.Engine (no GPU): the surface StreamDecoder / TranscriptionOrchestrator use
-(encode, ctc_collapse, embd_rows, llm_reset / llm_prefill / llm_generate), deterministic in each clip's own samples
+(encode, ctc_collapse, embd_rows, llm_reset / llm_prefill(_batch) / llm_generate), deterministic in each clip's own samples
 and independent of how clips are batched, so a sharded run must equal a single-rank run exactly. Lets the real
 orchestration code (windows, LPT sharding, record gather, merge) run in multi-process CPU tests."""
 import numpy as np
@@ -58,6 +58,9 @@ class FakeEngine:
         h = int(np.abs(embd).sum() * 1000) % 100003
         self.seqs[s] = h
         return 1000 + h % 20
+
+    def llm_prefill_batch(self, seqs, embds, **samp):
+        return [self.llm_prefill(s, e, **samp) for s, e in zip(seqs, embds)]
 
     def llm_generate(self, seqs, n, **samp):
         out = np.zeros((len(seqs), n), np.int32)

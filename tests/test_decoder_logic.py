@@ -55,6 +55,9 @@ class FakeEngine:
         self.calls.append(("prefill", seq, temperature))
         return st[0]
 
+    def llm_prefill_batch(self, seqs, embds, temperature=0.0, **kw):
+        return [self.llm_prefill(s, e, temperature) for s, e in zip(seqs, embds)]
+
     def llm_generate(self, seqs, n, temperature=0.0, **kw):
         out = np.zeros((len(seqs), n), np.int32)
         for r, s in enumerate(seqs):

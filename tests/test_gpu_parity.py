@@ -362,3 +362,40 @@ def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
         s = np.sort(lu[k])
         if s[-1] - s[-2] > 1e-3:
             assert tf[k + 1] == tu[k + 1]
+
+
+def test_llm_prefill_batch_equals_per_sequence(llm_tiny_oracle):
+    """fa_llm_prefill_batch: three prompts of different lengths in one forward (each row attends its own sequence's
+    keys) against prefilling each alone: same first token (non-tie margins), logits within the q8_0 noise floor (the
+    batch takes other GEMM shapes, so f32 summation orders differ), positions advanced, and the first decode step
+    teacher-forced against the oracle."""
+    from fun_asr_gguf import _native
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(21)
+    prompts = [np.concatenate([m.embed_prompt(rng.integers(0, 4096, n)),
+                               (rng.standard_normal((5, 1024)) * 0.3).astype(np.float32)], 0) for n in (7, 30, 16)]
+    e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=128, max_seqs=4), max_batch=1, max_samples=16000)
+    try:
+        e.synthetic_weights(0)
+        single = []
+        for s, p in enumerate(prompts):
+            e.llm_reset(s)
+            t = e.llm_prefill(s, p, temperature=0.0)
+            single.append((t, e.llm_logits(s)))
+        for s in range(3):
+            e.llm_reset(s)
+        toks = e.llm_prefill_batch([0, 1, 2], prompts, temperature=0.0)
+        for s in range(3):
+            lg = e.llm_logits(s)
+            assert _cos(lg, single[s][1]) > 0.9995
+            srt = np.sort(single[s][1])
+            if srt[-1] - srt[-2] > 0.25:
+                assert toks[s] == single[s][0], s
+            assert e.llm_n_past(s) == prompts[s].shape[0]
+        m.reset()
+        _check_step(e.llm_logits(1), m.forward(prompts[1], 0))
+        step = e.llm_generate([0, 1, 2], 1)
+        _check_step(e.llm_logits(1), m.forward(m.embed_tokens([toks[1]]), prompts[1].shape[0]))
+        assert step.shape == (3, 1)
+    finally:
+        e.close()
