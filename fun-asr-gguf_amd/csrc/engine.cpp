@@ -126,6 +126,9 @@ struct Engine {
   int64_t seq_stride = 0, layer_stride = 0;
   int m_max = 0, n_part = 0, n_part_cur = 0;  // partial stride allocated / written by the last lm_head
   int pf_max = 0;                               // row capacity of one forward (multi-sequence prefill batches)
+  int4* d_ptiles = nullptr;                     // prefill query tiles {row0, n_rows, seq, 0} (attn_prefill)
+  int n_ptiles = 0;                             // tiles of the forward being run (0: per-row attn_block)
+  int attn_pf_min_m = 512;                      // query-tiled prefill attention from this many rows (env knob)
   float* lxg = nullptr;                         // gathered last rows of a prefill batch
   int* d_lastrow = nullptr;
   int chunk_cur = 1;                            // rows per partial of the last lm_head
@@ -616,6 +619,7 @@ struct Engine {
 
     d_tok_seq = alloc<int>(pf_max);
     d_tok_pos = alloc<int>(pf_max);
+    d_ptiles = alloc<int4>(pf_max);
     d_step = alloc<int>(m_max);
     d_tok_cur = alloc<int>(lc.max_seqs);
     hist_max = 4096;
@@ -812,6 +816,22 @@ struct Engine {
   }
 
   // ---------------------------------------------------------------------------------------------
+  // prefill rows -> query tiles of <= 64 consecutive positions of one sequence (uploaded on the stream; host copy
+  // kept in h_ptiles until the next call). Below attn_pf_min_m rows (or head dim != 128) the per-row path runs.
+  std::vector<int4> h_ptiles;
+  void set_prefill_tiles(const int* sq, const int* ps, int rows) {
+    n_ptiles = 0;
+    if (rows < attn_pf_min_m || lc.head_dim != 128 || lc.n_head != 2 * lc.n_head_kv) return;
+    h_ptiles.clear();
+    for (int r = 0; r < rows; ++r) {
+      const bool cont = r > 0 && h_ptiles.back().y < 64 && h_ptiles.back().z == sq[r] && ps[r - 1] + 1 == ps[r];
+      if (cont) ++h_ptiles.back().y;
+      else h_ptiles.push_back(make_int4(r, 1, sq[r], 0));
+    }
+    n_ptiles = (int)h_ptiles.size();
+    FA_HIP(hipMemcpyAsync(d_ptiles, h_ptiles.data(), n_ptiles * sizeof(int4), hipMemcpyHostToDevice, stream));
+  }
+
   // decoder forward over M token rows (embeddings already in lx, positions in d_tok_pos)
   // n_last > 0 (prefill batch): logits for rows d_lastrow[0 .. n_last) (each sequence's last prompt row)
   void llm_forward(int M, bool decode, int max_pos, int n_last = 0) {
@@ -851,9 +871,13 @@ struct Engine {
           qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
                         seq_stride, stream);
         // M > 4: the attention also leaves its rows as q8_0 blocks for the o GEMM (no prep launch)
-        attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
-                   d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream, small ? nullptr : lxq2,
-                   small ? nullptr : lxd2);
+        if (!decode && n_ptiles > 0)  // query tiles: each K/V tile serves 64 rows x 2 heads
+          attn_prefill(d_ptiles, n_ptiles, d_tok_pos, H, KV, seq_stride, kc, vc, lq, latt, small ? nullptr : lxq2,
+                       small ? nullptr : lxd2, stream);
+        else
+          attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
+                     d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream, small ? nullptr : lxq2,
+                     small ? nullptr : lxd2);
         prof_end(3, 0, 0);
       }
       // x += Wo . attn
@@ -1085,6 +1109,11 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
+    {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
+      const char* g = getenv("FUNASR_GEMM_T_MIN_M");
+      fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;
+    }
+    if (const char* g = getenv("FUNASR_ATTN_PREFILL_MIN_M")) e->attn_pf_min_m = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_ENC_GEMM")) e->enc_gemm = strcmp(g, "f32") == 0 ? 0 : 1;
     e->build_arenas();
     e->build_constants();
@@ -1371,7 +1400,9 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   e->set_sampling(s);
+  e->set_prefill_tiles(sq.data(), ps.data(), n_tokens);
   e->llm_forward(n_tokens, false, e->n_past[seq] + n_tokens - 1);
+  e->n_ptiles = 0;
   // the first token's draw is keyed by the last prompt row's (seq, position)
   e->sample(1, e->d_tok_seq + (n_tokens - 1), e->d_tok_pos + (n_tokens - 1), nullptr, e->d_tok_cur, nullptr);
   int tok = 0;
@@ -1425,7 +1456,9 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+    e->set_prefill_tiles(sq.data(), ps.data(), rows);
     e->llm_forward(rows, false, 0, n);
+    e->n_ptiles = 0;
     // each first token's draw is keyed by its sequence's last prompt row (seq, position), as fa_llm_prefill's
     FA_HIP(hipMemcpyAsync(e->d_ids, lseq.data(), n * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_step, lpos.data(), n * 4, hipMemcpyHostToDevice, e->stream));

@@ -111,6 +111,7 @@ extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 7
 extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)
 bool gemv_small(int M);
 extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
+extern int g_gemm_t_min_m;  // token count from which the 128x128-tile int8 GEMM runs (prefill batches; default 512)
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,
                    int64_t seq_stride, hipStream_t s);
@@ -125,6 +126,10 @@ struct AttnWork {
   int max_tokens = 0, max_kv = 0;
   int max_split_tokens = 0;   // launches with more rows than this run unsplit (large prefill batches always do)
 };
+// Prefill over query tiles (multi-sequence batches): tiles[i] = {row0, n_rows <= 64, seq, 0}, rows of one sequence at
+// consecutive positions; q from qk_rope_store (head dim 128); out / qout / dout as attn_block's
+void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int KV, int64_t seq_stride, const __half* kc,
+                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s);
 // qout/dout (optional): the output rows also as q8_0 blocks (the o GEMM's pre-quantised input, no prep launch)
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,

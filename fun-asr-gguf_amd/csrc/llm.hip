@@ -887,6 +887,200 @@ static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Tiled q8_0 x q8_0 GEMM for large token counts (multi-sequence prefill, M >= g_gemm_t_min_m): 128 weight rows x
+// 128 tokens per block, 2x2 waves each owning 2x2 tiles of v_mfma_i32_32x32x32_i8 (the exact per-block integer dot),
+// K staged 64 (two q8_0 blocks) at a time through double-buffered LDS: every weight / activation byte a block reads
+// feeds 128 tokens / rows (the K-in-block kernel re-reads both per 32x32 tile: 4x the bytes per MAC). The f32 scaling
+// per block (acc += f32(dot) * (f32(d_w) * d_x), ggml_vec_dot_q8_0_q8_0) is the VALU work that bounds it. SwiGLU
+// (EPI 2) runs gate and up in the same waves and quantises the act rows for the down GEMM in registers (a token's
+// 32 rows of a tile are lanes l and l + 32). LDS rows of 64 B + 16 B: 16-B operand reads of 16 rows start in distinct
+// 4-bank groups.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int QT_LD = 80;  // bytes per staged row
+template <int EPI>
+struct QTile {
+  static constexpr int NM = EPI == 2 ? 2 : 1;           // weight matrices (gate, up)
+  static constexpr int W = 128 * QT_LD;                 // bytes per staged weight / activation tile
+  static constexpr int STAGE = (NM + 1) * W + (NM + 1) * 128 * 2 * 4;  // + f32 scales [m][blk][128]
+  static constexpr int BYTES = 2 * STAGE;
+};
+
+template <int EPI>
+__device__ __forceinline__ void qt_load(const GemvArgs& a, int K, int o0, int t0, int kb, int t, i32x4_t (&rw)[QTile<EPI>::NM][2],
+                                        i32x4_t (&rx)[2], float (&rdw)[QTile<EPI>::NM], float& rdx) {
+  const int nb = K >> 5;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = t + 256 * c, row = idx >> 2, k16 = idx & 3;
+    const int8_t* xp = a.xq + (int64_t)min(t0 + row, a.M - 1) * K + kb * 32 + 16 * k16;
+    rx[c] = *reinterpret_cast<const i32x4_t*>(xp);
+#pragma unroll
+    for (int m = 0; m < QTile<EPI>::NM; ++m) {
+      const int8_t* wp = (m ? a.wq2 : a.wq) + (int64_t)min(o0 + row, a.O - 1) * K + kb * 32 + 16 * k16;
+      rw[m][c] = *reinterpret_cast<const i32x4_t*>(wp);
+    }
+  }
+  const int row = t >> 1, blk = t & 1;
+#pragma unroll
+  for (int m = 0; m < QTile<EPI>::NM; ++m)
+    rdw[m] = __half2float((m ? a.wd2 : a.wd)[(int64_t)min(o0 + row, a.O - 1) * nb + kb + blk]);
+  rdx = a.xd[(int64_t)min(t0 + row, a.M - 1) * nb + kb + blk];
+}
+
+template <int EPI>
+__device__ __forceinline__ void qt_store(uint8_t* st, int t, const i32x4_t (&rw)[QTile<EPI>::NM][2], const i32x4_t (&rx)[2],
+                                         const float (&rdw)[QTile<EPI>::NM], float rdx) {
+  using T = QTile<EPI>;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int idx = t + 256 * c, row = idx >> 2, k16 = idx & 3;
+#pragma unroll
+    for (int m = 0; m < T::NM; ++m) *reinterpret_cast<i32x4_t*>(st + m * T::W + row * QT_LD + 16 * k16) = rw[m][c];
+    *reinterpret_cast<i32x4_t*>(st + T::NM * T::W + row * QT_LD + 16 * k16) = rx[c];
+  }
+  float* sc = reinterpret_cast<float*>(st + (T::NM + 1) * T::W);  // [m (weights) | NM (tokens)][blk][128]
+  const int row = t >> 1, blk = t & 1;
+#pragma unroll
+  for (int m = 0; m < T::NM; ++m) sc[(m * 2 + blk) * 128 + row] = rdw[m];
+  sc[(T::NM * 2 + blk) * 128 + row] = rdx;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
+  using T = QTile<EPI>;
+  constexpr int NM = T::NM;
+  extern __shared__ __attribute__((aligned(16))) uint8_t qsm[];
+  const int o0 = blockIdx.x * 128, t0 = blockIdx.y * 128;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+  const int wr = wave >> 1, wc = wave & 1;
+  f32x16 acc[NM][2][2];
+#pragma unroll
+  for (int m = 0; m < NM; ++m)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[m][i][j] = f32x16{};
+  i32x4_t rw[NM][2], rx[2];
+  float rdw[NM], rdx;
+  const int nk = K / 64;
+  qt_load<EPI>(a, K, o0, t0, 0, t, rw, rx, rdw, rdx);
+  qt_store<EPI>(qsm, t, rw, rx, rdw, rdx);
+  __syncthreads();
+  const i32x16_t zero = {};
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) qt_load<EPI>(a, K, o0, t0, 2 * (kt + 1), t, rw, rx, rdw, rdx);
+    const uint8_t* st = qsm + cur * T::STAGE;
+    const float* sc = reinterpret_cast<const float*>(st + (NM + 1) * T::W);
+#pragma unroll 1
+    for (int j = 0; j < 2; ++j) {  // the stage's two q8_0 blocks
+      i32x4_t bx[2];
+      float dx[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int tok = wc * 64 + jj * 32 + r;
+        bx[jj] = *reinterpret_cast<const i32x4_t*>(st + NM * T::W + tok * QT_LD + 32 * j + 16 * h);
+        dx[jj] = sc[(NM * 2 + j) * 128 + tok];
+      }
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int rb = wr * 64 + i * 32;
+          const i32x4_t aw = *reinterpret_cast<const i32x4_t*>(st + m * T::W + (rb + r) * QT_LD + 32 * j + 16 * h);
+          float4 dw4[4];  // this lane's 16 rows: (reg & 3) + 8 (reg >> 2) + 4 h
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            dw4[g] = *reinterpret_cast<const float4*>(sc + (m * 2 + j) * 128 + rb + 8 * g + 4 * h);
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(aw, bx[jj], zero, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              acc[m][i][jj][4 * g + 0] += (float)D[4 * g + 0] * (dw4[g].x * dx[jj]);
+              acc[m][i][jj][4 * g + 1] += (float)D[4 * g + 1] * (dw4[g].y * dx[jj]);
+              acc[m][i][jj][4 * g + 2] += (float)D[4 * g + 2] * (dw4[g].z * dx[jj]);
+              acc[m][i][jj][4 * g + 3] += (float)D[4 * g + 3] * (dw4[g].w * dx[jj]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one (matrix, row tile) at a time: two MFMA results live, not eight
+        }
+    }
+    if (kt + 1 < nk) qt_store<EPI>(qsm + (cur ^ 1) * T::STAGE, t, rw, rx, rdw, rdx);
+    __syncthreads();
+  }
+  // epilogue: lane -> token t0 + wc 64 + jj 32 + r; reg -> row o0 + wr 64 + i 32 + (reg & 3) + 8 (reg >> 2) + 4 h
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int tok = t0 + wc * 64 + jj * 32 + r, rb = o0 + wr * 64 + i * 32;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float y = acc[0][i][jj][q];
+        if constexpr (EPI == 2) {
+          const float y2 = acc[NM - 1][i][jj][q];
+          v[q] = (y / (1.0f + expf(-y))) * y2;
+        } else {
+          v[q] = y;
+        }
+      }
+      if (tok < a.M) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = rb + (q & 3) + 8 * (q >> 2) + 4 * h;
+          if (row < a.O) {
+            float* op = a.out + (int64_t)tok * a.ldo + row;
+            if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + v[q];
+            else *op = v[q];
+          }
+        }
+      }
+      if constexpr (EPI == 2) {
+        if (a.qout) {  // the down GEMM's q8_0 input: rows rb .. rb + 31 of this token are one block (swiglu_tile_q8)
+          float am = 0.f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) am = fmaxf(am, fabsf(v[q]));
+          am = fmaxf(am, __shfl_xor(am, 32, 64));
+          const float d = am / 127.0f;
+          const float id = d != 0.0f ? 1.0f / d : 0.0f;
+          if (tok < a.M) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int b0 = (int)roundf(__fmul_rn(v[4 * g], id)) & 0xFF, b1 = (int)roundf(__fmul_rn(v[4 * g + 1], id)) & 0xFF;
+              const int b2 = (int)roundf(__fmul_rn(v[4 * g + 2], id)) & 0xFF, b3 = (int)roundf(__fmul_rn(v[4 * g + 3], id)) & 0xFF;
+              *reinterpret_cast<int32_t*>(a.qout + (int64_t)tok * a.ldo + rb + 8 * g + 4 * h) =
+                  b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+            }
+            if (h == 0) a.dout[(int64_t)tok * (a.ldo / 32) + rb / 32] = __half2float(__float2half_rn(d));
+          }
+        }
+      }
+    }
+}
+
+int g_gemm_t_min_m = 512;  // token count from which prefill GEMMs take the tiled kernel (FUNASR_GEMM_T_MIN_M)
+
+static bool gemm_q8_t(const GemvArgs& a, int K, int epi, hipStream_t s) {
+  if (a.M < g_gemm_t_min_m || epi == 3 || K % 64 || a.O % 32) return false;
+  const dim3 grid(cdiv(a.O, 128), cdiv(a.M, 128));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<0>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<0>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<1>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<1>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<2>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<2>::BYTES);
+    attr = true;
+  }
+  switch (epi) {
+    case 0: hipLaunchKernelGGL(k_gemm_q8_t<0>, grid, dim3(256), QTile<0>::BYTES, s, a, K); break;
+    case 1: hipLaunchKernelGGL(k_gemm_q8_t<1>, grid, dim3(256), QTile<1>::BYTES, s, a, K); break;
+    default: hipLaunchKernelGGL(k_gemm_q8_t<2>, grid, dim3(256), QTile<2>::BYTES, s, a, K); break;
+  }
+  return true;
+}
+
 int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0); 2: K-in-block for all
 
 // split-K shape: NBW q8_0 blocks per wave (8, 4 or 2: one load round trip) and KS = nb / (waves per matrix x NBW)
@@ -961,6 +1155,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
+  if (!a.ssp && gemm_q8_t(a, K, epi, s)) return;
   if (!a.ssp && g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
   int NBW, KS;
   gemm_sk_shape(a.O, a.M, K, epi, &NBW, &KS);
@@ -1534,6 +1729,164 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   if (qout) store_q8_row4(qout, dout, (int64_t)m * H * D + (g * GQ + j) * D + d0, lane, r);
   if (lane == 0) __hip_atomic_store(counters + (m * KV + g) * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   STAMP(10);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Prefill attention over query tiles (multi-sequence prefill batches): block = (tile of up to 64 consecutive rows of
+// ONE sequence, kv head g); its 2 query heads x 64 rows = 128 query slots share every K/V tile (32 keys, fp16 cache ->
+// f32 LDS), so K/V bytes are read once per 64 rows instead of once per row (k_attn_block). Flash style on exact-f32
+// MFMA (v_mfma_f32_32x32x2_f32, as the encoder's k_attn_f32): S^T = K . Q^T with the query slot on the lane, online
+// softmax in registers, P^T straight into O^T += V^T . P^T. Causal: key k of row r counts iff k <= pos(r). Writes the
+// rows (f32) and their q8_0 blocks for the o GEMM. Tiles: int4 {row0, n_rows, seq, 0} from the host.
+constexpr int PAQ = 128, PAK = 32, PAD = 128, PAS = PAD + 8;  // query slots, keys per tile, head dim, LDS row stride
+
+__global__ __launch_bounds__(256) void k_attn_prefill(const int4* __restrict__ tiles, const int* __restrict__ tok_pos,
+                                                      int H, int KV, int64_t seq_stride, int64_t head_stride,
+                                                      const __half* __restrict__ kc, const __half* __restrict__ vc,
+                                                      const float* __restrict__ q, float scale, float* __restrict__ out,
+                                                      int8_t* __restrict__ qout, float* __restrict__ dout) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * PAK * PAS];  // K, V x 2 stages; O staging reuses it
+  __shared__ float s_l[PAQ];
+  const int4 td = tiles[blockIdx.x];
+  const int row0 = td.x, nr = td.y, seq = td.z, g = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int hh = wave >> 1, rr = (wave & 1) * 32 + r;  // this lane's query slot: head 2 g + hh, tile row rr
+  const int rrc = min(rr, nr - 1);
+  const int pos = tok_pos[row0 + rrc];
+  const int pmax = tok_pos[row0 + nr - 1];             // rows of a tile are consecutive positions
+  const __half* kb = kc + (int64_t)seq * seq_stride + g * head_stride;
+  const __half* vb = vc + (int64_t)seq * seq_stride + g * head_stride;
+  float qreg[PAD / 2];
+  {
+    const float* p = q + (int64_t)(row0 + rrc) * H * PAD + (2 * g + hh) * PAD + h * (PAD / 2);
+#pragma unroll
+    for (int d = 0; d < PAD / 2; d += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p + d);
+      qreg[d] = v.x * scale; qreg[d + 1] = v.y * scale; qreg[d + 2] = v.z * scale; qreg[d + 3] = v.w * scale;
+    }
+  }
+  // staging: 32 keys x 128 dims fp16 = 512 chunks of 8 halves per K (and per V) tile, 2 per thread
+  auto load = [&](int kt, uint4 (&pk)[2], uint4 (&pv)[2]) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = threadIdx.x + 256 * c, key = min(kt * PAK + (f >> 4), pmax), d8 = f & 15;
+      pk[c] = *reinterpret_cast<const uint4*>(kb + (int64_t)key * PAD + 8 * d8);
+      pv[c] = *reinterpret_cast<const uint4*>(vb + (int64_t)key * PAD + 8 * d8);
+    }
+  };
+  auto store = [&](int stage, const uint4 (&pk)[2], const uint4 (&pv)[2]) {
+    float* ks_ = smem + stage * 2 * PAK * PAS;
+    float* vs_ = ks_ + PAK * PAS;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = threadIdx.x + 256 * c, key = f >> 4, d8 = f & 15;
+      const __half* hk = reinterpret_cast<const __half*>(&pk[c]);
+      const __half* hv = reinterpret_cast<const __half*>(&pv[c]);
+      float4 k0, k1, v0, v1;
+      k0 = make_float4(__half2float(hk[0]), __half2float(hk[1]), __half2float(hk[2]), __half2float(hk[3]));
+      k1 = make_float4(__half2float(hk[4]), __half2float(hk[5]), __half2float(hk[6]), __half2float(hk[7]));
+      v0 = make_float4(__half2float(hv[0]), __half2float(hv[1]), __half2float(hv[2]), __half2float(hv[3]));
+      v1 = make_float4(__half2float(hv[4]), __half2float(hv[5]), __half2float(hv[6]), __half2float(hv[7]));
+      *reinterpret_cast<float4*>(ks_ + key * PAS + 8 * d8) = k0;
+      *reinterpret_cast<float4*>(ks_ + key * PAS + 8 * d8 + 4) = k1;
+      *reinterpret_cast<float4*>(vs_ + key * PAS + 8 * d8) = v0;
+      *reinterpret_cast<float4*>(vs_ + key * PAS + 8 * d8 + 4) = v1;
+    }
+  };
+  f32x16 o[PAD / 32];
+#pragma unroll
+  for (int i = 0; i < PAD / 32; ++i) o[i] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int n_kt = pmax / PAK + 1;
+  uint4 pk[2], pv[2];
+  load(0, pk, pv);
+  store(0, pk, pv);
+  __syncthreads();
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int stage = kt & 1;
+    if (kt + 1 < n_kt) load(kt + 1, pk, pv);
+    const float* ks_ = smem + stage * 2 * PAK * PAS;
+    const float* vs_ = ks_ + PAK * PAS;
+    f32x16 sc = {};
+#pragma unroll
+    for (int c = 0; c < PAD / 2; c += 4) {
+      const float4 kv = *reinterpret_cast<const float4*>(ks_ + r * PAS + h * (PAD / 2) + c);
+      sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qreg[c], sc, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qreg[c + 1], sc, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qreg[c + 2], sc, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qreg[c + 3], sc, 0, 0, 0);
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int key = kt * PAK + (t & 3) + 8 * (t >> 2) + 4 * h;
+      const float v = key <= pos ? sc[t] : -INFINITY;
+      sc[t] = v;
+      mt = fmaxf(mt, v);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float pr = sc[t] == -INFINITY ? 0.f : __expf(sc[t] - m_new);
+      sc[t] = pr;
+      ls += pr;
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < PAD / 32; ++i) o[i] *= alpha;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int kl = (t & 3) + 8 * (t >> 2) + 4 * h;
+#pragma unroll
+      for (int i = 0; i < PAD / 32; ++i)
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(vs_[kl * PAS + i * 32 + r], sc[t], o[i], 0, 0, 0);
+    }
+    if (kt + 1 < n_kt) store(stage ^ 1, pk, pv);
+    __syncthreads();
+  }
+  // O^T (d on registers, slot on lanes) -> LDS [slot][d]; slot = hh 64 + rr
+  float* so = smem;  // 128 x (128 + 4) floats = 67.6 KB > the K/V stages: use it in two halves by head
+  constexpr int OS = PAD + 4;
+  static_assert(64 * OS <= 2 * 2 * PAK * PAS, "k_attn_prefill: O staging per head must fit the K/V stages");
+  if (h == 0) s_l[hh * 64 + rr] = l_run;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (hh == half) {
+#pragma unroll
+      for (int i = 0; i < PAD / 32; ++i)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) so[rr * OS + i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h] = o[i][t];
+    }
+    __syncthreads();
+    // 64 rows x 32 float4 = 2048 float4, 8 per thread; 8 consecutive threads = one 32-dim q8_0 block
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int f = threadIdx.x + 256 * c, row = f >> 5, d4 = f & 31;
+      const float inv = 1.0f / s_l[half * 64 + row];
+      float4 v = *reinterpret_cast<const float4*>(so + row * OS + 4 * d4);
+      v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+      const int orow = row0 + min(row, nr - 1);
+      const int64_t e = (int64_t)orow * H * PAD + (2 * g + half) * PAD + 4 * d4;
+      if (row < nr) {  // whole 32-thread rows: the 8-lane groups of store_q8_row4 stay together
+        *reinterpret_cast<float4*>(out + e) = v;
+        if (qout) store_q8_row4(qout, dout, e, threadIdx.x, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int KV, int64_t seq_stride, const __half* kc,
+                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ, "attn_prefill: n_head must be 2*n_head_kv");
+  if (n_tiles <= 0) return;
+  hipLaunchKernelGGL(k_attn_prefill, dim3(n_tiles, KV), dim3(256), 0, s, tiles, tok_pos, H, KV, seq_stride,
+                     seq_stride / KV, kc, vc, q, 1.0f / sqrtf(128.0f), out, qout, dout);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,

@@ -180,6 +180,24 @@ def test_llm_full_prefill_and_steps_teacher_forced(eng, cllm, g60, clip):
     assert eng.llm_n_past(0) == p.shape[0] + 6
 
 
+def test_llm_full_prefill_batch_tiled_gemm(eng, cllm, g60):
+    """configs[2] prefill: four 204-row prompts in one forward (816 rows: the 128x128-tile q8_0 GEMM for q|k|v, o,
+    gate|up with the SwiGLU q8_0 epilogue, and down; the prefill attention of every row over its own sequence) against
+    the oracle run of each prompt alone (first and last sequence), then one decode step of all four."""
+    prompts = [_prompt(cllm, g60["adaptor"], 10 + i) for i in range(4)]
+    for s in range(4):
+        eng.llm_reset(s)
+    toks = eng.llm_prefill_batch([0, 1, 2, 3], prompts)
+    for s in (0, 3):
+        lg = eng.llm_logits(s)
+        _check_step(lg, cllm.forward(prompts[s], 0))
+        assert toks[s] == int(np.argmax(lg))
+    step = eng.llm_generate([0, 1, 2, 3], 1)
+    lg = eng.llm_logits(3)
+    _check_step(lg, cllm.forward(cllm.embed_tokens([toks[3]]), prompts[3].shape[0]))  # the oracle holds prompt 3
+    assert int(step[3][0]) == int(np.argmax(lg))
+
+
 @pytest.mark.parametrize("n_seq", [5, 32])
 def test_llm_full_batched_decode_rows(eng, cllm, n_seq):
     """configs[2] continuous batch at full dims: M = 32 (int8 MFMA GEMMs + the batched LM head with its argmax

@@ -364,16 +364,22 @@ def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
             assert tf[k + 1] == tu[k + 1]
 
 
-def test_llm_prefill_batch_equals_per_sequence(llm_tiny_oracle):
+@pytest.mark.parametrize("t_min_m,apf_min_m", [(512, 512), (32, 512), (512, 16)])
+def test_llm_prefill_batch_equals_per_sequence(llm_tiny_oracle, monkeypatch, t_min_m, apf_min_m):
     """fa_llm_prefill_batch: three prompts of different lengths in one forward (each row attends its own sequence's
     keys) against prefilling each alone: same first token (non-tie margins), logits within the q8_0 noise floor (the
     batch takes other GEMM shapes, so f32 summation orders differ), positions advanced, and the first decode step
-    teacher-forced against the oracle."""
+    teacher-forced against the oracle. t_min_m = 32 sends the batch (68 rows) and the 35-row prompt through the
+    128x128-tile q8_0 GEMM (FUNASR_GEMM_T_MIN_M, read at engine creation); apf_min_m = 16 sends the batch and the
+    75- and 21-row prompts through the query-tiled prefill attention (k_attn_prefill; the 75-row prompt spans two
+    64-row tiles) while the 12-row prompt stays on the per-row kernel."""
     from fun_asr_gguf import _native
+    monkeypatch.setenv("FUNASR_GEMM_T_MIN_M", str(t_min_m))
+    monkeypatch.setenv("FUNASR_ATTN_PREFILL_MIN_M", str(apf_min_m))
     m = llm_tiny_oracle
     rng = np.random.default_rng(21)
     prompts = [np.concatenate([m.embed_prompt(rng.integers(0, 4096, n)),
-                               (rng.standard_normal((5, 1024)) * 0.3).astype(np.float32)], 0) for n in (7, 30, 16)]
+                               (rng.standard_normal((5, 1024)) * 0.3).astype(np.float32)], 0) for n in (7, 70, 16)]
     e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=128, max_seqs=4), max_batch=1, max_samples=16000)
     try:
         e.synthetic_weights(0)
