@@ -1320,7 +1320,9 @@ struct AttnQIn {
 // One wave's share of one key split: NI = its 4-key groups per pass rounded up to a power of two (loads of
 // the rounded-up slots are clamped duplicates, masked). Issues the K/V stream first, then finishes q while
 // it is in flight.
-template <int NI, int AW>
+// PIPE: the next pass's K/V loads are issued before this pass's math (2x the K/V registers: non-lean blocks only;
+// batch-1 B of the fused layer 7.44 -> 7.32 us, scripts/ubench/decode_step)
+template <int NI, int AW, bool PIPE>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
@@ -1371,7 +1373,15 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
   }
   STAMP(3);
   const int fresh = fresh_here ? pos : -1;
+  int4 kn_[PIPE ? NI : 1], vn_[PIPE ? NI : 1];  // PIPE: the next pass's K/V
   for (;;) {
+    if constexpr (PIPE) {
+      const int g1 = g0 + AW * NI;
+      if (g1 < ge) {
+        load_kv_groups<NI, AW>(kb, KV, g1, n_keys, kq, dq, kn_);
+        load_kv_groups<NI, AW>(vb, KV, g1, n_keys, kq, dq, vn_);
+      }
+    }
     // scores of key 4 (g0 + AW i) + kq: 8-dim partial dot per lane, summed over the row's 16 lanes (DPP)
     float sc[NI][GQ];
 #pragma unroll
@@ -1435,8 +1445,16 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
     STAMP(6);
     g0 += AW * NI;
     if (g0 >= ge) break;
-    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+    if constexpr (PIPE) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        kt[i] = kn_[PIPE ? i : 0];
+        vt[i] = vn_[PIPE ? i : 0];
+      }
+    } else {
+      load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+      load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+    }
   }
 }
 
@@ -1540,16 +1558,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     __half* vd = vb + (int64_t)pos * D;
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
-      attn_wave<1, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<1, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 2)
-      attn_wave<2, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<2, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 4 || LEAN)
-      attn_wave<4, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<4, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
     else
-      attn_wave<8, AWV>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<8, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
   }
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add

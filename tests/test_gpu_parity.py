@@ -405,3 +405,40 @@ def test_llm_prefill_batch_equals_per_sequence(llm_tiny_oracle, monkeypatch, t_m
         assert step.shape == (3, 1)
     finally:
         e.close()
+
+
+def test_llm_prefill_batch_continuation_query_tiles(llm_tiny_oracle, monkeypatch):
+    """Query-tiled prefill attention (k_attn_prefill) on prompts that continue a cached prefix (tiles start at n_past
+    > 0, keys [0, pos] from the cache) and on tiles cut at 64 rows: prefilling [p0 | p1] in two batched calls equals one
+    per-sequence prefill of the whole prompt (cosine within the q8_0 noise floor) and the oracle's teacher-forced
+    logits."""
+    from fun_asr_gguf import _native
+    monkeypatch.delenv("FUNASR_ATTN_PREFILL_MIN_M", raising=False)
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(5)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (90, 20, 70)]
+    cut = [33, 7, 64]
+    cfg = dict(synth.LLM_TINY, n_ctx=128, max_seqs=4)
+    e = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)  # per-row attention (default threshold)
+    try:
+        e.synthetic_weights(0)
+        single = []
+        for s, p in enumerate(prompts):
+            e.llm_reset(s)
+            e.llm_prefill(s, p, temperature=0.0)
+            single.append(e.llm_logits(s))
+    finally:
+        e.close()
+    monkeypatch.setenv("FUNASR_ATTN_PREFILL_MIN_M", "8")  # read at engine creation
+    e = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)
+    try:
+        e.synthetic_weights(0)
+        e.llm_prefill_batch([0, 1, 2], [p[:c] for p, c in zip(prompts, cut)], temperature=0.0)
+        e.llm_prefill_batch([2, 0, 1], [prompts[2][cut[2]:], prompts[0][cut[0]:], prompts[1][cut[1]:]], temperature=0.0)
+        for s in range(3):
+            assert e.llm_n_past(s) == prompts[s].shape[0]
+            assert _cos(e.llm_logits(s), single[s]) > 0.9995
+        m.reset()
+        _check_step(e.llm_logits(0), m.forward(prompts[0], 0))
+    finally:
+        e.close()
