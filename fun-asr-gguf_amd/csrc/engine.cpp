@@ -1113,6 +1113,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
       fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;
     }
+    if (const char* g = getenv("FUNASR_LM_HEAD_B")) fa::g_lm_head_b = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_PREFILL_MIN_M")) e->attn_pf_min_m = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_ENC_GEMM")) e->enc_gemm = strcmp(g, "f32") == 0 ? 0 : 1;
     e->build_arenas();

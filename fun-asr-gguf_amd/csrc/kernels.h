@@ -111,6 +111,7 @@ extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 7
 extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)
 bool gemv_small(int M);
 extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
+extern int g_lm_head_b;     // 1: batched LM head on the persistent tile loop (k_lm_head_b); 0: split-K block kernel
 extern int g_gemm_t_min_m;  // token count from which the 128x128-tile int8 GEMM runs (prefill batches; default 512)
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
                    const float* rsin, const int* tok_seq, const int* tok_pos, float* qout, __half* kc, __half* vc,

@@ -739,6 +739,149 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   KSTAMP(5);
 }
 
+// Batched LM head (5-32 tokens, K = 1024, the 151936 vocabulary rows): the split-K block kernel's tile arithmetic
+// (4 waves x 8 q8_0 blocks of K, fixed-order wave sum, argmax partial per 32-row tile) in a persistent loop over
+// tiles, 3 blocks per CU. A block loads its waves' activation blocks and scales (NRM: rstd applied) once for every
+// tile. Weight rows are fetched coalesced (each load instruction 4 rows x 256 contiguous B; 16 B per lane from 32
+// rows was the old kernel's pattern) and turned into the MFMA fragment layout through LDS; the next tile's loads go out
+// before the current tile's math; scales are staged as f32 (no per-product conversion); logits leave through LDS as
+// 128-B token rows. scripts/ubench/gemm_batch (M = 32, graph-replayed): 133 -> 44.8 us per launch (3.7 TB/s).
+constexpr int LMB_PER_CU = 3;                 // 156 VGPRs, 43 KB of LDS per block
+constexpr int LMB_BLOCKS = 256 * LMB_PER_CU;  // every block resident
+
+template <bool NRM>
+__global__ __launch_bounds__(256, LMB_PER_CU) void k_lm_head_b(GemvArgs a) {
+  constexpr int K = 1024, NB = K / 32, NBW = 8, WLD = 256 + 16;  // LDS weight rows: the wave's 256 B + 16 B pad
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int bw0 = wave * NBW;
+  const int t_b = min(r, a.M - 1);
+  const int n_tiles = (a.O + 31) >> 5;
+  __shared__ __attribute__((aligned(16))) int8_t s_w[4][32 * WLD];  // per wave: its K quarter of the tile's 32 rows
+  __shared__ __attribute__((aligned(16))) float s_sc[4][NBW][64];  // per wave: [block j][lane -> row lane & 31], f32
+  // s_red[wave] aliases the wave's own weight image: written after the wave has read its A fragments, read between
+  // the two barriers, and the image is rewritten only after the second barrier
+  static_assert(16 * 64 * 4 <= 32 * WLD, "k_lm_head_b: wave partials must fit the wave's weight image");
+  __shared__ float s_act[32][33];  // [token][row]
+  // a tile's loads, coalesced: instruction i reads rows 4 i .. 4 i + 3, 256 contiguous bytes each (lanes 16 q .. 16 q
+  // + 15 -> row 4 i + q); the scale slab: lane l -> row l & 31, the wave's 8 fp16 scales
+  auto load_tile = [&](int tile, i32x4_t (&W)[NBW], uint4& sl) {
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      const int row = min(tile * 32 + 4 * i + (lane >> 4), a.O - 1);
+      W[i] = __builtin_nontemporal_load(
+          reinterpret_cast<const i32x4_t*>(a.wq + (int64_t)row * K + bw0 * 32 + 16 * (lane & 15)));
+    }
+    sl = *reinterpret_cast<const uint4*>(a.wd + (int64_t)min(tile * 32 + r, a.O - 1) * NB + bw0);
+  };
+  i32x4_t W[NBW];
+  uint4 sl;
+  int tile = blockIdx.x;
+  if (tile < n_tiles) load_tile(tile, W, sl);
+  float4 sv[NRM ? 8 : 1];
+  if constexpr (NRM) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = *reinterpret_cast<const float4*>(a.ssp + (int64_t)t_b * 32 + 4 * i);
+  }
+  i32x4_t B[NBW];
+  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + bw0 * 32;
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
+  float dx[NBW];
+#pragma unroll
+  for (int q = 0; q < NBW / 2; ++q) {
+    const float2 v = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * NB + bw0 + 2 * q);
+    dx[2 * q] = v.x;
+    dx[2 * q + 1] = v.y;
+  }
+  if constexpr (NRM) {  // as k_gemm_q8_sk<NRM>: the producer's 32 partials in tile order, f16 block scales
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss = (((ss + sv[i].x) + sv[i].y) + sv[i].z) + sv[i].w;
+    const float rstd = 1.0f / sqrtf(ss / (float)K + a.eps);
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) dx[j] = __half2float(__float2half_rn(rstd * dx[j]));
+  }
+  const int l = lane, g = wave, col = l & 31;
+  const i32x16_t zero = {};
+  // the activation blocks are waited for here, once: inside the loop every vmcnt wait then counts only weight loads
+  // (a pending pre-loop load would make each MFMA drain the next tile's prefetch)
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) asm volatile("" ::"v"(B[j]));
+  int8_t* sw = s_w[wave];
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const int o0 = tile * 32;
+    // the landed tile -> LDS (every lane, no branch), then the next tile's loads go out before any math
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+      *reinterpret_cast<i32x4_t*>(sw + (4 * i + (lane >> 4)) * WLD + 16 * (lane & 15)) = W[i];
+    {  // row r's 8 scales as f32, transposed so a fragment's 16 rows are 4 x 16-B reads (every lane: no branch)
+      const uint32_t pr[4] = {sl.x, sl.y, sl.z, sl.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const __half* hp = reinterpret_cast<const __half*>(&pr[k]);
+        s_sc[wave][2 * k][lane] = __half2float(hp[0]);
+        s_sc[wave][2 * k + 1][lane] = __half2float(hp[1]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (tile + (int)gridDim.x < n_tiles) load_tile(tile + gridDim.x, W, sl);
+    float acc[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
+#pragma unroll
+    for (int jp = 0; jp < NBW / 2; ++jp) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = 2 * jp + jj;
+        float dw[16];  // block j's scales of rows (reg & 3) + 8 (reg >> 2) + 4 h (wave-half broadcast reads)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(&s_sc[wave][j][8 * q + 4 * h]);
+          dw[4 * q] = v.x; dw[4 * q + 1] = v.y; dw[4 * q + 2] = v.z; dw[4 * q + 3] = v.w;
+        }
+        const i32x4_t Aj = *reinterpret_cast<const i32x4_t*>(sw + r * WLD + 32 * j + 16 * h);  // MFMA layout
+        const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aj, B[j], zero, 0, 0, 0);
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) acc[reg] += (float)D[reg] * (dw[reg] * dx[j]);
+      }
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) *reinterpret_cast<float*>(s_w[wave] + (reg * 64 + lane) * 4) = acc[reg];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int reg = 4 * g + q;
+      auto red = [&](int w) { return *reinterpret_cast<const float*>(s_w[w] + (reg * 64 + l) * 4); };
+      const float y = ((red(0) + red(1)) + red(2)) + red(3);
+      const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
+      s_act[col][rrow] = o0 + rrow < a.O ? y : -INFINITY;
+    }
+    __syncthreads();
+    {  // thread t: token t >> 3, rows [4 (t & 7), +4): logits as 16-B pieces of the token's 128-B row; argmax over 8 lanes
+      const int tk = threadIdx.x >> 3, rq = (threadIdx.x & 7) * 4;
+      const float4 v = make_float4(s_act[tk][rq], s_act[tk][rq + 1], s_act[tk][rq + 2], s_act[tk][rq + 3]);
+      if (tk < a.M && o0 + rq < a.O) *reinterpret_cast<float4*>(a.out + (int64_t)tk * a.ldo + o0 + rq) = v;
+      float bv = v.x;
+      int bi = o0 + rq;
+      argmax_combine(bv, bi, v.y, o0 + rq + 1);
+      argmax_combine(bv, bi, v.z, o0 + rq + 2);
+      argmax_combine(bv, bi, v.w, o0 + rq + 3);
+#pragma unroll
+      for (int off = 1; off < 8; off <<= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        argmax_combine(bv, bi, ov, oi);
+      }
+      if ((threadIdx.x & 7) == 0 && tk < a.M) {
+        a.pval[(int64_t)tk * a.n_part + tile] = bv;
+        a.pidx[(int64_t)tk * a.n_part + tile] = bi;
+      }
+    }
+  }
+}
+
 // Same GEMM with K split over the NW waves of ONE block instead of over blocks: no cross-block split-K hop (on
 // this chip an in-launch hand-off costs about a kernel boundary: scripts/ubench/edge_chain.hip), and every wave
 // issues ALL its loads (NBW q8_0 blocks of weights and activations, their scales) before its MFMAs, so a tile
@@ -1081,6 +1224,7 @@ static bool gemm_q8_t(const GemvArgs& a, int K, int epi, hipStream_t s) {
   return true;
 }
 
+int g_lm_head_b = 1;  // 0: batched LM head on the one-tile-per-block split-K kernel (A/B, FUNASR_LM_HEAD_B=0)
 int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, FUNASR_GEMM_KW=0); 2: K-in-block for all
 
 // split-K shape: NBW q8_0 blocks per wave (8, 4 or 2: one load round trip) and KS = nb / (waves per matrix x NBW)
@@ -1155,6 +1299,12 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
+  if (epi == 3 && K == 1024 && a.M <= 32 && g_lm_head_b) {  // batched LM head: persistent tile loop
+    const int nblk = std::min(cdiv(a.O, 32), LMB_BLOCKS);
+    if (a.ssp) hipLaunchKernelGGL(k_lm_head_b<true>, dim3(nblk), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_lm_head_b<false>, dim3(nblk), dim3(256), 0, s, a);
+    return;
+  }
   if (!a.ssp && gemm_q8_t(a, K, epi, s)) return;
   if (!a.ssp && g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
   int NBW, KS;

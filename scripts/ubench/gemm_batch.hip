@@ -71,6 +71,7 @@ int main(int argc, char** argv) {
   for (auto& sh : shapes) {
     for (int kw : {0, 2, 1}) {
       g_gemm_q8_kw = kw;
+      g_lm_head_b = kw == 1;  // lm_head: kw 0 / 2 time the one-tile-per-block kernel, kw 1 the persistent loop
       const double us = timed([&] {
         for (int i = 0; i < sh.n; ++i) {
           GemvArgs ga{};
