@@ -545,6 +545,9 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
 // rstd = 1/sqrtf(sum/K + eps) scales every block uniformly, so the q8_0 rows of y = (x * rstd) * w are the same
 // integers (up to float rounding at .5 ties) with scale f16(rstd * d_z): this GEMM only applies rstd, and the two
 // k_prep_q8 launches per layer (with their kernel boundaries) disappear.
+#ifndef FA_SK_COALESCE
+#define FA_SK_COALESCE 1
+#endif
 template <int EPI, int NBW, int KSM, bool NRM = false>
 __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
@@ -567,11 +570,29 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     for (int i = 0; i < 8; ++i) sv[i] = *reinterpret_cast<const float4*>(a.ssp + (int64_t)t_b * 32 + 4 * i);
   }
   i32x4_t A[NBW], B[NBW];
+#if FA_SK_COALESCE
+  // coalesced: load instruction i reads RPI rows x RB contiguous bytes of the wave's K slice (weights and activations);
+  // the fragments are rebuilt through LDS below (16 B per lane from 32 rows per instruction ran the LM head at a third
+  // of the coalesced rate)
+  constexpr int RB = NBW * 32, LPR = RB / 16, RPI = 64 / LPR, SLD = RB + 16;
+  __shared__ __attribute__((aligned(16))) int8_t s_ab[4][2][32 * SLD];
+  (void)wa;
+  (void)xb;
+  {
+    const int rr = lane / LPR, off = bw0 * 32 + 16 * (lane % LPR);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      A[i] = *reinterpret_cast<const i32x4_t*>(wq + (int64_t)min(o0 + RPI * i + rr, a.O - 1) * K + off);
+      B[i] = *reinterpret_cast<const i32x4_t*>(a.xq + (int64_t)min(t0 + RPI * i + rr, a.M - 1) * K + off);
+    }
+  }
+#else
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
     B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
   }
+#endif
   uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg)
@@ -608,6 +629,24 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
   const i32x16_t zero = {};
+#if FA_SK_COALESCE
+  {  // rows -> LDS, then the MFMA layout: lane (r, h) -> row r, 16 B half h of block j
+    const int rr = lane / LPR, cb = 16 * (lane % LPR);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      *reinterpret_cast<i32x4_t*>(&s_ab[wave][0][(RPI * i + rr) * SLD + cb]) = A[i];
+      *reinterpret_cast<i32x4_t*>(&s_ab[wave][1][(RPI * i + rr) * SLD + cb]) = B[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      A[j] = *reinterpret_cast<const i32x4_t*>(&s_ab[wave][0][r * SLD + 32 * j + 16 * h]);
+      B[j] = *reinterpret_cast<const i32x4_t*>(&s_ab[wave][1][r * SLD + 32 * j + 16 * h]);
+    }
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
@@ -619,11 +658,19 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     }
   }
   // fixed-order reduction over the waves
+#if FA_SK_COALESCE
+  // s_red[w] in wave w's own staging image (written after the wave read its fragments, read after the barrier)
+  static_assert(16 * 64 * 4 <= 2 * 32 * SLD, "k_gemm_q8_sk: wave partials must fit the wave's staging image");
+  float(&s_red)[4][2 * 32 * SLD / 4] = *reinterpret_cast<float(*)[4][2 * 32 * SLD / 4]>(&s_ab[0][0][0]);
+#define SRED(w, reg, l) s_red[w][(reg) * 64 + (l)]
+#else
   __shared__ float s_red[4][16][64];
+#define SRED(w, reg, l) s_red[w][reg][l]
+#endif
   __shared__ float s_act[EPI >= 2 ? 32 : 1][33];  // tile [token][row]: SwiGLU q8_0 epilogue, lm_head argmax
   __shared__ int s_last;
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
+  for (int reg = 0; reg < 16; ++reg) SRED(wave, reg, lane) = acc[reg];
   __syncthreads();
   KSTAMP(2);
   float y[4], y2[4];
@@ -631,10 +678,10 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   for (int q = 0; q < 4; ++q) {
     const int reg = 4 * g + q;
     if (EPI == 2) {
-      y[q] = s_red[0][reg][l] + s_red[1][reg][l];
-      y2[q] = s_red[2][reg][l] + s_red[3][reg][l];
+      y[q] = SRED(0, reg, l) + SRED(1, reg, l);
+      y2[q] = SRED(2, reg, l) + SRED(3, reg, l);
     } else {
-      y[q] = ((s_red[0][reg][l] + s_red[1][reg][l]) + s_red[2][reg][l]) + s_red[3][reg][l];
+      y[q] = ((SRED(0, reg, l) + SRED(1, reg, l)) + SRED(2, reg, l)) + SRED(3, reg, l);
       y2[q] = 0.f;
     }
   }
@@ -738,6 +785,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   }
   KSTAMP(5);
 }
+#undef SRED
 
 // Batched LM head (5-32 tokens, K = 1024, the 151936 vocabulary rows): the split-K block kernel's tile arithmetic
 // (4 waves x 8 q8_0 blocks of K, fixed-order wave sum, argmax partial per 32-row tile) in a persistent loop over
@@ -2557,6 +2605,10 @@ __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) 
 
 constexpr int FO_ROWS = 64;  // o-projection rows per split block (E / ASPLIT, E = 1024)
 
+#ifndef FA_AO_COALESCE
+#define FA_AO_COALESCE 1
+#endif
+
 struct AttnOArgs {
   const int* tok_seq;
   const int* tok_pos;
@@ -2588,12 +2640,27 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
   // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
-  const int tr = threadIdx.x >> 2, tq = threadIdx.x & 3, KO = a.H * D;
+  const int KO = a.H * D;
+#if FA_AO_COALESCE
+  // coalesced: load k reads rows 16 wave + 4 k + (lane >> 4) of the slice, 256 contiguous bytes each; lane chunk
+  // c = lane & 15 is half c & 1 of q8_0 block c >> 1 of the head pair's 256 columns
+  const int c16 = lane & 15;
+  int4 wk[4];
+  float dwk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int orow = FO_ROWS * sp + 16 * wave + 4 * k + (lane >> 4);
+    wk[k] = ld_nt16(a.wo_q + (int64_t)orow * KO + GQ * D * g + 16 * c16);
+    dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
+  }
+#else
+  const int tr = threadIdx.x >> 2, tq = threadIdx.x & 3;
   const int orow = FO_ROWS * sp + tr;
   const int8_t* wp = a.wo_q + (int64_t)orow * KO + GQ * D * g + 64 * tq;
   const int4 w0 = ld_nt16(wp), w1 = ld_nt16(wp + 16), w2 = ld_nt16(wp + 32), w3 = ld_nt16(wp + 48);
   const __half* dp = a.wo_d + (int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + 2 * tq;
   const float dw0 = __half2float(dp[0]), dw1 = __half2float(dp[1]);
+#endif
   __builtin_amdgcn_sched_barrier(0);
   int n_active = 0, j = 0, d0 = 0;
   float M = -INFINITY, L = 0.f;
@@ -2629,6 +2696,20 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     if ((lane & 7) == 0) s_ad[(jj * D + dd) / 32] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
+#if FA_AO_COALESCE
+  const int4 xc = *reinterpret_cast<const int4*>(s_aq + 16 * c16);
+  const float xd = s_ad[c16 >> 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int si = dot16(wk[k], xc, 0);
+    si += dpp_i<DPP_XOR1>(si);  // the block's two halves: exact integer block dot in both lanes of the pair
+    float v = (float)si * (dwk[k] * xd);
+    v += dpp_f<DPP_XOR2>(v);  // the 8 blocks of the row (pairs hold duplicates: skip the xor-1 step)
+    v += dpp_f<DPP_HALF_MIRROR>(v);
+    v += dpp_f<DPP_MIRROR>(v);
+    if (c16 == 0) a.opart[(int64_t)g * a.E + FO_ROWS * sp + 16 * wave + 4 * k + (lane >> 4)] = v;
+  }
+#else
   const int4 x0 = *reinterpret_cast<const int4*>(s_aq + 64 * tq), x1 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 16);
   const int4 x2 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 32), x3 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 48);
   const int s0 = dot16(w1, x1, dot16(w0, x0, 0)), s1 = dot16(w3, x3, dot16(w2, x2, 0));
@@ -2636,6 +2717,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   v += dpp_f<DPP_XOR1>(v);  // the row's 4 threads are 4 consecutive lanes: fixed-order quad sum
   v += dpp_f<DPP_XOR2>(v);
   if (tq == 0) a.opart[(int64_t)g * a.E + orow] = v;
+#endif
 }
 
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
