@@ -613,13 +613,12 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   }
   // this thread finalises regs [4 g, 4 g + 4) of lane l (token col, rows rrow): residual fetched now, used after the hop
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6, col = l & 31, tok = t0 + col;
+  // (regs 4 g .. 4 g + 3 of lane l are rows [8 g + 4 (l >> 5), +4) of token col: one 16-B piece; O % 32 == 0)
   float rv[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (EPI == 1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int reg = 4 * g + q, row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5), a.O - 1);
-      rv[q] = a.res[(int64_t)min(tok, a.M - 1) * a.ldr + row];
-    }
+    const float4 r4 =
+        *reinterpret_cast<const float4*>(a.res + (int64_t)min(tok, a.M - 1) * a.ldr + o0 + 8 * g + 4 * (l >> 5));
+    rv[0] = r4.x; rv[1] = r4.y; rv[2] = r4.z; rv[3] = r4.w;
   }
 #ifdef FA_GEMV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -719,23 +718,22 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     y2[0] = sum2.x; y2[1] = sum2.y; y2[2] = sum2.z; y2[3] = sum2.w;
     if (threadIdx.x == 0) __hip_atomic_store(a.kcnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  float nv[4];  // EPI 1: the new residual values of this thread's 4 consecutive rows [8 g + 4 (l >> 5), +4)
+  float nv[4], ov[4];  // nv (EPI 1): the new residual values of this thread's 4 consecutive rows [8 g + 4 (l >> 5), +4)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int reg = 4 * g + q;
-    const int rrow = (reg & 3) + 8 * (reg >> 2) + 4 * (l >> 5);
-    const int row = o0 + rrow;
-    float v = 0.f;
-    if (row < a.O && tok < a.M) {
-      float* op = a.out + (int64_t)tok * a.ldo + row;
-      if (EPI == 0 || EPI == 3) *op = v = y[q];
-      else if (EPI == 1) *op = rv[q] + y[q];
-      else *op = v = (y[q] / (1.0f + expf(-y[q]))) * y2[q];
-    }
-    if (EPI == 2) s_act[col][rrow] = v;
-    if (EPI == 3) s_act[col][rrow] = row < a.O ? v : -INFINITY;
+    const int rrow = 8 * g + 4 * (l >> 5) + q;
     nv[q] = rv[q] + y[q];
+    float v = 0.f;
+    if (EPI == 0 || EPI == 3) v = y[q];
+    else if (EPI == 1) v = nv[q];
+    else v = (y[q] / (1.0f + expf(-y[q]))) * y2[q];
+    ov[q] = v;
+    if (EPI == 2) s_act[col][rrow] = v;
+    if (EPI == 3) s_act[col][rrow] = o0 + rrow < a.O ? v : -INFINITY;
   }
+  if (tok < a.M && o0 + 8 * g + 4 * (l >> 5) < a.O)  // one 16-B store (O % 32 == 0)
+    *reinterpret_cast<float4*>(a.out + (int64_t)tok * a.ldo + o0 + 8 * g + 4 * (l >> 5)) =
+        make_float4(ov[0], ov[1], ov[2], ov[3]);
   if (EPI == 1 && a.ssp_out) {
     // the next NRM GEMM's input (its K = this GEMM's O = 1024): the tile is one q8_0 block of every token, so it
     // quantises z = x_new * qn_w (block scale d_z = amax / 127 left unrounded in f32, dout) into qout, and leaves the
@@ -1355,6 +1353,8 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
   if (!a.ssp && gemm_q8_t(a, K, epi, s)) return;
   if (!a.ssp && g_gemm_q8_kw && gemm_q8_kw(a, K, epi, s)) return;
+  FA_REQUIRE(a.O % 32 == 0 && a.ldo % 4 == 0 && (!a.res || a.ldr % 4 == 0),
+             "gemm_q8: rows must come in whole 32-row tiles with 16-B aligned output / residual rows");
   int NBW, KS;
   gemm_sk_shape(a.O, a.M, K, epi, &NBW, &KS);
   FA_REQUIRE(NBW > 0, "gemm_q8: no split-K shape");
@@ -2786,6 +2786,18 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   load_group<1, 2>(a, row_base, 0, lane, G);
   // down slice: rows [FD_ROWS bi, +FD_ROWS), K columns [FF_GROUP_ROWS grp, +FF_GROUP_ROWS); thread -> row dr, q8_0
   // blocks dk and (dk < 4) dk + 8 of the group's 12
+#if FA_AO_COALESCE
+  // coalesced: load i reads 128 contiguous bytes (chunks 8 i .. 8 i + 7) of each of the wave's 8 rows; lane chunk
+  // c = 8 i + (lane & 7) is half c & 1 of the group's q8_0 block c >> 1
+  const int drow = FD_ROWS * bi + 8 * wave + (lane >> 3), c8 = lane & 7;
+  int4 dwv[3];
+  float dsv[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    dwv[i] = ld_nt16(f.dq + (int64_t)drow * f.F + FF_GROUP_ROWS * grp + 16 * (8 * i + c8));
+    dsv[i] = __half2float(f.dd[(int64_t)drow * (f.F / 32) + GB * grp + 4 * i + (c8 >> 1)]);
+  }
+#else
   const int dr = t >> 3, dk = t & 7;
   const int drow = FD_ROWS * bi + dr;
   const int8_t* wdp = f.dq + (int64_t)drow * f.F + FF_GROUP_ROWS * grp + 32 * dk;
@@ -2794,6 +2806,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   const int4 db0 = ld_nt16(wdp2), db1 = ld_nt16(wdp2 + 16);
   const __half* ddp = f.dd + (int64_t)drow * (f.F / 32) + GB * grp + dk;
   const float ds0 = __half2float(ddp[0]), ds1 = __half2float(ddp[dk < 4 ? 8 : 0]);
+#endif
   __builtin_amdgcn_sched_barrier(0);
   // ---- x_mid = x + sum_g opart[g]; rmsnorm + q8_0 into LDS
 #pragma unroll
@@ -2847,6 +2860,20 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     if ((t & 7) == 0) s_ad[t >> 3] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
+#if FA_AO_COALESCE
+  // ---- down slice: row drow over the group's 12 q8_0 blocks, 4 per load (8 lanes), loads summed in order
+  float v = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    int si = dot16(dwv[i], *reinterpret_cast<const int4*>(s_aq + 16 * (8 * i + c8)), 0);
+    si += dpp_i<DPP_XOR1>(si);  // the block's two halves: exact integer block dot in both lanes of the pair
+    float u = (float)si * (dsv[i] * s_ad[4 * i + (c8 >> 1)]);
+    u += dpp_f<DPP_XOR2>(u);  // 4 blocks (pairs hold duplicates: no xor-1 step)
+    u += dpp_f<DPP_HALF_MIRROR>(u);
+    v += u;
+  }
+  if (c8 == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
+#else
   // ---- down slice: row dr over the group's 12 q8_0 blocks (thread: blocks dk, dk + 8), 8-lane fixed-order sum
   const int4 xa0 = *reinterpret_cast<const int4*>(s_aq + 32 * dk), xa1 = *reinterpret_cast<const int4*>(s_aq + 32 * dk + 16);
   float v = (float)dot16(da1, xa1, dot16(da0, xa0, 0)) * (ds0 * s_ad[dk]);
@@ -2859,6 +2886,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   v += dpp_f<DPP_XOR2>(v);
   v += dpp_f<DPP_HALF_MIRROR>(v);
   if (dk == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
+#endif
 }
 
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
