@@ -2639,6 +2639,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   int pos = a.tok_pos[0];
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
+  STAMP(0);
   // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
   const int KO = a.H * D;
 #if FA_AO_COALESCE
@@ -2679,7 +2680,9 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
       st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
     }
   }
+  STAMP(9);
   fanin_wait(a.cnt + g * CNT_LINE, FS, a.err);
+  STAMP(10);
   // every split combines the n_active partials (combine_splits, as the last arriver of k_attn_block does)
   __shared__ __attribute__((aligned(16))) int8_t s_aq[GQ * D];
   __shared__ float s_ad[GQ * D / 32];
@@ -2696,6 +2699,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     if ((lane & 7) == 0) s_ad[(jj * D + dd) / 32] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
+  STAMP(11);
 #if FA_AO_COALESCE
   const int4 xc = *reinterpret_cast<const int4*>(s_aq + 16 * c16);
   const float xd = s_ad[c16 >> 1];

@@ -27,6 +27,8 @@ int main(int argc, char** argv) {
   // argv[1] = M tokens (default 1: one sequence at n_past 40 / 330 / 700; M > 1: token m is sequence m at
   // n_past 200 + (97 m) % 261, the C3 batch shape)
   const int M = argc > 1 ? atoi(argv[1]) : 1;
+  // argv[2] == "o": the fused batch-1 layer's B launch (k_attn_o: attention + fan-in + combine + o slice), M = 1
+  const bool fused_o = argc > 2 && argv[2][0] == 'o';
   if (const char* e = getenv("FUNASR_ATTN_LEAN")) g_attn_lean = atoi(e);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int H = 16, KV = 8, D = 128, NCTX = 1024, QKV = 4096;
@@ -46,6 +48,13 @@ int main(int argc, char** argv) {
   std::vector<int> hseq(M);
   for (int m = 0; m < M; ++m) hseq[m] = m;
   CK(hipMemcpy(seq, hseq.data(), M * 4, hipMemcpyHostToDevice));
+  int8_t* wo_q = dalloc<int8_t>((size_t)1024 * 2048);
+  __half* wo_d = dalloc<__half>((size_t)1024 * 64);
+  CK(hipMemset(wo_q, 1, (size_t)1024 * 2048)); CK(hipMemset(wo_d, 0, (size_t)1024 * 64 * 2));
+  FusedDecodeWork fw;
+  fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(3072);
+  fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(16 * CNT_LINE); fw.err = dalloc<int>(1);
+  CK(hipMemset(fw.cnt, 0, 16 * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   const int nblk = M * KV * ATTN_SPLITS;
   if (nblk > 4096) { printf("M too large for the stamp buffer\n"); return 1; }
   std::vector<unsigned long long> st((size_t)nblk * 12);
@@ -58,7 +67,11 @@ int main(int argc, char** argv) {
     attn_stamps_clear();
     for (int rep = 0; rep < 30; ++rep) {
       const int l = rep % 28;  // rotate layers: cold K/V like in the engine
-      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, M, H, KV, seq, pos, seq_stride, att, wk, s);
+      if (fused_o)
+        attn_o_fused(qkv, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, H, KV, seq, pos, seq_stride, wo_q, wo_d,
+                     1024, wk, fw, s);
+      else
+        attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, M, H, KV, seq, pos, seq_stride, att, wk, s);
     }
     CK(hipStreamSynchronize(s));
     attn_stamps_read(st.data(), nblk);
@@ -66,10 +79,15 @@ int main(int argc, char** argv) {
     for (int b = 0; b < nblk; ++b) if (st[b * 12]) t0 = std::min(t0, st[b * 12]);
     if (p0 >= 0) printf("decode attention, n_past %d:\n", p0);
     else printf("decode attention, batch %d, n_past 200-460:\n", M);
-    const int slot[] = {0, 1, 3, 7, 11, 9, 10};
-    const char* nm[] = {"block start", "pos/splits known", "q normed/roped", "split merged", "partial stored",
-                        "combine / direct start", "combined out"};
-    for (int k = 0; k < 7; ++k) {
+    const int slot_b[] = {0, 1, 3, 7, 11, 9, 10};
+    const char* nm_b[] = {"block start", "pos/splits known", "q normed/roped", "split merged", "partial stored",
+                          "combine / direct start", "combined out"};
+    const int slot_o[] = {1, 3, 7, 9, 10, 11, -1};
+    const char* nm_o[] = {"splits known", "q normed/roped", "split merged", "partial published", "fan-in passed",
+                          "combined + quantised", ""};
+    const int* slot = fused_o ? slot_o : slot_b;
+    const char* const* nm = fused_o ? nm_o : nm_b;
+    for (int k = 0; k < (fused_o ? 6 : 7); ++k) {
       std::vector<double> v;
       for (int b = 0; b < nblk; ++b) {  // stamps left by an earlier launch (before t0) are not this launch's
         const long long d = (long long)(st[b * 12 + slot[k]] - t0);
