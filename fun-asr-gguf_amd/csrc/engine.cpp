@@ -1104,7 +1104,10 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
     // A/B knobs of the decode GEMV: fused-GEMV batch limit (0..7; lm_head partials are sized for <= 7) and
     // tokens per fused-GEMV block (1 or 2: the instantiated and tested variants)
-    if (const char* g = getenv("FUNASR_GEMV_SMALL")) fa::g_gemv_small_max = std::min(7, std::max(0, atoi(g)));
+    {  // process-wide decode-path knob: re-read (or reset to the default 5) at every engine creation
+      const char* g = getenv("FUNASR_GEMV_SMALL");
+      fa::g_gemv_small_max = g ? std::min(7, std::max(0, atoi(g))) : 5;
+    }
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;

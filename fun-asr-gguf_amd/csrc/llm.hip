@@ -1305,13 +1305,13 @@ int gemv_rows_per_wave(int O) {
   return rpw < 1 ? 1 : rpw;
 }
 
-// decode batches up to g_gemv_small_max tokens take the fused GEMV (above: prep + MFMA GEMM); from 3 tokens on,
-// g_gemv_mt tokens share a block (weights streamed once per block for its tokens). Measured decode step (full
-// model, graph-replayed, scripts/prof_batch_decode.py): batch 3 / 4 / 5 / 6 / 7 = 0.82 / 0.94 / 1.03 / 1.15 /
-// 1.21 ms with 2 tokens per block, vs 0.86 / 0.97 / 1.11 / 1.21 / 1.35 with one token per block and 0.86 / 0.97 /
-// 1.25 / 1.26 / 1.29 on the MFMA GEMM; batch 8 and up: the MFMA GEMM (1.30 vs 1.35). More tokens per block
-// serialise more prologue / dot work per block than the saved weight re-reads (MT 4 / 8: slower).
-int g_gemv_small_max = 7;
+// decode batches up to g_gemv_small_max tokens take the fused GEMV (above: the MFMA GEMM with producer-normalised
+// inputs); from 3 tokens on, g_gemv_mt tokens share a block (weights streamed once per block for its tokens). Measured
+// decode step (full model, graph-replayed, scripts/prof_batch_decode.py, after the coalesced split-K loads): batch
+// 2 / 3 / 4 / 5 / 6 / 7 = 0.711 / 0.822 / 0.945 / 1.004 / 1.143 / 1.210 ms on the fused GEMV vs 1.010 / 1.043 / 1.041 /
+// 1.038 / 1.063 / 1.081 on the MFMA GEMM: the GEMV up to 5 tokens. More tokens per block serialise more prologue / dot
+// work per block than the saved weight re-reads (MT 4 / 8: slower).
+int g_gemv_small_max = 5;
 int g_gemv_mt = 2;
 
 bool gemv_small(int M) { return M <= g_gemv_small_max; }
