@@ -743,6 +743,17 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
                      reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
+// microbenchmark helper: resident blocks per CU of the 128x128x32 bf16x3 kernel (linear epilogue), its dynamic LDS
+int gemm_bf3_occupancy_128() {
+  using T = TileB3<2, 2, 32>;
+  const size_t lds = 2 * T::STAGE * 2;
+  (void)hipFuncSetAttribute((const void*)k_gemm_bf3<ALoadPlain, EpiLinear, 2, 2, 32, 1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int n = -1;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gemm_bf3<ALoadPlain, EpiLinear, 2, 2, 32, 1>, 256, lds);
+  return n;
+}
+
 template <class AL, class EPI>
 static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
   const int f = g_gemm_bf3_force;

@@ -9,6 +9,7 @@
 namespace fa {
 extern int g_gemm_f32_force;
 extern int g_gemm_bf3_force;
+int gemm_bf3_occupancy_128();
 extern int g_gemm_ks_force;
 void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
 void log(int, const std::string&) {}
@@ -130,6 +131,7 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  printf("bf3 128x128x32: %d resident blocks per CU\n", gemm_bf3_occupancy_128());
   printf("row stride pad %d floats\n", pad);
   for (int M : {1001, 32032}) {
     if (pad && M > 2000) break;
