@@ -11,7 +11,6 @@ Differences in *mechanism* only (results are the reference's):
 """
 import codecs
 import time
-from concurrent.futures import ThreadPoolExecutor
 from typing import List, Optional
 
 import numpy as np
@@ -210,24 +209,15 @@ class StreamDecoder:
         # 4. LLM with the reference's retry policy (decoder.py:201-211), per sequence
         final = self.llm_decoder.decode_with_retry(embds, m.config.n_predict, temperature, top_p, top_k, reporter,
                                                    verbose)
-        # 5. char timestamps: the native DP releases the GIL, so a batch aligns its streams on a few host threads
-        texts = [final[b].text.strip() for b in range(B)]
-        t = time.perf_counter()
-        jobs = [(ctc_results[b], texts[b]) for b in range(B)]
-        if B > 1:
-            with ThreadPoolExecutor(max_workers=min(8, B)) as pool:
-                aligned_all = list(pool.map(lambda j: align_timestamps(*j) if j[0] else None, jobs))
-        else:
-            aligned_all = [align_timestamps(*jobs[0]) if jobs[0][0] else None]
-        t_align = (time.perf_counter() - t) / B
         results = []
         for b in range(B):
             r = final[b]
-            text = texts[b]
+            text = r.text.strip()
             tm = timings[b]
             tm.inject, tm.llm_generate = r.t_inject, r.t_gen
-            aligned = aligned_all[b]
-            tm.align = t_align
+            t = time.perf_counter()
+            aligned = align_timestamps(ctc_results[b], text) if ctc_results[b] else None
+            tm.align = time.perf_counter() - t
             toks = [a["char"] for a in aligned] if aligned else []
             ts = [a["start"] for a in aligned] if aligned else []
             streams[b].set_result(text=text, timestamps=ts, tokens=toks)
