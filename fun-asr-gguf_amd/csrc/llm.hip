@@ -545,9 +545,6 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
 // rstd = 1/sqrtf(sum/K + eps) scales every block uniformly, so the q8_0 rows of y = (x * rstd) * w are the same
 // integers (up to float rounding at .5 ties) with scale f16(rstd * d_z): this GEMM only applies rstd, and the two
 // k_prep_q8 launches per layer (with their kernel boundaries) disappear.
-#ifndef FA_SK_COALESCE
-#define FA_SK_COALESCE 1
-#endif
 template <int EPI, int NBW, int KSM, bool NRM = false>
 __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
@@ -560,9 +557,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   const int bw0 = (ks * WPM + (EPI == 2 ? (wave & 1) : wave)) * NBW;  // host: nb == KS * WPM * NBW
   const int8_t* wq = upw ? a.wq2 : a.wq;
   const __half* wd = upw ? a.wd2 : a.wd;
-  const int8_t* wa = wq + (int64_t)min(o0 + r, a.O - 1) * K + 16 * h + bw0 * 32;
   const int t_b = min(t0 + r, a.M - 1);
-  const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + bw0 * 32;
   KSTAMP(0);
   float4 sv[NRM ? 8 : 1];
   if constexpr (NRM) {  // this lane's token's 32 partials, issued first (vmcnt retires in issue order)
@@ -570,14 +565,11 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     for (int i = 0; i < 8; ++i) sv[i] = *reinterpret_cast<const float4*>(a.ssp + (int64_t)t_b * 32 + 4 * i);
   }
   i32x4_t A[NBW], B[NBW];
-#if FA_SK_COALESCE
   // coalesced: load instruction i reads RPI rows x RB contiguous bytes of the wave's K slice (weights and activations);
   // the fragments are rebuilt through LDS below (16 B per lane from 32 rows per instruction ran the LM head at a third
   // of the coalesced rate)
   constexpr int RB = NBW * 32, LPR = RB / 16, RPI = 64 / LPR, SLD = RB + 16;
   __shared__ __attribute__((aligned(16))) int8_t s_ab[4][2][32 * SLD];
-  (void)wa;
-  (void)xb;
   {
     const int rr = lane / LPR, off = bw0 * 32 + 16 * (lane % LPR);
 #pragma unroll
@@ -586,13 +578,6 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
       B[i] = *reinterpret_cast<const i32x4_t*>(a.xq + (int64_t)min(t0 + RPI * i + rr, a.M - 1) * K + off);
     }
   }
-#else
-#pragma unroll
-  for (int j = 0; j < NBW; ++j) {
-    A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
-    B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
-  }
-#endif
   uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg)
@@ -628,7 +613,6 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
   const i32x16_t zero = {};
-#if FA_SK_COALESCE
   {  // rows -> LDS, then the MFMA layout: lane (r, h) -> row r, 16 B half h of block j
     const int rr = lane / LPR, cb = 16 * (lane % LPR);
 #pragma unroll
@@ -645,7 +629,6 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
       B[j] = *reinterpret_cast<const i32x4_t*>(&s_ab[wave][1][r * SLD + 32 * j + 16 * h]);
     }
   }
-#endif
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
@@ -657,15 +640,10 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     }
   }
   // fixed-order reduction over the waves
-#if FA_SK_COALESCE
   // s_red[w] in wave w's own staging image (written after the wave read its fragments, read after the barrier)
   static_assert(16 * 64 * 4 <= 2 * 32 * SLD, "k_gemm_q8_sk: wave partials must fit the wave's staging image");
   float(&s_red)[4][2 * 32 * SLD / 4] = *reinterpret_cast<float(*)[4][2 * 32 * SLD / 4]>(&s_ab[0][0][0]);
 #define SRED(w, reg, l) s_red[w][(reg) * 64 + (l)]
-#else
-  __shared__ float s_red[4][16][64];
-#define SRED(w, reg, l) s_red[w][reg][l]
-#endif
   __shared__ float s_act[EPI >= 2 ? 32 : 1][33];  // tile [token][row]: SwiGLU q8_0 epilogue, lm_head argmax
   __shared__ int s_last;
 #pragma unroll
@@ -2605,10 +2583,6 @@ __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) 
 
 constexpr int FO_ROWS = 64;  // o-projection rows per split block (E / ASPLIT, E = 1024)
 
-#ifndef FA_AO_COALESCE
-#define FA_AO_COALESCE 1
-#endif
-
 struct AttnOArgs {
   const int* tok_seq;
   const int* tok_pos;
@@ -2642,7 +2616,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   STAMP(0);
   // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
   const int KO = a.H * D;
-#if FA_AO_COALESCE
   // coalesced: load k reads rows 16 wave + 4 k + (lane >> 4) of the slice, 256 contiguous bytes each; lane chunk
   // c = lane & 15 is half c & 1 of q8_0 block c >> 1 of the head pair's 256 columns
   const int c16 = lane & 15;
@@ -2654,14 +2627,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     wk[k] = ld_nt16(a.wo_q + (int64_t)orow * KO + GQ * D * g + 16 * c16);
     dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
   }
-#else
-  const int tr = threadIdx.x >> 2, tq = threadIdx.x & 3;
-  const int orow = FO_ROWS * sp + tr;
-  const int8_t* wp = a.wo_q + (int64_t)orow * KO + GQ * D * g + 64 * tq;
-  const int4 w0 = ld_nt16(wp), w1 = ld_nt16(wp + 16), w2 = ld_nt16(wp + 32), w3 = ld_nt16(wp + 48);
-  const __half* dp = a.wo_d + (int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + 2 * tq;
-  const float dw0 = __half2float(dp[0]), dw1 = __half2float(dp[1]);
-#endif
   __builtin_amdgcn_sched_barrier(0);
   int n_active = 0, j = 0, d0 = 0;
   float M = -INFINITY, L = 0.f;
@@ -2700,7 +2665,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   }
   __syncthreads();
   STAMP(11);
-#if FA_AO_COALESCE
   const int4 xc = *reinterpret_cast<const int4*>(s_aq + 16 * c16);
   const float xd = s_ad[c16 >> 1];
 #pragma unroll
@@ -2713,15 +2677,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     v += dpp_f<DPP_MIRROR>(v);
     if (c16 == 0) a.opart[(int64_t)g * a.E + FO_ROWS * sp + 16 * wave + 4 * k + (lane >> 4)] = v;
   }
-#else
-  const int4 x0 = *reinterpret_cast<const int4*>(s_aq + 64 * tq), x1 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 16);
-  const int4 x2 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 32), x3 = *reinterpret_cast<const int4*>(s_aq + 64 * tq + 48);
-  const int s0 = dot16(w1, x1, dot16(w0, x0, 0)), s1 = dot16(w3, x3, dot16(w2, x2, 0));
-  float v = (float)s0 * (dw0 * s_ad[2 * tq]) + (float)s1 * (dw1 * s_ad[2 * tq + 1]);
-  v += dpp_f<DPP_XOR1>(v);  // the row's 4 threads are 4 consecutive lanes: fixed-order quad sum
-  v += dpp_f<DPP_XOR2>(v);
-  if (tq == 0) a.opart[(int64_t)g * a.E + orow] = v;
-#endif
 }
 
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
@@ -2790,7 +2745,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   load_group<1, 2>(a, row_base, 0, lane, G);
   // down slice: rows [FD_ROWS bi, +FD_ROWS), K columns [FF_GROUP_ROWS grp, +FF_GROUP_ROWS); thread -> row dr, q8_0
   // blocks dk and (dk < 4) dk + 8 of the group's 12
-#if FA_AO_COALESCE
   // coalesced: load i reads 128 contiguous bytes (chunks 8 i .. 8 i + 7) of each of the wave's 8 rows; lane chunk
   // c = 8 i + (lane & 7) is half c & 1 of the group's q8_0 block c >> 1
   const int drow = FD_ROWS * bi + 8 * wave + (lane >> 3), c8 = lane & 7;
@@ -2801,16 +2755,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     dwv[i] = ld_nt16(f.dq + (int64_t)drow * f.F + FF_GROUP_ROWS * grp + 16 * (8 * i + c8));
     dsv[i] = __half2float(f.dd[(int64_t)drow * (f.F / 32) + GB * grp + 4 * i + (c8 >> 1)]);
   }
-#else
-  const int dr = t >> 3, dk = t & 7;
-  const int drow = FD_ROWS * bi + dr;
-  const int8_t* wdp = f.dq + (int64_t)drow * f.F + FF_GROUP_ROWS * grp + 32 * dk;
-  const int4 da0 = ld_nt16(wdp), da1 = ld_nt16(wdp + 16);
-  const int8_t* wdp2 = wdp + 32 * 8 * (dk < 4 ? 1 : 0);
-  const int4 db0 = ld_nt16(wdp2), db1 = ld_nt16(wdp2 + 16);
-  const __half* ddp = f.dd + (int64_t)drow * (f.F / 32) + GB * grp + dk;
-  const float ds0 = __half2float(ddp[0]), ds1 = __half2float(ddp[dk < 4 ? 8 : 0]);
-#endif
   __builtin_amdgcn_sched_barrier(0);
   // ---- x_mid = x + sum_g opart[g]; rmsnorm + q8_0 into LDS
 #pragma unroll
@@ -2864,7 +2808,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     if ((t & 7) == 0) s_ad[t >> 3] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
-#if FA_AO_COALESCE
   // ---- down slice: row drow over the group's 12 q8_0 blocks, 4 per load (8 lanes), loads summed in order
   float v = 0.f;
 #pragma unroll
@@ -2877,20 +2820,6 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     v += u;
   }
   if (c8 == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
-#else
-  // ---- down slice: row dr over the group's 12 q8_0 blocks (thread: blocks dk, dk + 8), 8-lane fixed-order sum
-  const int4 xa0 = *reinterpret_cast<const int4*>(s_aq + 32 * dk), xa1 = *reinterpret_cast<const int4*>(s_aq + 32 * dk + 16);
-  float v = (float)dot16(da1, xa1, dot16(da0, xa0, 0)) * (ds0 * s_ad[dk]);
-  if (dk < 4) {
-    const int4 xb0 = *reinterpret_cast<const int4*>(s_aq + 32 * (dk + 8));
-    const int4 xb1 = *reinterpret_cast<const int4*>(s_aq + 32 * (dk + 8) + 16);
-    v = v + (float)dot16(db1, xb1, dot16(db0, xb0, 0)) * (ds1 * s_ad[dk + 8]);
-  }
-  v += dpp_f<DPP_XOR1>(v);
-  v += dpp_f<DPP_XOR2>(v);
-  v += dpp_f<DPP_HALF_MIRROR>(v);
-  if (dk == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
-#endif
 }
 
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
