@@ -1671,7 +1671,7 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
                                                  const float* __restrict__ qn, const float* __restrict__ kn,
                                                  const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
                                                  float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
-                                                 float4& o) {
+                                                 float4& o, const AttnQIn* pre = nullptr) {
   constexpr int D = 128;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_keys = pos + 1;
@@ -1704,7 +1704,11 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   const int g0 = gb + wave;
   if (g0 < ge) {
     AttnQIn qi;
-    if (DM) {
+    if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read
+      qi = *pre;
+      qi.c = rcos[(int64_t)pos * 64 + lane];
+      qi.sn = rsin[(int64_t)pos * 64 + lane];
+    } else if (DM) {
       const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
       for (int j = 0; j < GQ; ++j) {
@@ -2610,6 +2614,26 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int g = blockIdx.x, sp = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // q|k|v row inputs do not depend on the position: issued before the tok_pos / tok_seq read (one round trip less
+  // on the critical path than loading them after it)
+  AttnQIn qpre;
+  {
+    const float* row = a.qkv;  // token 0
+#pragma unroll
+    for (int jh = 0; jh < GQ; ++jh) {
+      qpre.x0[jh] = row[(g * GQ + jh) * D + lane];
+      qpre.x1[jh] = row[(g * GQ + jh) * D + lane + 64];
+    }
+    qpre.w0 = a.qn[lane];
+    qpre.w1 = a.qn[lane + 64];
+    qpre.kx0 = row[(a.H + g) * D + lane];
+    qpre.kx1 = row[(a.H + g) * D + lane + 64];
+    qpre.kw0 = a.kn[lane];
+    qpre.kw1 = a.kn[lane + 64];
+    qpre.v0 = row[(a.H + a.KV + g) * D + lane];
+    qpre.v1 = row[(a.H + a.KV + g) * D + lane + 64];
+    qpre.c = qpre.sn = 0.f;
+  }
   int pos = a.tok_pos[0];
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
@@ -2633,7 +2657,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
   const bool active = attn_split_merge<1, 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
                                              a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
-                                             M, L, o);
+                                             M, L, o, &qpre);
   float* pbase = a.partials + (int64_t)g * FS * APART;
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
   if (active && wave == 0) {
