@@ -2742,6 +2742,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
   const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
+  STAMP(0);
   __shared__ __attribute__((aligned(16))) int8_t s_q[K];
   __shared__ float s_d[NB];
   __shared__ float s_red[4];
@@ -2791,6 +2792,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   if (b == 0) *reinterpret_cast<float4*>(f.xmid + t * PER) = make_float4(xv[0], xv[1], xv[2], xv[3]);
   norm_quant_block_regs<PER>(xv, wv, true, f.eps, K, s_q, s_d, s_red);
   __syncthreads();
+  STAMP(1);
   // ---- gate|up + SwiGLU for this wave's 3 rows (compute_group's arithmetic)
   {
     float acc[3] = {0.f, 0.f, 0.f}, acc2[3] = {0.f, 0.f, 0.f};
@@ -2819,7 +2821,9 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     const f4v v = {s_act[4 * t], s_act[4 * t + 1], s_act[4 * t + 2], s_act[4 * t + 3]};
     st_sc1_f4(v, ra, (FF_ROWS * b + 4 * t) * 4);
   }
+  STAMP(2);
   fanin_wait(f.cnt + grp * CNT_LINE, FF_GROUP_BLOCKS, f.err);
+  STAMP(3);
   // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
   if (t < FF_GROUP_ROWS / 4) {
     const f4v v = ld_sc1_f4(ra, (FF_GROUP_ROWS * grp + 4 * t) * 4);
@@ -2832,6 +2836,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     if ((t & 7) == 0) s_ad[t >> 3] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
+  STAMP(4);
   // ---- down slice: row drow over the group's 12 q8_0 blocks, 4 per load (8 lanes), loads summed in order
   float v = 0.f;
 #pragma unroll
@@ -2844,6 +2849,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     v += u;
   }
   if (c8 == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
+  STAMP(5);
 }
 
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,

@@ -29,6 +29,8 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 1;
   // argv[2] == "o": the fused batch-1 layer's B launch (k_attn_o: attention + fan-in + combine + o slice), M = 1
   const bool fused_o = argc > 2 && argv[2][0] == 'o';
+  // argv[2] == "c": the fused layer's C launch (k_ffn_fused: x_mid + norm + gate|up + group fan-in + down slice)
+  const bool fused_c = argc > 2 && argv[2][0] == 'c';
   if (const char* e = getenv("FUNASR_ATTN_LEAN")) g_attn_lean = atoi(e);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int H = 16, KV = 8, D = 128, NCTX = 1024, QKV = 4096;
@@ -48,14 +50,17 @@ int main(int argc, char** argv) {
   std::vector<int> hseq(M);
   for (int m = 0; m < M; ++m) hseq[m] = m;
   CK(hipMemcpy(seq, hseq.data(), M * 4, hipMemcpyHostToDevice));
+  int8_t* wg_q = dalloc<int8_t>((size_t)3072 * 1024);  // gate / up stand-in [3072][1024], down [1024][3072]
+  int8_t* wd_q = dalloc<int8_t>((size_t)1024 * 3072);
+  CK(hipMemset(wg_q, 1, (size_t)3072 * 1024)); CK(hipMemset(wd_q, 1, (size_t)1024 * 3072));
   int8_t* wo_q = dalloc<int8_t>((size_t)1024 * 2048);
-  __half* wo_d = dalloc<__half>((size_t)1024 * 64);
-  CK(hipMemset(wo_q, 1, (size_t)1024 * 2048)); CK(hipMemset(wo_d, 0, (size_t)1024 * 64 * 2));
+  __half* wo_d = dalloc<__half>((size_t)3072 * 96);  // scales for every stand-in matrix (zeros)
+  CK(hipMemset(wo_q, 1, (size_t)1024 * 2048)); CK(hipMemset(wo_d, 0, (size_t)3072 * 96 * 2));
   FusedDecodeWork fw;
   fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(3072);
   fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(16 * CNT_LINE); fw.err = dalloc<int>(1);
   CK(hipMemset(fw.cnt, 0, 16 * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
-  const int nblk = M * KV * ATTN_SPLITS;
+  const int nblk = fused_c ? 256 : M * KV * ATTN_SPLITS;
   if (nblk > 4096) { printf("M too large for the stamp buffer\n"); return 1; }
   std::vector<unsigned long long> st((size_t)nblk * 12);
   std::vector<int> cases = M == 1 ? std::vector<int>{40, 330, 700} : std::vector<int>{-1};
@@ -67,7 +72,9 @@ int main(int argc, char** argv) {
     attn_stamps_clear();
     for (int rep = 0; rep < 30; ++rep) {
       const int l = rep % 28;  // rotate layers: cold K/V like in the engine
-      if (fused_o)
+      if (fused_c)
+        ffn_fused(qkv, qkv + 1024, 1e-6f, wg_q, wo_d, wg_q, wo_d, wd_q, wo_d, 1024, 3072, fw, s);
+      else if (fused_o)
         attn_o_fused(qkv, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, H, KV, seq, pos, seq_stride, wo_q, wo_d,
                      1024, wk, fw, s);
       else
@@ -85,9 +92,12 @@ int main(int argc, char** argv) {
     const int slot_o[] = {1, 3, 7, 9, 10, 11, -1};
     const char* nm_o[] = {"splits known", "q normed/roped", "split merged", "partial published", "fan-in passed",
                           "combined + quantised", ""};
-    const int* slot = fused_o ? slot_o : slot_b;
-    const char* const* nm = fused_o ? nm_o : nm_b;
-    for (int k = 0; k < (fused_o ? 6 : 7); ++k) {
+    const int slot_c[] = {0, 1, 2, 3, 4, 5, -1};
+    const char* nm_c[] = {"block start", "x normed + q8", "act published", "group fan-in passed", "act quantised",
+                          "down slice stored", ""};
+    const int* slot = fused_c ? slot_c : fused_o ? slot_o : slot_b;
+    const char* const* nm = fused_c ? nm_c : fused_o ? nm_o : nm_b;
+    for (int k = 0; k < (fused_c || fused_o ? 6 : 7); ++k) {
       std::vector<double> v;
       for (int b = 0; b < nblk; ++b) {  // stamps left by an earlier launch (before t0) are not this launch's
         const long long d = (long long)(st[b * 12 + slot[k]] - t0);
