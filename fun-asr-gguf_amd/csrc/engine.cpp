@@ -140,6 +140,11 @@ struct Engine {
   int *d_tok_seq = nullptr, *d_tok_pos = nullptr, *d_step = nullptr, *d_tok_cur = nullptr, *d_tok_hist = nullptr,
       *d_ids = nullptr;
   int hist_max = 0;
+  int* h_hist = nullptr;           // pinned host copy of the sampled-token history (fa_llm_generate_begin / _end)
+  hipEvent_t ev_gen = nullptr;     // recorded after that copy
+  bool gen_pending = false;        // a generate call is in flight
+  std::vector<int> gen_seqs;       // its sequences (row order) and steps
+  int gen_steps = 0;
   SampleParams* d_samp = nullptr;  // sampler chain parameters of the current call (read by the sampler launch)
   SampleParams h_samp{};
   std::vector<int> n_past, last_tok;
@@ -187,6 +192,8 @@ struct Engine {
       hipEventDestroy(e.second);
     }
     for (void* p : allocs) hipFree(p);
+    if (h_hist) hipHostFree(h_hist);
+    if (ev_gen) hipEventDestroy(ev_gen);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -624,6 +631,8 @@ struct Engine {
     d_tok_cur = alloc<int>(lc.max_seqs);
     hist_max = 4096;
     d_tok_hist = alloc<int>((size_t)lc.max_seqs * hist_max);
+    FA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_hist), (size_t)lc.max_seqs * hist_max * 4, hipHostMallocDefault));
+    FA_HIP(hipEventCreateWithFlags(&ev_gen, hipEventDisableTiming));
     d_ids = alloc<int>(m_max);
     d_samp = alloc<SampleParams>(1);
     attn_wk.max_tokens = pf_max;
@@ -1384,6 +1393,7 @@ int fa_embd_rows(fa_engine* h, const int32_t* ids, int32_t n, int32_t fp16_round
 int fa_llm_reset(fa_engine* h, int32_t seq) {
   FA_API_BEGIN
   Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   e->n_past[seq] = 0;
   e->last_tok[seq] = -1;
@@ -1395,6 +1405,7 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
                    int32_t* tok_out, float* logits_out) {
   FA_API_BEGIN
   Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   FA_REQUIRE(n_tokens >= 1 && e->n_past[seq] + n_tokens <= e->lc.n_ctx, "prefill exceeds n_ctx");
   const int E = e->lc.n_embd;
@@ -1427,6 +1438,7 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
                          const fa_sampling* s, int32_t* tok_out) {
   FA_API_BEGIN
   Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs, "prefill batch: n_seqs out of range");
   const int E = e->lc.n_embd;
   std::vector<char> seen(e->lc.max_seqs, 0);
@@ -1485,10 +1497,10 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
   FA_API_END
 }
 
-int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
-                    int32_t* tokens_out) {
+int fa_llm_generate_begin(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s) {
   FA_API_BEGIN
   Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is already in flight (fa_llm_generate_end first)");
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs && n_steps >= 1 && n_steps <= e->hist_max, "generate args");
   std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0);
   std::vector<char> seen(e->lc.max_seqs, 0);
@@ -1518,24 +1530,48 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   } else {
     for (int st = 0; st < n_steps; ++st) e->decode_step(n_seqs);
   }
-  std::vector<int> hist((size_t)n_seqs * e->hist_max);
-  FA_HIP(hipMemcpyAsync(hist.data(), e->d_tok_hist, hist.size() * 4, hipMemcpyDeviceToHost, e->stream));
-  FA_HIP(hipStreamSynchronize(e->stream));
+  // the sampled tokens land in pinned host memory; fa_llm_generate_end waits for them (the host may work meanwhile)
+  FA_HIP(hipMemcpyAsync(e->h_hist, e->d_tok_hist, (size_t)n_seqs * e->hist_max * 4, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipEventRecord(e->ev_gen, e->stream));
+  e->gen_seqs = sq;
+  e->gen_steps = n_steps;
+  e->gen_pending = true;
+  FA_API_END
+}
+
+int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(e->gen_pending, "no generate call in flight");
+  e->gen_pending = false;
+  FA_HIP(hipEventSynchronize(e->ev_gen));
+  const int n_seqs = (int)e->gen_seqs.size(), n_steps = e->gen_steps;
   e->prof_collect();
   if (n_seqs == 1) e->check_fused_error();
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
-    for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hist[(size_t)i * e->hist_max + st];
-    e->n_past[seqs[i]] += n_steps;
-    e->last_tok[seqs[i]] = hist[(size_t)i * e->hist_max + n_steps - 1];
-    e->logits_row[seqs[i]] = i;
+    const int q = e->gen_seqs[i];
+    const int* hrow = e->h_hist + (size_t)i * e->hist_max;
+    if (tokens_out)
+      for (int st = 0; st < n_steps; ++st) tokens_out[(size_t)i * n_steps + st] = hrow[st];
+    e->n_past[q] += n_steps;
+    e->last_tok[q] = hrow[n_steps - 1];
+    e->logits_row[q] = i;
   }
   FA_API_END
+}
+
+int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
+                    int32_t* tokens_out) {
+  const int rc = fa_llm_generate_begin(h, seqs, n_seqs, n_steps, s);
+  if (rc != FA_OK) return rc;
+  return fa_llm_generate_end(h, tokens_out);
 }
 
 int fa_llm_logits(fa_engine* h, int32_t seq, float* out) {
   FA_API_BEGIN
   Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   const int row = e->logits_row[seq];
   FA_REQUIRE(row >= 0, "fa_llm_logits: the most recent forward did not include this sequence");

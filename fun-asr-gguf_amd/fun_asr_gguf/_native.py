@@ -15,7 +15,8 @@ EXPORTS = [
     "fa_engine_create", "fa_engine_destroy", "fa_last_error", "fa_set_log_callback", "fa_weights_synthetic",
     "fa_set_tensor_f32", "fa_set_tensor_q8_0", "fa_load_gguf", "fa_get_tensor_q8_0", "fa_encode",
     "fa_encode_device", "fa_encode_fetch", "fa_ctc_collapse", "fa_set_debug", "fa_encode_tap", "fa_embd_rows",
-    "fa_llm_reset", "fa_llm_prefill", "fa_llm_prefill_batch", "fa_llm_generate", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
+    "fa_llm_reset", "fa_llm_prefill", "fa_llm_prefill_batch", "fa_llm_generate", "fa_llm_generate_begin",
+    "fa_llm_generate_end", "fa_llm_logits", "fa_llm_n_past", "fa_profile_enable",
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
@@ -79,6 +80,8 @@ def load():
     lib.fa_llm_reset.argtypes = [P, I32]
     lib.fa_llm_prefill.argtypes = [P, I32, P, I32, ctypes.POINTER(Sampling), P, P]
     lib.fa_llm_generate.argtypes = [P, P, I32, I32, ctypes.POINTER(Sampling), P]
+    lib.fa_llm_generate_begin.argtypes = [P, P, I32, I32, ctypes.POINTER(Sampling)]
+    lib.fa_llm_generate_end.argtypes = [P, P]
     lib.fa_llm_prefill_batch.argtypes = [P, P, I32, P, P, ctypes.POINTER(Sampling), P]
     lib.fa_llm_logits.argtypes = [P, I32, P]
     lib.fa_llm_n_past.argtypes = [P, I32, P]
@@ -292,6 +295,20 @@ class Engine:
         s = self._sampling(**samp)
         _check(self.lib.fa_llm_generate(self.h, _ptr(sq), sq.size, n_steps, ctypes.byref(s), _ptr(out)),
                "fa_llm_generate")
+        return out
+
+    def llm_generate_begin(self, seqs, n_steps, **samp):
+        """Enqueue n_steps decode steps for `seqs` and return at once (fa_llm_generate_begin); the tokens come from
+        llm_generate_end(). The host may process earlier tokens in between."""
+        sq = np.ascontiguousarray(seqs, dtype=np.int32)
+        s = self._sampling(**samp)
+        _check(self.lib.fa_llm_generate_begin(self.h, _ptr(sq), sq.size, n_steps, ctypes.byref(s)), "fa_llm_generate_begin")
+        self._gen_shape = (sq.size, n_steps)
+        return self._gen_shape
+
+    def llm_generate_end(self):
+        out = np.empty(self._gen_shape, np.int32)
+        _check(self.lib.fa_llm_generate_end(self.h, _ptr(out)), "fa_llm_generate_end")
         return out
 
     def llm_logits(self, seq=0):

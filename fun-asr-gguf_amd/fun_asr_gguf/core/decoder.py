@@ -113,14 +113,34 @@ class LLMDecoder:
             states.append(st)
             res.append(r)
         t_gen = time.perf_counter()
-        while True:
-            active = [s for s, st in enumerate(states) if not st.done]
-            if not active:
-                break
-            chunk = min(GEN_CHUNK, max(states[s].remaining() for s in active))
-            toks = eng.llm_generate(active, chunk, **samp)
+        stop_ids = np.array(sorted({self.models.eos_token} | set(STOP_TOKENS)), np.int64)
+        active = [s for s, st in enumerate(states) if not st.done]
+        chunk = min(GEN_CHUNK, max(states[s].remaining() for s in active)) if active else 0
+        if active:
+            eng.llm_generate_begin(active, chunk, **samp)
+        while active:
+            toks = eng.llm_generate_end()
+            # the sequences this chunk leaves unfinished, from the token ids alone (stop ids, n_predict), go into the
+            # next chunk, which is enqueued BEFORE the host detokenises this one (the host work overlaps the GPU's);
+            # a sequence the repetition breaker cuts during feed() rides along one chunk and its tokens are ignored
+            nxt, left_after = [], []
+            for row, s in enumerate(active):
+                st = states[s]
+                left = st.remaining()
+                if left <= 0:
+                    continue
+                used = toks[row][:min(chunk, left)]
+                if not st.ignore_eos and np.isin(used, stop_ids).any():
+                    continue
+                if left > chunk:
+                    nxt.append(s)
+                    left_after.append(left - chunk)
+            nchunk = min(GEN_CHUNK, max(left_after)) if nxt else 0
+            if nxt:
+                eng.llm_generate_begin(nxt, nchunk, **samp)
             for row, s in enumerate(active):
                 states[s].feed(toks[row])
+            active, chunk = nxt, nchunk
         dt = time.perf_counter() - t_gen
         for st, r in zip(states, res):
             st.ps.flush()

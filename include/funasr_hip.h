@@ -141,6 +141,13 @@ int fa_llm_prefill_batch(fa_engine* e, const int32_t* seqs, int32_t n_seqs, cons
  * (decoder.py:91-98). tokens_out [n_seqs, n_steps]. No host round trip inside the call. */
 int fa_llm_generate(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s,
                     int32_t* tokens_out);
+/* fa_llm_generate in two halves: _begin validates, enqueues the n_steps graph replays and the copy of the sampled
+ * tokens into pinned host memory, and returns at once; _end waits for that copy and does the host bookkeeping
+ * (positions, last tokens, logits rows), writing the tokens as fa_llm_generate does (tokens_out may be NULL). One call
+ * in flight per engine; the other fa_llm_* calls refuse while it is. The host can work on the previous chunk's tokens
+ * in between (the llama_decode loop of decoder.py:91-98 has no such overlap: its sampling is on the host). */
+int fa_llm_generate_begin(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s);
+int fa_llm_generate_end(fa_engine* e, int32_t* tokens_out);
 /* Logits [n_vocab] of sequence `seq` from the most recent forward (fa_llm_prefill, or the last step of
  * fa_llm_generate) when that forward included it; FA_ERR_ARG otherwise (test hook; llama_get_logits_ith). */
 int fa_llm_logits(fa_engine* e, int32_t seq, float* out);

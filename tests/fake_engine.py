@@ -70,6 +70,13 @@ class FakeEngine:
                 out[r, k] = 1000 + self.seqs[s] % 40
         return out
 
+    def llm_generate_begin(self, seqs, n, **samp):
+        self._pending = self.llm_generate(seqs, n, **samp)
+
+    def llm_generate_end(self):
+        out, self._pending = self._pending, None
+        return out
+
 
 def fake_models(max_batch=4, n_predict=24):
     cfg = ASREngineConfig(encoder_onnx_path="synthetic", ctc_onnx_path="synthetic", decoder_gguf_path="synthetic",

@@ -67,6 +67,14 @@ class FakeEngine:
         self.calls.append(("generate", tuple(seqs), n))
         return out
 
+    def llm_generate_begin(self, seqs, n, temperature=0.0, **kw):
+        assert getattr(self, "_pending", None) is None, "one generate call in flight"
+        self._pending = self.llm_generate(seqs, n, temperature=temperature, **kw)
+
+    def llm_generate_end(self):
+        out, self._pending = self._pending, None
+        return out
+
 
 class FakeModels:
     def __init__(self, scripts, n_predict, base_temp, ignore_eos=False):

@@ -442,3 +442,35 @@ def test_llm_prefill_batch_continuation_query_tiles(llm_tiny_oracle, monkeypatch
         _check_step(e.llm_logits(0), m.forward(prompts[0], 0))
     finally:
         e.close()
+
+
+def test_llm_generate_begin_end_equals_generate(llm_tiny_oracle):
+    """fa_llm_generate_begin / _end (the host works while the chunk runs) give the tokens of fa_llm_generate, chunk
+    after chunk, and the other LLM calls refuse while a chunk is in flight."""
+    from fun_asr_gguf import _native
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(9)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (9, 14, 11)]
+    runs = []
+    for split in (False, True):
+        e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=128, max_seqs=4), max_batch=1, max_samples=16000)
+        try:
+            e.synthetic_weights(0)
+            for s in range(3):
+                e.llm_reset(s)
+            e.llm_prefill_batch([0, 1, 2], prompts, temperature=0.0)
+            if not split:
+                runs.append(e.llm_generate([0, 1, 2], 12))
+                runs.append(e.llm_generate([0, 2], 7))
+            else:
+                e.llm_generate_begin([0, 1, 2], 12)
+                with pytest.raises(RuntimeError):
+                    e.llm_prefill(3, prompts[0])
+                runs.append(e.llm_generate_end())
+                e.llm_generate_begin([0, 2], 7)
+                runs.append(e.llm_generate_end())
+                assert e.llm_n_past(0) == prompts[0].shape[0] + 19 and e.llm_n_past(1) == prompts[1].shape[0] + 12
+        finally:
+            e.close()
+    np.testing.assert_array_equal(runs[0], runs[2])
+    np.testing.assert_array_equal(runs[1], runs[3])
