@@ -101,17 +101,31 @@ __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __r
   const float* xr = x + (int64_t)row * ldx;
   float v[PER];
   float s = 0.f;
+  // D == 64 PER with 16-B aligned rows: each lane owns PER contiguous columns (PER / 4 float4 loads, not PER dwords)
+  const bool vec = PER % 4 == 0 && D == 64 * PER && (ldx & 3) == 0 && (ldy & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(w) |
+                     reinterpret_cast<uintptr_t>(bb)) & 15) == 0;
+  if (vec) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    int c = lane + i * 64;
-    v[i] = c < D ? xr[c] : 0.f;
-    s += v[i];
+    for (int i = 0; i < PER; i += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(xr + lane * PER + i);
+      v[i] = f.x; v[i + 1] = f.y; v[i + 2] = f.z; v[i + 3] = f.w;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s += v[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + i * 64;
+      v[i] = c < D ? xr[c] : 0.f;
+      s += v[i];
+    }
   }
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    int c = lane + i * 64;
+    int c = vec ? lane * PER + i : lane + i * 64;
     float dv = c < D ? v[i] - mean : 0.f;
     q += dv * dv;
   }
@@ -122,10 +136,22 @@ __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __r
     mk = t < lens[b] ? 1.0f : 0.0f;
   }
   float* yr = y + (int64_t)row * ldy;
+  if (vec) {
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    int c = lane + i * 64;
-    if (c < D) yr[c] = r16e((v[i] - mean) * rstd * w[c] + bb[c], r16) * mk;
+    for (int i = 0; i < PER; i += 4) {
+      const int c = lane * PER + i;
+      const float4 wv = *reinterpret_cast<const float4*>(w + c), bv = *reinterpret_cast<const float4*>(bb + c);
+      *reinterpret_cast<float4*>(yr + c) = make_float4(r16e((v[i] - mean) * rstd * wv.x + bv.x, r16) * mk,
+                                                       r16e((v[i + 1] - mean) * rstd * wv.y + bv.y, r16) * mk,
+                                                       r16e((v[i + 2] - mean) * rstd * wv.z + bv.z, r16) * mk,
+                                                       r16e((v[i + 3] - mean) * rstd * wv.w + bv.w, r16) * mk);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + i * 64;
+      if (c < D) yr[c] = r16e((v[i] - mean) * rstd * w[c] + bb[c], r16) * mk;
+    }
   }
 }
 
