@@ -100,6 +100,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int
 __device__ __forceinline__ f32x4_t ld_sc1_f4(__amdgpu_buffer_rsrc_t rs, int byte_off) {
   return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, CPOL_SC1));
 }
+__device__ __forceinline__ float ld_sc1_f1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, byte_off, 0, CPOL_SC1));
+}
 __device__ __forceinline__ void st_sc1_f4(f32x4_t v, __amdgpu_buffer_rsrc_t rs, int byte_off) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v_t, v), rs, byte_off, 0, CPOL_SC1);
 }

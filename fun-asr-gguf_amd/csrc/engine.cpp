@@ -151,7 +151,8 @@ struct Engine {
   std::vector<int> logits_row;  // per sequence: its row of `logits` in the most recent forward (-1: none)
   AttnWork attn_wk;
   FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
-  bool use_fused = true;   // FUNASR_FUSED_DECODE=0: the 5-launch layer at M = 1 too (A/B)
+  int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
+                           // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
   float* d_ssp = nullptr;  // batched decode: per-token sum-of-squares partials [max_seqs][32] of the residual stream
   AttnF32Work enc_attn_wk;
@@ -645,9 +646,9 @@ struct Engine {
     fdw.dpart = alloc<float>((size_t)FUSED_PARTS * E);
     fdw.act = alloc<float>(lc.n_ff);
     fdw.xmid = alloc<float>(E);
-    fdw.cnt = alloc<unsigned>((size_t)2 * FUSED_PARTS * CNT_LINE);
+    fdw.cnt = alloc<unsigned>((size_t)FUSED_CNT_LINES * CNT_LINE);
     fdw.err = alloc<int>(1);
-    FA_HIP(hipMemset(fdw.cnt, 0, (size_t)2 * FUSED_PARTS * CNT_LINE * sizeof(unsigned)));
+    FA_HIP(hipMemset(fdw.cnt, 0, (size_t)FUSED_CNT_LINES * CNT_LINE * sizeof(unsigned)));
     FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
     // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)
     gk_cnt_n = 1024;                             // tiles of a split-K launch
@@ -958,15 +959,24 @@ struct Engine {
       prof_sample = l == 0;
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
-      GemvArgs a{};
-      a.M = 1;
-      a.eps = lc.rms_eps;
-      a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
-      a.out = lqkv; a.ldo = QKV; a.ldx = E; a.norm_w = w.attn_norm;
-      if (l == 0) a.x = lx;
-      else { a.x = fdw.xmid; a.psum = fdw.dpart; a.xsum = lx; }
-      gemv(a, E, 0);
-      {
+      if (use_fused == 1) {
+        hipEvent_t ev;
+        prof_begin(3, &ev);
+        qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
+                         w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
+                         w.o.q, w.o.d, E, attn_wk, fdw, stream);
+        prof_end(3, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0, 0);
+      } else {
+        GemvArgs a{};
+        a.M = 1;
+        a.eps = lc.rms_eps;
+        a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
+        a.out = lqkv; a.ldo = QKV; a.ldx = E; a.norm_w = w.attn_norm;
+        if (l == 0) a.x = lx;
+        else { a.x = fdw.xmid; a.psum = fdw.dpart; a.xsum = lx; }
+        gemv(a, E, 0);
+      }
+      if (use_fused != 1) {
         hipEvent_t ev;
         prof_begin(3, &ev);
         attn_o_fused(lqkv, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
@@ -1119,7 +1129,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     }
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
-    if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
@@ -1353,12 +1363,13 @@ int fa_set_encoder_gemm(fa_engine* h, int32_t mode) {
 int fa_set_decode_fused(fa_engine* h, int32_t on) {
   FA_API_BEGIN
   Engine* e = h->e;
-  if (e->use_fused != (on != 0)) {
+  FA_REQUIRE(on >= 0 && on <= 2, "fa_set_decode_fused: 0 (5-launch), 1 (two-launch), 2 (three-launch)");
+  if (e->use_fused != on) {
     FA_HIP(hipStreamSynchronize(e->stream));
     for (auto& g : e->step_graphs) FA_HIP(hipGraphExecDestroy(g.second));
     e->step_graphs.clear();  // captured steps bake the layer structure in
   }
-  e->use_fused = on != 0;
+  e->use_fused = on;
   FA_API_END
 }
 

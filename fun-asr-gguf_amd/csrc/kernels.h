@@ -140,18 +140,27 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
 // projection, each with an in-launch group fan-in (see the kernels). FUSED_PARTS = partial vectors summed by the next
 // launch's prologue (8 kv heads for o, 8 groups of 384 act rows for down).
 constexpr int FUSED_PARTS = 8;
+constexpr int FUSED_CNT_LINES = 3 * FUSED_PARTS;
 struct FusedDecodeWork {
   float* opart = nullptr;   // [FUSED_PARTS][E]
   float* dpart = nullptr;   // [FUSED_PARTS][E]
   float* act = nullptr;     // [F] act hand-off
   float* xmid = nullptr;    // [E] residual stream after the attention block
-  unsigned* cnt = nullptr;  // [2 * FUSED_PARTS][CNT_LINE] ticket counters (zeroed once, never re-armed)
+  unsigned* cnt = nullptr;  // [FUSED_CNT_LINES][CNT_LINE] ticket counters (zeroed once, never re-armed): o fan-in,
+                            // down-group fan-in, q|k|v fan-in (two-launch layer), FUSED_PARTS lines each
   int* err = nullptr;       // set to 1 by a timed-out fan-in wait
 };
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
                   const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,
                   hipStream_t s);
+// Two-launch layer: the q|k|v GEMV (prologue x = x + sum psum, block (0, 0) stores it to xsum) in the attention
+// launch (k_attn_o<true>); psum = nullptr for layer 0.
+void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const float* norm_w, const int8_t* wqkv_q,
+                      const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
+                      const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
+                      int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
+                      const FusedDecodeWork& fw, hipStream_t s);
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s);

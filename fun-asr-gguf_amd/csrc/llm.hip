@@ -2607,17 +2607,67 @@ struct AttnOArgs {
   unsigned* cnt;       // [KV][CNT_LINE]
   float* partials;     // [KV][ASPLIT][APART]
   int* err;
+  // QKV (two-launch layer): the q|k|v GEMV of the layer runs in the same launch (k_attn_o<true>)
+  const float* x;      // residual row (layer 0: the embedded row; else x_mid of the previous layer)
+  const float* psum;   // previous layer's down partials [FUSED_PARTS][E], or nullptr (layer 0)
+  float* xsum;         // block (0, 0) stores x + sum psum here (the residual stream) when psum
+  const float* norm_w; // attn_norm
+  const int8_t* wqkv_q;  // q|k|v [(H + 2 KV) D][E], engine layout
+  const __half* wqkv_d;
+  unsigned* cnt_qkv;   // [KV][CNT_LINE]
 };
 
+constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
+
+// QKV = true: the two-launch batch-1 layer. The 16 split blocks of kv head g first compute the 512 q|k|v rows that
+// head's attention reads (q heads GQ g .. GQ g + 1, k head g, v head g), FQ_ROWS each, with the prologue and the
+// arithmetic of k_gemv_q8<1, 1, true, 0, PS> (x = x_mid + sum dpart, rmsnorm + q8_0 in LDS, exact block dots, the
+// same wave_sum per row: bit-identical q|k|v values), publish them with sc1 stores and pass a 16-block fan-in;
+// then the attention + o slice of k_attn_o<false>, with the q|k|v inputs read back with sc1 loads. This replaces
+// a kernel boundary (A -> B) by a group-local fan-in whose producers are its consumers.
+template <bool QKV>
 __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   constexpr int D = 128, FS = ASPLIT;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int g = blockIdx.x, sp = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // q|k|v row inputs do not depend on the position: issued before the tok_pos / tok_seq read (one round trip less
-  // on the critical path than loading them after it)
   AttnQIn qpre;
-  {
+  // ---- QKV: activation loads, then this wave's 8 q|k|v weight rows (one 1-KB row per load instruction)
+  constexpr int QR = FQ_ROWS / AWV;  // rows per wave
+  float xv[4], pv[FUSED_PARTS][4], xw[4];
+  int4 wq[QKV ? QR : 1];
+  float dq[QKV ? QR : 1];
+  int qrow0 = 0;  // global q|k|v row of this block's first row
+  if constexpr (QKV) {
+    const float4 x4 = *reinterpret_cast<const float4*>(a.x + threadIdx.x * 4);
+    xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
+    if (a.psum) {  // kernel-uniform
+#pragma unroll
+      for (int p = 0; p < FUSED_PARTS; ++p) {
+        const float4 f = *reinterpret_cast<const float4*>(a.psum + p * 1024 + threadIdx.x * 4);
+        pv[p][0] = f.x; pv[p][1] = f.y; pv[p][2] = f.z; pv[p][3] = f.w;
+      }
+    }
+    const float4 w4 = *reinterpret_cast<const float4*>(a.norm_w + threadIdx.x * 4);
+    xw[0] = w4.x; xw[1] = w4.y; xw[2] = w4.z; xw[3] = w4.w;
+    __builtin_amdgcn_sched_barrier(0);
+    // local rows [FQ_ROWS sp, +FQ_ROWS) of head g's list (q head GQ g, q head GQ g + 1, k head g, v head g)
+    const int lr0 = FQ_ROWS * sp, seg = lr0 / D, off = lr0 % D;
+    qrow0 = (seg < GQ ? (g * GQ + seg) * D : seg == GQ ? (a.H + g) * D : (a.H + a.KV + g) * D) + off;
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+      const int row = qrow0 + QR * wave + r;
+      wq[r] = ld_nt16(a.wqkv_q + (int64_t)row * 1024 + lane * 16);
+      dq[r] = __half2float(a.wqkv_d[(int64_t)row * 32 + (lane >> 1)]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    qpre.w0 = a.qn[lane];
+    qpre.w1 = a.qn[lane + 64];
+    qpre.kw0 = a.kn[lane];
+    qpre.kw1 = a.kn[lane + 64];
+  } else {
+    // q|k|v row inputs do not depend on the position: issued before the tok_pos / tok_seq read (one round trip less
+    // on the critical path than loading them after it)
     const float* row = a.qkv;  // token 0
 #pragma unroll
     for (int jh = 0; jh < GQ; ++jh) {
@@ -2632,8 +2682,8 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     qpre.kw1 = a.kn[lane + 64];
     qpre.v0 = row[(a.H + a.KV + g) * D + lane];
     qpre.v1 = row[(a.H + a.KV + g) * D + lane + 64];
-    qpre.c = qpre.sn = 0.f;
   }
+  qpre.c = qpre.sn = 0.f;
   int pos = a.tok_pos[0];
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
@@ -2652,6 +2702,54 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
   }
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (QKV) {
+    // ---- prologue (k_gemv_q8 PS): x = x_mid + sum dpart; block (0, 0) stores it; rmsnorm + q8_0 into LDS
+    __shared__ __attribute__((aligned(16))) int8_t s_xq[1024];
+    __shared__ float s_xd[32];
+    __shared__ float s_red[4];
+    if (a.psum) {
+#pragma unroll
+      for (int jv = 0; jv < 4; ++jv) {
+        float v = xv[jv];
+#pragma unroll
+        for (int p = 0; p < FUSED_PARTS; ++p) v = v + pv[p][jv];
+        xv[jv] = v;
+      }
+      if (a.xsum && g == 0 && sp == 0)
+        *reinterpret_cast<float4*>(a.xsum + threadIdx.x * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+    }
+    norm_quant_block_regs<4>(xv, xw, true, a.eps, 1024, s_xq, s_xd, s_red);
+    __syncthreads();
+    // ---- the wave's QR rows (compute_group<1, 1, 0>'s arithmetic), published as two 16-B sc1 stores
+    const int4 xq = *reinterpret_cast<const int4*>(s_xq + lane * 16);
+    const float xdv = s_xd[lane >> 1];
+    float y[QR];
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+      int si = dot16(wq[r], xq, 0);
+      si += dpp_i<DPP_XOR1>(si);
+      float acc = 0.f;
+      if (!(lane & 1)) acc += (float)si * (dq[r] * xdv);
+      y[r] = wave_sum(acc);
+    }
+    static_assert(QR == 8, "two 16-B stores per wave");
+    const __amdgpu_buffer_rsrc_t rq = buf_rsrc(a.qkv, (a.H + 2 * a.KV) * D * 4);
+    if (lane < 2) {
+      const f4v v = lane == 0 ? f4v{y[0], y[1], y[2], y[3]} : f4v{y[4], y[5], y[6], y[7]};
+      st_sc1_f4(v, rq, (qrow0 + QR * wave + 4 * lane) * 4);
+    }
+    fanin_wait(a.cnt_qkv + g * CNT_LINE, FS, a.err);
+    // ---- head g's q|k|v inputs, written by the group's blocks (sc1: from L2, never a stale L1 line)
+#pragma unroll
+    for (int jh = 0; jh < GQ; ++jh) {
+      qpre.x0[jh] = ld_sc1_f1(rq, ((g * GQ + jh) * D + lane) * 4);
+      qpre.x1[jh] = ld_sc1_f1(rq, ((g * GQ + jh) * D + lane + 64) * 4);
+    }
+    qpre.kx0 = ld_sc1_f1(rq, ((a.H + g) * D + lane) * 4);
+    qpre.kx1 = ld_sc1_f1(rq, ((a.H + g) * D + lane + 64) * 4);
+    qpre.v0 = ld_sc1_f1(rq, ((a.H + a.KV + g) * D + lane) * 4);
+    qpre.v1 = ld_sc1_f1(rq, ((a.H + a.KV + g) * D + lane + 64) * 4);
+  }
   int n_active = 0, j = 0, d0 = 0;
   float M = -INFINITY, L = 0.f;
   float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2711,7 +2809,22 @@ void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps,
   FA_REQUIRE(wk.partials && fw.opart && fw.cnt && fw.err, "attn_o_fused: workspace");
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err};
-  hipLaunchKernelGGL(k_attn_o, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
+  hipLaunchKernelGGL(k_attn_o<false>, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
+}
+
+void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const float* norm_w, const int8_t* wqkv_q,
+                      const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
+                      const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
+                      int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
+                      const FusedDecodeWork& fw, hipStream_t s) {
+  FA_REQUIRE(H == KV * GQ && KV == FUSED_PARTS && E == FO_ROWS * ASPLIT && E == 1024 &&
+                 (GQ + 2) * 128 == FQ_ROWS * ASPLIT,
+             "qkv_attn_o_fused: Qwen3-0.6B head layout");
+  FA_REQUIRE(wk.partials && fw.opart && fw.cnt && fw.err && x && norm_w, "qkv_attn_o_fused: workspace");
+  AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
+              1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err,
+              x, psum, xsum, norm_w, wqkv_q, wqkv_d, fw.cnt + 2 * FUSED_PARTS * CNT_LINE};
+  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
 }
 
 struct FfnArgs {

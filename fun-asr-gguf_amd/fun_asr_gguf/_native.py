@@ -155,8 +155,10 @@ class Engine:
         _check(self.lib.fa_set_encoder_gemm(self.h, {"f32": 0, "bf16x3": 1}[mode]), "fa_set_encoder_gemm")
 
     def set_decode_fused(self, on=True):
-        """Batch-1 decode layer: fused 3-launch structure (default) or the 5-launch layer."""
-        _check(self.lib.fa_set_decode_fused(self.h, 1 if on else 0), "fa_set_decode_fused")
+        """Batch-1 decode layer: True / 1 the two-launch fused layer (default), 2 the three-launch fused layer,
+        False / 0 the 5-launch layer."""
+        mode = int(on) if not isinstance(on, bool) else (1 if on else 0)
+        _check(self.lib.fa_set_decode_fused(self.h, mode), "fa_set_decode_fused")
 
     def synthetic_weights(self, seed=0):
         _check(self.lib.fa_weights_synthetic(self.h, seed), "fa_weights_synthetic")

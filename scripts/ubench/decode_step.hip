@@ -66,17 +66,26 @@ int main(int argc, char** argv) {
   int mask = 63;  // 1 qkv, 2 attn, 4 o, 8 gate/up, 16 down, 32 lm_head (ablation: time a subset of the chain)
   // "fused": the 3-launch batch-1 layer (A = qkv with the partial-sum prologue, B = attention + o slice, C = gate|up +
   // down slice); masks: 1 A, 2 B, 8 C, 32 lm_head
-  const bool fused = argc > 1 && !strcmp(argv[1], "fused");
+  // "fused2": the two-launch layer (AB = q|k|v GEMV + attention + o slice in one launch, C); mask 2 times AB
+  const bool two = argc > 1 && !strcmp(argv[1], "fused2");
+  const bool fused = two || (argc > 1 && !strcmp(argv[1], "fused"));
   FusedDecodeWork fw;
   fw.opart = dalloc<float>(8 * E); fw.dpart = dalloc<float>(8 * E); fw.act = dalloc<float>(F); fw.xmid = dalloc<float>(E);
-  fw.cnt = dalloc<unsigned>(16 * CNT_LINE); fw.err = dalloc<int>(1);
-  CK(hipMemset(fw.cnt, 0, 16 * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
+  fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
+  CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   CK(hipMemset(fw.opart, 0, 8 * E * 4)); CK(hipMemset(fw.dpart, 0, 8 * E * 4)); CK(hipMemset(fw.xmid, 0, E * 4));
   wk.max_tokens = 1;
   auto step_fused = [&]() {
     for (int l = 0; l < L; ++l) {
       auto& w = lw[l % n_distinct];
       auto a = G(w.qkv, w.dqkv, QKV, fw.xmid, E, nw, qkv, nullptr); a.psum = fw.dpart; a.xsum = x;
+      if (two) {
+        if (mask & 2) qkv_attn_o_fused(fw.xmid, fw.dpart, x, nw, w.qkv, w.dqkv, qkv, qn, qn, 1e-6f, rc, rs,
+                                       kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D, H, KV, seq, pos,
+                                       (int64_t)NCTX * KV * D, w.o, w.dO, E, wk, fw, s);
+        if (mask & 8) ffn_fused(x, nw, 1e-6f, w.g, w.dg, w.u, w.du, w.d, w.dd, E, F, fw, s);
+        continue;
+      }
       if (mask & 1) gemv_q8(a, E, 0, s);
       if (mask & 2) attn_o_fused(qkv, qn, qn, 1e-6f, rc, rs, kc + (size_t)l * NCTX * KV * D, vc + (size_t)l * NCTX * KV * D,
                                  H, KV, seq, pos, (int64_t)NCTX * KV * D, w.o, w.dO, E, wk, fw, s);

@@ -334,13 +334,15 @@ def test_encoder_full_10s_vs_reference_golden():
 def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
     """The fused batch-1 layer (attention + split o projection, gate|up + split down projection, in-launch fan-ins)
     against the 5-launch layer on the same steps: logits equal up to f32 summation order, same greedy token where the
-    margin is not a tie; teacher-forced against the oracle too; over a long context (12 active key splits)."""
+    margin is not a tie; teacher-forced against the oracle too; over a long context (12 active key splits). The
+    two-launch fused layer (q|k|v GEMV inside the attention launch, default) and the three-launch one (the q|k|v GEMV
+    as its own launch) compute the same arithmetic: bit-identical logits and tokens."""
     m = llm_tiny_oracle
     rng = np.random.default_rng(12)
     prompt = np.concatenate([m.embed_prompt(rng.integers(0, 4096, 40)),
                              (rng.standard_normal((330, 1024)) * 0.5).astype(np.float32)], 0)
     runs = []
-    for fused in (True, False):
+    for fused in (1, 0, 2):
         tiny_engine.set_decode_fused(fused)
         tiny_engine.llm_reset(0)
         tok = tiny_engine.llm_prefill(0, prompt)
@@ -350,7 +352,10 @@ def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
             lgs.append(tiny_engine.llm_logits(0))
         runs.append((toks, lgs))
     tiny_engine.set_decode_fused(True)
-    (tf, lf), (tu, lu) = runs
+    (tf, lf), (tu, lu), (t3, l3) = runs
+    assert t3 == tf
+    for k in range(8):
+        assert np.array_equal(l3[k], lf[k])
     m.reset()
     m.forward(prompt, 0)
     for k in range(8):
