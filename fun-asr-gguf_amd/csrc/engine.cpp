@@ -960,12 +960,13 @@ struct Engine {
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       if (use_fused == 1) {
+        // a q8_0 weight-streaming layer launch (class 0, like C): q|k|v + Wo weight bytes (its K/V reads are not counted)
         hipEvent_t ev;
-        prof_begin(3, &ev);
+        prof_begin(0, &ev);
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
                          w.o.q, w.o.d, E, attn_wk, fdw, stream);
-        prof_end(3, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0, 0);
+        prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0, 2.0 * (E * H * D + (double)QKV * E));
       } else {
         GemvArgs a{};
         a.M = 1;

@@ -1431,13 +1431,13 @@ void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const floa
 // qk_rope_store and the cache is complete.
 #ifdef FA_ATTN_STAMPS
 // per-block s_memrealtime (100 MHz, chip-wide) stamps of wave 0, lane 0: [i] at the STAMP(i) points
-__device__ unsigned long long g_attn_stamps[4096][12];
+__device__ unsigned long long g_attn_stamps[4096][16];
 #define STAMP(i) do { if (threadIdx.x == 0) g_attn_stamps[(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 void attn_stamps_read(unsigned long long* host, int n_blocks) {
-  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)n_blocks * 96, 0, hipMemcpyDeviceToHost);
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_stamps), (size_t)n_blocks * 128, 0, hipMemcpyDeviceToHost);
 }
 void attn_stamps_clear() {
-  static unsigned long long z[4096][12];
+  static unsigned long long z[4096][16];
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 #else
@@ -2720,6 +2720,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     }
     norm_quant_block_regs<4>(xv, xw, true, a.eps, 1024, s_xq, s_xd, s_red);
     __syncthreads();
+    STAMP(12);
     // ---- the wave's QR rows (compute_group<1, 1, 0>'s arithmetic), published as two 16-B sc1 stores
     const int4 xq = *reinterpret_cast<const int4*>(s_xq + lane * 16);
     const float xdv = s_xd[lane >> 1];
@@ -2738,7 +2739,9 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
       const f4v v = lane == 0 ? f4v{y[0], y[1], y[2], y[3]} : f4v{y[4], y[5], y[6], y[7]};
       st_sc1_f4(v, rq, (qrow0 + QR * wave + 4 * lane) * 4);
     }
+    STAMP(13);
     fanin_wait(a.cnt_qkv + g * CNT_LINE, FS, a.err);
+    STAMP(14);
     // ---- head g's q|k|v inputs, written by the group's blocks (sc1: from L2, never a stale L1 line)
 #pragma unroll
     for (int jh = 0; jh < GQ; ++jh) {

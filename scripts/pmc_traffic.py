@@ -11,14 +11,17 @@ import sys
 from collections import defaultdict
 
 # algorithmic q8_0 weight bytes per launch for the Qwen3-0.6B decode launches (34 B per 32 weights). The batch-1
-# step runs the fused 3-launch layer: A = q|k|v GEMV with the partial-sum prologue, B = attention + o slice
-# (k_attn_o: Wo only here, its K/V bytes are not weights), C = gate|up + SwiGLU + down slice (k_ffn_fused); the
-# 5-launch layer's GEMVs (fa_set_decode_fused(0)) are listed too. Names as rocprofv3 prints them.
+# step runs the fused two-launch layer: AB = q|k|v GEMV + attention + o slice (k_attn_o<true>: its K/V bytes are not
+# weights, so its traffic exceeds the weight bytes by the K/V stream), C = gate|up + SwiGLU + down slice
+# (k_ffn_fused); the three-launch layer (fa_set_decode_fused(2): A = q|k|v GEMV with the partial-sum prologue,
+# B = k_attn_o<false>) and the 5-launch layer's GEMVs (fa_set_decode_fused(0)) are listed too. Names as rocprofv3
+# prints them.
 QKV, O, GU, DOWN = 4096 * 1024 * 34 / 32, 1024 * 2048 * 34 / 32, 2 * 3072 * 1024 * 34 / 32, 1024 * 3072 * 34 / 32
 ALGO = {
     "k_gemv_q8<1, 1, true, 0, true>": QKV,      # A: q|k|v (fused layer)
     "k_ffn_fused(": GU + DOWN,                 # C: gate|up + down (fused layer)
-    "k_attn_o(": O,                            # B: o projection slice weights
+    "k_attn_o<true>": QKV + O,                 # AB: q|k|v rows + o projection slice weights (two-launch layer)
+    "k_attn_o<false>": O,                      # B: o projection slice weights (three-launch layer)
     "k_gemv_q8<1, 1, true, 0, false>": QKV,     # 5-launch layer
     "k_gemv_q8<2, 1, true, 1, false>": O,
     "k_gemv_q8<1, 1, true, 2, false>": GU,
@@ -26,9 +29,9 @@ ALGO = {
     "k_gemv_q8<1, 1, true, 3, true>": 151936 * 1024 * 34 / 32,   # lm_head (fused layer's partial-sum prologue)
     "k_gemv_q8<1, 1, true, 3, false>": 151936 * 1024 * 34 / 32,  # lm_head
 }
-# the bench's dominant class "q8_0 GEMV/GEMM (decoder layers)" = the weight-streaming layer launches A and C
-# (B is the "decode attention" class): their mean is what roofline.traffic reports
-LAYER_CLASS = ("k_gemv_q8<1, 1, true, 0, true>", "k_ffn_fused(", "k_gemv_q8<1, 1, true, 0, false>",
+# the bench's dominant class "q8_0 GEMV/GEMM (decoder layers)" = the weight-streaming layer launches AB and C (or A
+# and C; B is the "decode attention" class): their mean is what roofline.traffic reports
+LAYER_CLASS = ("k_attn_o<true>", "k_gemv_q8<1, 1, true, 0, true>", "k_ffn_fused(", "k_gemv_q8<1, 1, true, 0, false>",
                "k_gemv_q8<1, 1, true, 2, false>", "k_gemv_q8<2, 1, true, 1, false>", "k_gemv_q8<3, 1, true, 1, false>")
 
 

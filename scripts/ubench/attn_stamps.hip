@@ -31,6 +31,8 @@ int main(int argc, char** argv) {
   const bool fused_o = argc > 2 && argv[2][0] == 'o';
   // argv[2] == "c": the fused layer's C launch (k_ffn_fused: x_mid + norm + gate|up + group fan-in + down slice)
   const bool fused_c = argc > 2 && argv[2][0] == 'c';
+  // argv[2] == "a": the two-launch layer's AB launch (k_attn_o<true>: q|k|v GEMV + fan-in, then as "o"), M = 1
+  const bool fused_a = argc > 2 && argv[2][0] == 'a';
   if (const char* e = getenv("FUNASR_ATTN_LEAN")) g_attn_lean = atoi(e);
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int H = 16, KV = 8, D = 128, NCTX = 1024, QKV = 4096;
@@ -54,15 +56,18 @@ int main(int argc, char** argv) {
   int8_t* wd_q = dalloc<int8_t>((size_t)1024 * 3072);
   CK(hipMemset(wg_q, 1, (size_t)3072 * 1024)); CK(hipMemset(wd_q, 1, (size_t)1024 * 3072));
   int8_t* wo_q = dalloc<int8_t>((size_t)1024 * 2048);
+  int8_t* wqkv_q = dalloc<int8_t>((size_t)4096 * 1024);  // q|k|v stand-in (scales: wo_d, 3072 x 96 >= 4096 x 32)
+  CK(hipMemset(wqkv_q, 1, (size_t)4096 * 1024));
   __half* wo_d = dalloc<__half>((size_t)3072 * 96);  // scales for every stand-in matrix (zeros)
   CK(hipMemset(wo_q, 1, (size_t)1024 * 2048)); CK(hipMemset(wo_d, 0, (size_t)3072 * 96 * 2));
   FusedDecodeWork fw;
   fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(3072);
-  fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(16 * CNT_LINE); fw.err = dalloc<int>(1);
-  CK(hipMemset(fw.cnt, 0, 16 * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
+  fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
+  CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
+  CK(hipMemset(fw.xmid, 0, 1024 * 4)); CK(hipMemset(fw.dpart, 0, 8 * 1024 * 4));
   const int nblk = fused_c ? 256 : M * KV * ATTN_SPLITS;
   if (nblk > 4096) { printf("M too large for the stamp buffer\n"); return 1; }
-  std::vector<unsigned long long> st((size_t)nblk * 12);
+  std::vector<unsigned long long> st((size_t)nblk * 16);
   std::vector<int> cases = M == 1 ? std::vector<int>{40, 330, 700} : std::vector<int>{-1};
   for (int p0 : cases) {
     std::vector<int> hpos(M);
@@ -74,6 +79,9 @@ int main(int argc, char** argv) {
       const int l = rep % 28;  // rotate layers: cold K/V like in the engine
       if (fused_c)
         ffn_fused(qkv, qkv + 1024, 1e-6f, wg_q, wo_d, wg_q, wo_d, wd_q, wo_d, 1024, 3072, fw, s);
+      else if (fused_a)
+        qkv_attn_o_fused(fw.xmid, fw.dpart, att, qkv, wqkv_q, wo_d, qkv, qn, qn, 1e-6f, rc, rs, kc + l * layer,
+                         vc + l * layer, H, KV, seq, pos, seq_stride, wo_q, wo_d, 1024, wk, fw, s);
       else if (fused_o)
         attn_o_fused(qkv, qn, qn, 1e-6f, rc, rs, kc + l * layer, vc + l * layer, H, KV, seq, pos, seq_stride, wo_q, wo_d,
                      1024, wk, fw, s);
@@ -83,7 +91,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     attn_stamps_read(st.data(), nblk);
     unsigned long long t0 = ~0ull;
-    for (int b = 0; b < nblk; ++b) if (st[b * 12]) t0 = std::min(t0, st[b * 12]);
+    for (int b = 0; b < nblk; ++b) if (st[b * 16]) t0 = std::min(t0, st[b * 16]);
     if (p0 >= 0) printf("decode attention, n_past %d:\n", p0);
     else printf("decode attention, batch %d, n_past 200-460:\n", M);
     const int slot_b[] = {0, 1, 3, 7, 11, 9, 10};
@@ -92,16 +100,19 @@ int main(int argc, char** argv) {
     const int slot_o[] = {1, 3, 7, 9, 10, 11, -1};
     const char* nm_o[] = {"splits known", "q normed/roped", "split merged", "partial published", "fan-in passed",
                           "combined + quantised", ""};
+    const int slot_a[] = {0, 12, 13, 14, 3, 7, 9, 10, 11};
+    const char* nm_a[] = {"loads issued", "x normed + q8", "q|k|v rows stored", "q|k|v fan-in passed", "q normed/roped",
+                          "split merged", "partial published", "fan-in passed", "combined + quantised"};
     const int slot_c[] = {0, 1, 2, 3, 4, 5, -1};
     const char* nm_c[] = {"block start", "x normed + q8", "act published", "group fan-in passed", "act quantised",
                           "down slice stored", ""};
-    const int* slot = fused_c ? slot_c : fused_o ? slot_o : slot_b;
-    const char* const* nm = fused_c ? nm_c : fused_o ? nm_o : nm_b;
-    for (int k = 0; k < (fused_c || fused_o ? 6 : 7); ++k) {
+    const int* slot = fused_a ? slot_a : fused_c ? slot_c : fused_o ? slot_o : slot_b;
+    const char* const* nm = fused_a ? nm_a : fused_c ? nm_c : fused_o ? nm_o : nm_b;
+    for (int k = 0; k < (fused_a ? 9 : fused_c || fused_o ? 6 : 7); ++k) {
       std::vector<double> v;
       for (int b = 0; b < nblk; ++b) {  // stamps left by an earlier launch (before t0) are not this launch's
-        const long long d = (long long)(st[b * 12 + slot[k]] - t0);
-        v.push_back(st[b * 12 + slot[k]] && d >= 0 ? d * 0.01 : -1.0);
+        const long long d = (long long)(st[b * 16 + slot[k]] - t0);
+        v.push_back(st[b * 16 + slot[k]] && d >= 0 ? d * 0.01 : -1.0);
       }
       stats(nm[k], v);
     }
