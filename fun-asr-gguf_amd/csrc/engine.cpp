@@ -644,10 +644,18 @@ struct Engine {
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
     fdw.opart = alloc<float>((size_t)FUSED_PARTS * E);
     fdw.dpart = alloc<float>((size_t)FUSED_PARTS * E);
-    fdw.act = alloc<float>(lc.n_ff);
+    fdw.act = alloc<float>(2 * (size_t)lc.n_ff);
+    FA_HIP(hipMemset(fdw.act, 0, 2 * (size_t)lc.n_ff * sizeof(float)));
     fdw.xmid = alloc<float>(E);
     fdw.cnt = alloc<unsigned>((size_t)FUSED_CNT_LINES * CNT_LINE);
     fdw.err = alloc<int>(1);
+    {
+      const size_t nq = (size_t)(lc.n_head + 2 * lc.n_head_kv) * lc.head_dim;
+      fdw.gqkv = reinterpret_cast<unsigned long long*>(alloc<float>(2 * nq));
+      FA_HIP(hipMemset(fdw.gqkv, 0, nq * 8));
+      fdw.pzero = alloc<float>((size_t)FUSED_PARTS * E);
+      FA_HIP(hipMemset(fdw.pzero, 0, (size_t)FUSED_PARTS * E * sizeof(float)));
+    }
     FA_HIP(hipMemset(fdw.cnt, 0, (size_t)FUSED_CNT_LINES * CNT_LINE * sizeof(unsigned)));
     FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
     // split-K GEMM workspace: splits are only used below 256 tiles (x <= 8 splits, x2 for gate|up)

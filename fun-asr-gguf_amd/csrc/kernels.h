@@ -144,11 +144,13 @@ constexpr int FUSED_CNT_LINES = 3 * FUSED_PARTS;
 struct FusedDecodeWork {
   float* opart = nullptr;   // [FUSED_PARTS][E]
   float* dpart = nullptr;   // [FUSED_PARTS][E]
-  float* act = nullptr;     // [F] act hand-off
+  float* act = nullptr;     // [2 F] act hand-off (F 8-byte granules; zeroed once)
   float* xmid = nullptr;    // [E] residual stream after the attention block
   unsigned* cnt = nullptr;  // [FUSED_CNT_LINES][CNT_LINE] ticket counters (zeroed once, never re-armed): o fan-in,
                             // down-group fan-in, q|k|v fan-in (two-launch layer), FUSED_PARTS lines each
   int* err = nullptr;       // set to 1 by a timed-out fan-in wait
+  float* pzero = nullptr;   // [FUSED_PARTS][E] zeros: layer 0's partials in the two-launch layer
+  unsigned long long* gqkv = nullptr;  // [(H + 2 KV) D] q|k|v granules of the two-launch layer (zeroed once)
 };
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,

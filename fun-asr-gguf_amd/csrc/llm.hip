@@ -1498,15 +1498,36 @@ struct AttnQIn {
 // it is in flight.
 // PIPE: the next pass's K/V loads are issued before this pass's math (2x the K/V registers: non-lean blocks only;
 // batch-1 B of the fused layer 7.44 -> 7.32 us, scripts/ubench/decode_step)
+// pre (NI <= KV_PRE, use_pre): the first pass's K/V, loaded by the caller (load_kv_groups<KV_PRE, AW> at the same g0);
+// carried as named values (an array here was demoted to scratch)
+constexpr int KV_PRE = 2;
+struct KvPre {
+  int4 k0, k1, v0, v1;
+};
 template <int NI, int AW, bool PIPE>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
-                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8]) {
+                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
+                                          KvPre pre_kv, bool use_pre) {
   int4 kt[NI], vt[NI];
-  load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-  load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+  if constexpr (NI <= KV_PRE) {
+    if (use_pre) {
+      kt[0] = pre_kv.k0;
+      vt[0] = pre_kv.v0;
+      if constexpr (NI > 1) {
+        kt[NI - 1] = pre_kv.k1;
+        vt[NI - 1] = pre_kv.v1;
+      }
+    } else {
+      load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+      load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+    }
+  } else {
+    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+  }
   __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
   if (decode) {
@@ -1671,7 +1692,8 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
                                                  const float* __restrict__ qn, const float* __restrict__ kn,
                                                  const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
                                                  float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
-                                                 float4& o, const AttnQIn* pre = nullptr) {
+                                                 float4& o, const AttnQIn* pre, bool pre_cs,
+                                                 KvPre pre_kv, bool use_pre) {
   constexpr int D = 128;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_keys = pos + 1;
@@ -1704,10 +1726,12 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   const int g0 = gb + wave;
   if (g0 < ge) {
     AttnQIn qi;
-    if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read
+    if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read (pre_cs: the rope too)
       qi = *pre;
-      qi.c = rcos[(int64_t)pos * 64 + lane];
-      qi.sn = rsin[(int64_t)pos * 64 + lane];
+      if (!pre_cs) {
+        qi.c = rcos[(int64_t)pos * 64 + lane];
+        qi.sn = rsin[(int64_t)pos * 64 + lane];
+      }
     } else if (DM) {
       const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
@@ -1739,16 +1763,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
       attn_wave<1, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, use_pre);
     else if (ni <= 2)
       attn_wave<2, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, use_pre);
     else if (ni <= 4 || LEAN)
       attn_wave<4, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, false);
     else
       attn_wave<8, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, false);
   }
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
   // unscaled): permlane32_swap pairs fold rows {r, r^2}, permlane16_swap pairs fold {r, r^1}; afterwards
@@ -1886,8 +1910,9 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   int n_active, j, d0;
   float M, L;
   float4 o;
+  const KvPre nokv{};
   if (!attn_split_merge<DM, LEAN>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc, qn, kn, rcos,
-                                  rsin, eps, scale, n_active, j, d0, M, L, o))
+                                  rsin, eps, scale, n_active, j, d0, M, L, o, nullptr, false, nokv, false))
     return;
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;  // j, d0: wave 0's lane map
   if (n_active == 1) {
@@ -2609,13 +2634,24 @@ struct AttnOArgs {
   int* err;
   // QKV (two-launch layer): the q|k|v GEMV of the layer runs in the same launch (k_attn_o<true>)
   const float* x;      // residual row (layer 0: the embedded row; else x_mid of the previous layer)
-  const float* psum;   // previous layer's down partials [FUSED_PARTS][E], or nullptr (layer 0)
-  float* xsum;         // block (0, 0) stores x + sum psum here (the residual stream) when psum
+  const float* psum;   // previous layer's down partials [FUSED_PARTS][E] (layer 0: FusedDecodeWork::pzero)
+  float* xsum;         // block (0, 0) stores x + sum psum here (the residual stream); nullptr for layer 0
   const float* norm_w; // attn_norm
   const int8_t* wqkv_q;  // q|k|v [(H + 2 KV) D][E], engine layout
   const __half* wqkv_d;
   unsigned* cnt_qkv;   // [KV][CNT_LINE]
+  unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
 };
+// FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
+// data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
+// no drain, no ticket, no read-back (FA_FFN_GRANULE's hand-off). 0: sc1 rows + ticket fan-in + sc1 read-back.
+#ifndef FA_QKV_GRANULE
+#define FA_QKV_GRANULE 1
+#endif
+// FA_KV_PRE = 1 (with FA_QKV_GRANULE): the rope row and each wave's first-pass K/V are loaded at kernel start
+#ifndef FA_KV_PRE
+#define FA_KV_PRE 1
+#endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
 
@@ -2632,21 +2668,21 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   const int g = blockIdx.x, sp = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   AttnQIn qpre;
+  qpre.c = qpre.sn = 0.f;
   // ---- QKV: activation loads, then this wave's 8 q|k|v weight rows (one 1-KB row per load instruction)
   constexpr int QR = FQ_ROWS / AWV;  // rows per wave
   float xv[4], pv[FUSED_PARTS][4], xw[4];
   int4 wq[QKV ? QR : 1];
   float dq[QKV ? QR : 1];
   int qrow0 = 0;  // global q|k|v row of this block's first row
+  unsigned ep_qkv = 0;
   if constexpr (QKV) {
     const float4 x4 = *reinterpret_cast<const float4*>(a.x + threadIdx.x * 4);
     xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
-    if (a.psum) {  // kernel-uniform
 #pragma unroll
-      for (int p = 0; p < FUSED_PARTS; ++p) {
-        const float4 f = *reinterpret_cast<const float4*>(a.psum + p * 1024 + threadIdx.x * 4);
-        pv[p][0] = f.x; pv[p][1] = f.y; pv[p][2] = f.z; pv[p][3] = f.w;
-      }
+    for (int p = 0; p < FUSED_PARTS; ++p) {  // layer 0: a zero block (no branch around the loads)
+      const float4 f = *reinterpret_cast<const float4*>(a.psum + p * 1024 + threadIdx.x * 4);
+      pv[p][0] = f.x; pv[p][1] = f.y; pv[p][2] = f.z; pv[p][3] = f.w;
     }
     const float4 w4 = *reinterpret_cast<const float4*>(a.norm_w + threadIdx.x * 4);
     xw[0] = w4.x; xw[1] = w4.y; xw[2] = w4.z; xw[3] = w4.w;
@@ -2665,6 +2701,10 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     qpre.w1 = a.qn[lane + 64];
     qpre.kw0 = a.kn[lane];
     qpre.kw1 = a.kn[lane + 64];
+    // this launch's epoch: head g's attention fan-in counter (+FS per launch) read before any block of head g can add
+    // to it in this launch (an add needs every block's q|k|v granules, each stored after its block read the counter)
+    if (FA_QKV_GRANULE)
+      ep_qkv = __hip_atomic_load(a.cnt + g * CNT_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / FS + 1;
   } else {
     // q|k|v row inputs do not depend on the position: issued before the tok_pos / tok_seq read (one round trip less
     // on the critical path than loading them after it)
@@ -2683,7 +2723,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     qpre.v0 = row[(a.H + a.KV + g) * D + lane];
     qpre.v1 = row[(a.H + a.KV + g) * D + lane + 64];
   }
-  qpre.c = qpre.sn = 0.f;
   int pos = a.tok_pos[0];
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
@@ -2702,22 +2741,43 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
   }
   __builtin_amdgcn_sched_barrier(0);
+  // QKV: the rope at pos and this wave's first-pass K/V (cached positions: independent of this step) are loaded now,
+  // in flight under the GEMV and the q|k|v hand-off (attn_split_merge's split of [0, pos], its first KV_PRE groups)
+  KvPre pkv{};
+  bool kv_pre = false;
+  if constexpr (QKV && FA_QKV_GRANULE && FA_KV_PRE) {
+    qpre.c = a.rcos[(int64_t)pos * 64 + lane];
+    qpre.sn = a.rsin[(int64_t)pos * 64 + lane];
+    const int n_keys = pos + 1, n_groups = (n_keys + 3) >> 2;
+    const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)FS));
+    const int gb = sp * gps, ge = min(n_groups, gb + gps), g0 = gb + wave;
+    kv_pre = g0 < ge && (ge - g0 + AWV - 1) / AWV <= KV_PRE;
+    const int gl = kv_pre ? g0 : 0;  // clamped: every wave issues the loads (branch-free), only kv_pre waves use them
+    const int64_t hb = (int64_t)seq * a.seq_stride + g * a.head_stride;
+    static_assert(KV_PRE == 2, "KvPre holds two groups");
+    int4 t[KV_PRE];
+    load_kv_groups<KV_PRE, AWV>(a.kc + hb, a.KV, gl, n_keys, lane >> 4, lane & 15, t);
+    pkv.k0 = t[0];
+    pkv.k1 = t[1];
+    load_kv_groups<KV_PRE, AWV>(a.vc + hb, a.KV, gl, n_keys, lane >> 4, lane & 15, t);
+    pkv.v0 = t[0];
+    pkv.v1 = t[1];
+  }
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (QKV) {
     // ---- prologue (k_gemv_q8 PS): x = x_mid + sum dpart; block (0, 0) stores it; rmsnorm + q8_0 into LDS
     __shared__ __attribute__((aligned(16))) int8_t s_xq[1024];
     __shared__ float s_xd[32];
     __shared__ float s_red[4];
-    if (a.psum) {
 #pragma unroll
-      for (int jv = 0; jv < 4; ++jv) {
-        float v = xv[jv];
+    for (int jv = 0; jv < 4; ++jv) {
+      float v = xv[jv];
 #pragma unroll
-        for (int p = 0; p < FUSED_PARTS; ++p) v = v + pv[p][jv];
-        xv[jv] = v;
-      }
-      if (a.xsum && g == 0 && sp == 0)
-        *reinterpret_cast<float4*>(a.xsum + threadIdx.x * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+      for (int p = 0; p < FUSED_PARTS; ++p) v = v + pv[p][jv];
+      xv[jv] = v;
     }
+    if (a.xsum && g == 0 && sp == 0)
+      *reinterpret_cast<float4*>(a.xsum + threadIdx.x * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
     norm_quant_block_regs<4>(xv, xw, true, a.eps, 1024, s_xq, s_xd, s_red);
     __syncthreads();
     STAMP(12);
@@ -2734,6 +2794,48 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
       y[r] = wave_sum(acc);
     }
     static_assert(QR == 8, "two 16-B stores per wave");
+#if FA_QKV_GRANULE
+    {
+      float yv = y[0];
+#pragma unroll
+      for (int r = 1; r < QR; ++r) yv = lane == r ? y[r] : yv;
+      if (lane < QR)
+        __hip_atomic_store(a.gqkv + qrow0 + QR * wave + lane, ((unsigned long long)ep_qkv << 32) | __float_as_uint(yv),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    STAMP(13);
+    // thread t: head g's local rows 2t, 2t + 1 (q head GQ g, q head GQ g + 1, k head g, v head g; 128 each)
+    __shared__ float s_qkv[(GQ + 2) * D];
+    {
+      const int lr = 2 * threadIdx.x, sg = lr / D;
+      const int grow = (sg < GQ ? (g * GQ + sg) * D : sg == GQ ? (a.H + g) * D : (a.H + a.KV + g) * D) + lr % D;
+      const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.gqkv, (a.H + 2 * a.KV) * D * 8);
+      f4v gv;
+      unsigned spins = 0;
+      for (;;) {
+        gv = ld_sc1_f4(rg, grow * 8);
+        if (__float_as_uint(gv.y) == ep_qkv && __float_as_uint(gv.w) == ep_qkv) break;
+        if (++spins > (1u << 22)) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_qkv[lr] = gv.x;
+      s_qkv[lr + 1] = gv.z;
+    }
+    __syncthreads();
+    STAMP(14);
+#pragma unroll
+    for (int jh = 0; jh < GQ; ++jh) {
+      qpre.x0[jh] = s_qkv[jh * D + lane];
+      qpre.x1[jh] = s_qkv[jh * D + lane + 64];
+    }
+    qpre.kx0 = s_qkv[GQ * D + lane];
+    qpre.kx1 = s_qkv[GQ * D + lane + 64];
+    qpre.v0 = s_qkv[(GQ + 1) * D + lane];
+    qpre.v1 = s_qkv[(GQ + 1) * D + lane + 64];
+#else
     const __amdgpu_buffer_rsrc_t rq = buf_rsrc(a.qkv, (a.H + 2 * a.KV) * D * 4);
     if (lane < 2) {
       const f4v v = lane == 0 ? f4v{y[0], y[1], y[2], y[3]} : f4v{y[4], y[5], y[6], y[7]};
@@ -2752,13 +2854,16 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     qpre.kx1 = ld_sc1_f1(rq, ((a.H + g) * D + lane + 64) * 4);
     qpre.v0 = ld_sc1_f1(rq, ((a.H + a.KV + g) * D + lane) * 4);
     qpre.v1 = ld_sc1_f1(rq, ((a.H + a.KV + g) * D + lane + 64) * 4);
+#endif
   }
   int n_active = 0, j = 0, d0 = 0;
   float M = -INFINITY, L = 0.f;
   float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-  const bool active = attn_split_merge<1, 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
+  // QKV: lean passes (at most 4 groups per wave pass, no next-pass prefetch): the GEMV and the preloads need the
+  // registers; identical arithmetic to k_attn_o<false> up to 4 groups per wave (n_past < 16 x 4 x 4 x 4 = 1024)
+  const bool active = attn_split_merge<1, QKV ? 1 : 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
                                              a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
-                                             M, L, o, &qpre);
+                                             M, L, o, &qpre, QKV && FA_QKV_GRANULE && FA_KV_PRE, pkv, kv_pre);
   float* pbase = a.partials + (int64_t)g * FS * APART;
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
   if (active && wave == 0) {
@@ -2824,9 +2929,11 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                  (GQ + 2) * 128 == FQ_ROWS * ASPLIT,
              "qkv_attn_o_fused: Qwen3-0.6B head layout");
   FA_REQUIRE(wk.partials && fw.opart && fw.cnt && fw.err && x && norm_w, "qkv_attn_o_fused: workspace");
+  FA_REQUIRE(psum || fw.pzero, "qkv_attn_o_fused: zero partials for layer 0");
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err,
-              x, psum, xsum, norm_w, wqkv_q, wqkv_d, fw.cnt + 2 * FUSED_PARTS * CNT_LINE};
+              x, psum ? psum : fw.pzero, psum ? xsum : nullptr, norm_w, wqkv_q, wqkv_d, fw.cnt + 2 * FUSED_PARTS * CNT_LINE, fw.gqkv};
+  FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
 }
 
@@ -2842,12 +2949,20 @@ struct FfnArgs {
   const __half* ud;
   const int8_t* dq;     // down [E][F]
   const __half* dd;
-  float* act;           // [F] hand-off
+  float* act;           // [F] hand-off (FA_FFN_GRANULE: [F] 8-byte granules {value, launch tag})
   float* dpart;         // [FUSED_PARTS][E]
   unsigned* cnt;        // [FUSED_PARTS][CNT_LINE]
   int* err;
   int E, F;
+  const unsigned* epoch;  // the attention launch's fan-in counter of kv head 0: + ASPLIT per launch, never re-armed
 };
+// FA_FFN_GRANULE = 1: the group's act rows are handed over as data-tagged 8-byte granules {f32 value, tag} (one sc1
+// store each; tag = the attention launch's epoch, new every layer and step), and each consumer polls the granules it
+// needs until every tag matches: no drain, no ticket atomic, no read-back after the fan-in (MI355X_MICROARCH.md
+// handoff-1to1 vs handoff-flag). 0: sc1 rows + ticket fan-in + sc1 read-back.
+#ifndef FA_FFN_GRANULE
+#define FA_FFN_GRANULE 1
+#endif
 
 constexpr int FF_ROWS = 12;                        // gate|up rows per block (3 per wave)
 constexpr int FF_GROUP_BLOCKS = 32;                // blocks per down-projection group: 384 act rows = 12 q8_0 blocks
@@ -2878,6 +2993,8 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     const float4 w4 = *reinterpret_cast<const float4*>(f.norm_w + t * PER);
     wv[0] = w4.x; wv[1] = w4.y; wv[2] = w4.z; wv[3] = w4.w;
   }
+  // the epoch: written by the previous launch's atomics (read past this CU's L1 and the XCD's L2 line)
+  const unsigned epoch_v = FA_FFN_GRANULE ? __hip_atomic_load(f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   __builtin_amdgcn_sched_barrier(0);
   GemvArgs a{};
   a.wq = f.gq; a.wd = f.gd; a.wq2 = f.uq; a.wd2 = f.ud; a.O = f.F; a.rpw = 3;
@@ -2930,8 +3047,39 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
     }
   }
   __syncthreads();
-  // ---- publish the block's 12 act rows (write-through), group fan-in
   typedef float f4v __attribute__((ext_vector_type(4)));
+#if FA_FFN_GRANULE
+  // ---- publish the block's 12 act rows as granules tagged with this launch's epoch; poll the group's 384
+  const unsigned ep = epoch_v / ASPLIT;  // >= 1 after the layer's attention launch
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act, f.F * 8);
+  if (t < FF_ROWS)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(f.act) + FF_ROWS * b + t,
+                       ((unsigned long long)ep << 32) | __float_as_uint(s_act[t]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  STAMP(2);
+  f4v gv0 = {0.f, 0.f, 0.f, 0.f}, gv1 = gv0;
+  if (t < FF_GROUP_ROWS / 4) {
+    unsigned spins = 0;
+    const int off = (FF_GROUP_ROWS * grp + 4 * t) * 8;
+    for (;;) {
+      gv0 = ld_sc1_f4(ra, off);
+      gv1 = ld_sc1_f4(ra, off + 16);
+      if (__float_as_uint(gv0.y) == ep && __float_as_uint(gv0.w) == ep && __float_as_uint(gv1.y) == ep &&
+          __float_as_uint(gv1.w) == ep)
+        break;
+      if (++spins > (1u << 22)) {
+        __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  STAMP(3);
+  // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
+  if (t < FF_GROUP_ROWS / 4) {
+    const f4v v = {gv0.x, gv0.z, gv1.x, gv1.z};
+#else
+  // ---- publish the block's 12 act rows (write-through), group fan-in
   const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act, f.F * 4);
   if (t < FF_ROWS / 4) {
     const f4v v = {s_act[4 * t], s_act[4 * t + 1], s_act[4 * t + 2], s_act[4 * t + 3]};
@@ -2943,6 +3091,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
   if (t < FF_GROUP_ROWS / 4) {
     const f4v v = ld_sc1_f4(ra, (FF_GROUP_ROWS * grp + 4 * t) * 4);
+#endif
     const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     const float d = am / 127.0f;
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
@@ -2975,7 +3124,7 @@ void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq,
              "ffn_fused: Qwen3-0.6B FFN shape (E 1024, F 3072)");
   FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
   FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart, fw.cnt + FUSED_PARTS * CNT_LINE,
-            fw.err, E, F};
+            fw.err, E, F, fw.cnt};
   hipLaunchKernelGGL(k_ffn_fused, dim3(F / FF_ROWS), dim3(256), 0, s, f);
 }
 

@@ -61,8 +61,9 @@ int main(int argc, char** argv) {
   __half* wo_d = dalloc<__half>((size_t)3072 * 96);  // scales for every stand-in matrix (zeros)
   CK(hipMemset(wo_q, 1, (size_t)1024 * 2048)); CK(hipMemset(wo_d, 0, (size_t)3072 * 96 * 2));
   FusedDecodeWork fw;
-  fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(3072);
+  fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(2 * 3072); CK(hipMemset(fw.act, 0, 2 * 3072 * 4));
   fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
+  fw.gqkv = dalloc<unsigned long long>(4096); CK(hipMemset(fw.gqkv, 0, 4096 * 8));
   CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   CK(hipMemset(fw.xmid, 0, 1024 * 4)); CK(hipMemset(fw.dpart, 0, 8 * 1024 * 4));
   const int nblk = fused_c ? 256 : M * KV * ATTN_SPLITS;

@@ -70,8 +70,9 @@ int main(int argc, char** argv) {
   const bool two = argc > 1 && !strcmp(argv[1], "fused2");
   const bool fused = two || (argc > 1 && !strcmp(argv[1], "fused"));
   FusedDecodeWork fw;
-  fw.opart = dalloc<float>(8 * E); fw.dpart = dalloc<float>(8 * E); fw.act = dalloc<float>(F); fw.xmid = dalloc<float>(E);
+  fw.opart = dalloc<float>(8 * E); fw.dpart = dalloc<float>(8 * E); fw.act = dalloc<float>(2 * F); CK(hipMemset(fw.act, 0, 2 * F * 4)); fw.xmid = dalloc<float>(E);
   fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
+  fw.gqkv = dalloc<unsigned long long>(4096); CK(hipMemset(fw.gqkv, 0, 4096 * 8));
   CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   CK(hipMemset(fw.opart, 0, 8 * E * 4)); CK(hipMemset(fw.dpart, 0, 8 * E * 4)); CK(hipMemset(fw.xmid, 0, E * 4));
   wk.max_tokens = 1;
