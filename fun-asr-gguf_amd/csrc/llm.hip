@@ -1498,36 +1498,15 @@ struct AttnQIn {
 // it is in flight.
 // PIPE: the next pass's K/V loads are issued before this pass's math (2x the K/V registers: non-lean blocks only;
 // batch-1 B of the fused layer 7.44 -> 7.32 us, scripts/ubench/decode_step)
-// pre (NI <= KV_PRE, use_pre): the first pass's K/V, loaded by the caller (load_kv_groups<KV_PRE, AW> at the same g0);
-// carried as named values (an array here was demoted to scratch)
-constexpr int KV_PRE = 2;
-struct KvPre {
-  int4 k0, k1, v0, v1;
-};
 template <int NI, int AW, bool PIPE>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
-                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
-                                          KvPre pre_kv, bool use_pre) {
+                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8]) {
   int4 kt[NI], vt[NI];
-  if constexpr (NI <= KV_PRE) {
-    if (use_pre) {
-      kt[0] = pre_kv.k0;
-      vt[0] = pre_kv.v0;
-      if constexpr (NI > 1) {
-        kt[NI - 1] = pre_kv.k1;
-        vt[NI - 1] = pre_kv.v1;
-      }
-    } else {
-      load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-      load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
-    }
-  } else {
-    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
-  }
+  load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+  load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
   __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
   if (decode) {
@@ -1692,8 +1671,7 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
                                                  const float* __restrict__ qn, const float* __restrict__ kn,
                                                  const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
                                                  float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
-                                                 float4& o, const AttnQIn* pre, bool pre_cs,
-                                                 KvPre pre_kv, bool use_pre) {
+                                                 float4& o, const AttnQIn* pre = nullptr) {
   constexpr int D = 128;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_keys = pos + 1;
@@ -1726,12 +1704,10 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   const int g0 = gb + wave;
   if (g0 < ge) {
     AttnQIn qi;
-    if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read (pre_cs: the rope too)
+    if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read
       qi = *pre;
-      if (!pre_cs) {
-        qi.c = rcos[(int64_t)pos * 64 + lane];
-        qi.sn = rsin[(int64_t)pos * 64 + lane];
-      }
+      qi.c = rcos[(int64_t)pos * 64 + lane];
+      qi.sn = rsin[(int64_t)pos * 64 + lane];
     } else if (DM) {
       const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
@@ -1763,16 +1739,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
       attn_wave<1, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, use_pre);
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 2)
       attn_wave<2, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, use_pre);
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else if (ni <= 4 || LEAN)
       attn_wave<4, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, false);
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
     else
       attn_wave<8, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc, pre_kv, false);
+                       s_q[wave], s_kn, s_vn, mx, l, acc);
   }
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
   // unscaled): permlane32_swap pairs fold rows {r, r^2}, permlane16_swap pairs fold {r, r^1}; afterwards
@@ -1910,9 +1886,8 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   int n_active, j, d0;
   float M, L;
   float4 o;
-  const KvPre nokv{};
   if (!attn_split_merge<DM, LEAN>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc, qn, kn, rcos,
-                                  rsin, eps, scale, n_active, j, d0, M, L, o, nullptr, false, nokv, false))
+                                  rsin, eps, scale, n_active, j, d0, M, L, o))
     return;
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;  // j, d0: wave 0's lane map
   if (n_active == 1) {
@@ -2648,10 +2623,6 @@ struct AttnOArgs {
 #ifndef FA_QKV_GRANULE
 #define FA_QKV_GRANULE 1
 #endif
-// FA_KV_PRE = 1 (with FA_QKV_GRANULE): the rope row and each wave's first-pass K/V are loaded at kernel start
-#ifndef FA_KV_PRE
-#define FA_KV_PRE 1
-#endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
 
@@ -2739,29 +2710,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
     const int orow = FO_ROWS * sp + 16 * wave + 4 * k + (lane >> 4);
     wk[k] = ld_nt16(a.wo_q + (int64_t)orow * KO + GQ * D * g + 16 * c16);
     dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  // QKV: the rope at pos and this wave's first-pass K/V (cached positions: independent of this step) are loaded now,
-  // in flight under the GEMV and the q|k|v hand-off (attn_split_merge's split of [0, pos], its first KV_PRE groups)
-  KvPre pkv{};
-  bool kv_pre = false;
-  if constexpr (QKV && FA_QKV_GRANULE && FA_KV_PRE) {
-    qpre.c = a.rcos[(int64_t)pos * 64 + lane];
-    qpre.sn = a.rsin[(int64_t)pos * 64 + lane];
-    const int n_keys = pos + 1, n_groups = (n_keys + 3) >> 2;
-    const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)FS));
-    const int gb = sp * gps, ge = min(n_groups, gb + gps), g0 = gb + wave;
-    kv_pre = g0 < ge && (ge - g0 + AWV - 1) / AWV <= KV_PRE;
-    const int gl = kv_pre ? g0 : 0;  // clamped: every wave issues the loads (branch-free), only kv_pre waves use them
-    const int64_t hb = (int64_t)seq * a.seq_stride + g * a.head_stride;
-    static_assert(KV_PRE == 2, "KvPre holds two groups");
-    int4 t[KV_PRE];
-    load_kv_groups<KV_PRE, AWV>(a.kc + hb, a.KV, gl, n_keys, lane >> 4, lane & 15, t);
-    pkv.k0 = t[0];
-    pkv.k1 = t[1];
-    load_kv_groups<KV_PRE, AWV>(a.vc + hb, a.KV, gl, n_keys, lane >> 4, lane & 15, t);
-    pkv.v0 = t[0];
-    pkv.v1 = t[1];
   }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (QKV) {
@@ -2863,7 +2811,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
   // registers; identical arithmetic to k_attn_o<false> up to 4 groups per wave (n_past < 16 x 4 x 4 x 4 = 1024)
   const bool active = attn_split_merge<1, QKV ? 1 : 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
                                              a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
-                                             M, L, o, &qpre, QKV && FA_QKV_GRANULE && FA_KV_PRE, pkv, kv_pre);
+                                             M, L, o, &qpre);
   float* pbase = a.partials + (int64_t)g * FS * APART;
   const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
   if (active && wave == 0) {
