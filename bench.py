@@ -353,7 +353,8 @@ def headline(args, world, dt, dt_prof, prof, stage):
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(enc_peak, 1), "unit": "TFLOP/s",
                 "frac": round(ach / enc_peak, 4), "traffic": None}
     roof.update(kernel=names[dom], avg_launch_us=round(avg_s * 1e6, 2), launches_timed=p["launches"],
-                per_launch=("q8_0 weight bytes" if dom in (0, 4) else "algorithmic FLOPs"),
+                per_launch=("q8_0 weight bytes (+ the two-launch layer's K/V rows)" if dom == 0 else
+                            "q8_0 weight bytes" if dom == 4 else "algorithmic FLOPs"),
                 est_device_ms_per_step={names[c]: round(est_ms[c] / args.steps, 2) for c in prof})
     # the encoder's MFMA classes (secondary: the clip's 705 GFLOP of f32 contractions) against the peak of the
     # arithmetic they run on: bf16x3 = three bf16 MFMA products per f32 product (2.5 PF/s / 3), or exact f32

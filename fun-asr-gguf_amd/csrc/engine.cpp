@@ -200,6 +200,7 @@ struct Engine {
 
   // ---- profiling helpers: bracket launches of class `cls` with events on the engine stream
   bool prof_sample = true;  // decode layers > 0 are not bracketed (keeps the eager host ahead of the GPU)
+  int prof_pos = 0;         // position of the profiled eager batch-1 decode step
   void prof_begin(int cls, hipEvent_t* a) {
     if (!prof || !prof_sample) return;
     if (ev_next >= ev_pool.size()) {
@@ -968,13 +969,15 @@ struct Engine {
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       if (use_fused == 1) {
-        // a q8_0 weight-streaming layer launch (class 0, like C): q|k|v + Wo weight bytes (its K/V reads are not counted)
+        // a q8_0 weight-streaming layer launch (class 0, like C): algorithmic bytes = q|k|v + Wo weights + the K/V
+        // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
         hipEvent_t ev;
         prof_begin(0, &ev);
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
                          w.o.q, w.o.d, E, attn_wk, fdw, stream);
-        prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0, 2.0 * (E * H * D + (double)QKV * E));
+        prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0 + 4.0 * KV * D * (prof_pos + 1.0),
+                 2.0 * (E * H * D + (double)QKV * E));
       } else {
         GemvArgs a{};
         a.M = 1;
@@ -1548,7 +1551,10 @@ int fa_llm_generate_begin(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int
     const hipGraphExec_t ex = e->step_graph(n_seqs);
     for (int st = 0; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, e->stream));
   } else {
-    for (int st = 0; st < n_steps; ++st) e->decode_step(n_seqs);
+    for (int st = 0; st < n_steps; ++st) {
+      e->prof_pos = ps[0] + st;  // the profiled fused layer's K/V bytes (batch 1)
+      e->decode_step(n_seqs);
+    }
   }
   // the sampled tokens land in pinned host memory; fa_llm_generate_end waits for them (the host may work meanwhile)
   FA_HIP(hipMemcpyAsync(e->h_hist, e->d_tok_hist, (size_t)n_seqs * e->hist_max * 4, hipMemcpyDeviceToHost, e->stream));
