@@ -101,15 +101,16 @@ int main(int argc, char** argv) {
     const int slot_o[] = {1, 3, 7, 9, 10, 11, -1};
     const char* nm_o[] = {"splits known", "q normed/roped", "split merged", "partial published", "fan-in passed",
                           "combined + quantised", ""};
-    const int slot_a[] = {0, 12, 13, 14, 3, 7, 9, 10, 11};
-    const char* nm_a[] = {"loads issued", "x normed + q8", "q|k|v rows stored", "q|k|v fan-in passed", "q normed/roped",
-                          "split merged", "partial published", "fan-in passed", "combined + quantised"};
+    const int slot_a[] = {0, 12, 13, 14, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11};
+    const char* nm_a[] = {"loads issued", "x normed + q8", "q|k|v rows stored", "q|k|v hand-off passed", "splits known",
+                          "K/V issued", "q normed/roped", "scores", "softmax", "p.V", "split merged",
+                          "partial published", "fan-in passed", "combined + quantised"};
     const int slot_c[] = {0, 1, 2, 3, 4, 5, -1};
     const char* nm_c[] = {"block start", "x normed + q8", "act published", "group fan-in passed", "act quantised",
                           "down slice stored", ""};
     const int* slot = fused_a ? slot_a : fused_c ? slot_c : fused_o ? slot_o : slot_b;
     const char* const* nm = fused_a ? nm_a : fused_c ? nm_c : fused_o ? nm_o : nm_b;
-    for (int k = 0; k < (fused_a ? 9 : fused_c || fused_o ? 6 : 7); ++k) {
+    for (int k = 0; k < (fused_a ? 14 : fused_c || fused_o ? 6 : 7); ++k) {
       std::vector<double> v;
       for (int b = 0; b < nblk; ++b) {  // stamps left by an earlier launch (before t0) are not this launch's
         const long long d = (long long)(st[b * 16 + slot[k]] - t0);

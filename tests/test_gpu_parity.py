@@ -479,3 +479,39 @@ def test_llm_generate_begin_end_equals_generate(llm_tiny_oracle):
             e.close()
     np.testing.assert_array_equal(runs[0], runs[2])
     np.testing.assert_array_equal(runs[1], runs[3])
+
+
+def test_two_launch_layer_long_context():
+    """The two-launch layer past the positions the other tests reach: n_past ~1300 gives each wave of a key split
+    more than 4 groups, so the AB launch runs several lean passes (the three-launch layer runs 8-group passes there:
+    the same math in another f32 order). Teacher-forced against the oracle and close to the three-launch layer; the
+    granule epochs keep working across mode switches (1 -> 2 -> 1 on one engine)."""
+    from fun_asr_gguf import _native
+    cfg = dict(synth.LLM_TINY, n_ctx=1400, max_seqs=2)
+    eng = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)
+    eng.synthetic_weights(0)
+    m = oqw.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=1400)
+    rng = np.random.default_rng(21)
+    prompt = np.concatenate([m.embed_prompt(rng.integers(0, 4096, 40)),
+                             (rng.standard_normal((1260, 1024)) * 0.5).astype(np.float32)], 0)
+    runs = []
+    for mode in (1, 2, 1):
+        eng.set_decode_fused(mode)
+        eng.llm_reset(0)
+        tok = eng.llm_prefill(0, prompt)
+        lgs, toks = [], [tok]
+        for _ in range(5):
+            toks.append(int(eng.llm_generate([0], 1)[0][0]))
+            lgs.append(eng.llm_logits(0))
+        runs.append((toks, lgs))
+    eng.close()
+    (t1, l1), (t2, l2), (t1b, l1b) = runs
+    assert t1b == t1 and all(np.array_equal(a, b) for a, b in zip(l1, l1b))  # the epochs after a mode switch
+    m.reset()
+    m.forward(prompt, 0)
+    for k in range(5):
+        if t1[:k + 1] != t2[:k + 1]:
+            break
+        assert _cos(l1[k], l2[k]) > 0.99999
+        ref = m.forward(m.embed_tokens([t1[k]]), prompt.shape[0] + k)
+        _check_step(l1[k], ref)
