@@ -151,6 +151,7 @@ struct Engine {
   std::vector<int> logits_row;  // per sequence: its row of `logits` in the most recent forward (-1: none)
   AttnWork attn_wk;
   FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
+  int fused_max_m = FUSED_MAX_M;  // decode batches up to this width take the two-launch layer (FUNASR_FUSED_MAX_M)
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
@@ -643,19 +644,19 @@ struct Engine {
     attn_wk.counters = alloc<int>((size_t)pf_max * KV * CNT_LINE);
     FA_HIP(hipMemset(attn_wk.counters, 0, (size_t)pf_max * KV * CNT_LINE * sizeof(int)));
     attn_wk.partials = alloc<float>((size_t)m_max * KV * ATTN_SPLITS * ATTN_PART_FLOATS);
-    fdw.opart = alloc<float>((size_t)FUSED_PARTS * E);
-    fdw.dpart = alloc<float>((size_t)FUSED_PARTS * E);
-    fdw.act = alloc<float>(2 * (size_t)lc.n_ff);
-    FA_HIP(hipMemset(fdw.act, 0, 2 * (size_t)lc.n_ff * sizeof(float)));
-    fdw.xmid = alloc<float>(E);
-    fdw.cnt = alloc<unsigned>((size_t)FUSED_CNT_LINES * CNT_LINE);
-    fdw.err = alloc<int>(1);
-    {
-      const size_t nq = (size_t)(lc.n_head + 2 * lc.n_head_kv) * lc.head_dim;
-      fdw.gqkv = reinterpret_cast<unsigned long long*>(alloc<float>(2 * nq));
-      FA_HIP(hipMemset(fdw.gqkv, 0, nq * 8));
-      fdw.pzero = alloc<float>((size_t)FUSED_PARTS * E);
-      FA_HIP(hipMemset(fdw.pzero, 0, (size_t)FUSED_PARTS * E * sizeof(float)));
+    {  // fused-layer workspace: one slab per token of a batch of up to FUSED_MAX_M
+      const size_t MF = FUSED_MAX_M, nq = (size_t)(lc.n_head + 2 * lc.n_head_kv) * lc.head_dim;
+      fdw.opart = alloc<float>(MF * FUSED_PARTS * E);
+      fdw.dpart = alloc<float>(MF * FUSED_PARTS * E);
+      fdw.act = alloc<float>(MF * 2 * (size_t)lc.n_ff);
+      FA_HIP(hipMemset(fdw.act, 0, MF * 2 * (size_t)lc.n_ff * sizeof(float)));
+      fdw.xmid = alloc<float>(MF * E);
+      fdw.cnt = alloc<unsigned>((size_t)FUSED_CNT_LINES * CNT_LINE);
+      fdw.err = alloc<int>(1);
+      fdw.gqkv = reinterpret_cast<unsigned long long*>(alloc<float>(MF * 2 * nq));
+      FA_HIP(hipMemset(fdw.gqkv, 0, MF * nq * 8));
+      fdw.pzero = alloc<float>(MF * FUSED_PARTS * E);
+      FA_HIP(hipMemset(fdw.pzero, 0, MF * FUSED_PARTS * E * sizeof(float)));
     }
     FA_HIP(hipMemset(fdw.cnt, 0, (size_t)FUSED_CNT_LINES * CNT_LINE * sizeof(unsigned)));
     FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
@@ -862,13 +863,15 @@ struct Engine {
     // batched decode: the residual GEMMs (o, down) quantise their new rows times the next RMSNorm weight and leave
     // per-token sum-of-squares partials; q|k|v, gate|up and the LM head apply rstd to those rows' block scales
     // (no k_prep_q8 launches but layer 0's)
-    const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm;
+    const bool fused = decode && fused_shape_ok() && ((M == 1 && use_fused) || (M <= fused_max_m && use_fused == 1));
+    const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm && !fused;
     (void)max_pos;
-    if (decode && M == 1 && use_fused && fused_shape_ok()) {
-      llm_forward_fused();
-      return;
+    if (fused) {
+      llm_forward_fused(M);
+      if (M == 1) return;  // the batch-1 LM head completes the residual in its prologue
+      psum_rows(fdw.xmid, fdw.dpart, M, E, lx, stream);
     }
-    for (int l = 0; l < lc.n_layer; ++l) {
+    for (int l = 0; l < (fused ? 0 : lc.n_layer); ++l) {
       const LlmLayerW& w = layers[l];
       prof_sample = l == 0;  // sampled timing: layer 0's launches stand for every layer (identical shapes)
       __half* kc = kcache + (size_t)l * layer_stride;
@@ -960,7 +963,9 @@ struct Engine {
   //   B  attention + this split's slice of the o projection -> opart
   //   C  x_mid = lx + sum opart; gate|up + SwiGLU; group fan-in; slice of the down projection -> dpart
   // then the LM head with the same partial-sum prologue.
-  void llm_forward_fused() {
+  // M > 1 (small decode batches, two-launch layer only): every launch has one grid slab per token; the layers end
+  // with x_mid + partials per token, which llm_forward sums (psum_rows) for the regular LM head.
+  void llm_forward_fused(int M = 1) {
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
     for (int l = 0; l < lc.n_layer; ++l) {
@@ -975,9 +980,9 @@ struct Engine {
         prof_begin(0, &ev);
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
-                         w.o.q, w.o.d, E, attn_wk, fdw, stream);
-        prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0 + 4.0 * KV * D * (prof_pos + 1.0),
-                 2.0 * (E * H * D + (double)QKV * E));
+                         w.o.q, w.o.d, E, attn_wk, fdw, stream, M);
+        prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0 + (M == 1 ? 4.0 * KV * D * (prof_pos + 1.0) : 0.0),
+                 2.0 * M * (E * H * D + (double)QKV * E));
       } else {
         GemvArgs a{};
         a.M = 1;
@@ -998,11 +1003,13 @@ struct Engine {
       {
         hipEvent_t ev;
         prof_begin(0, &ev);
-        ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream);
-        prof_end(0, 3.0 * F * E * 34.0 / 32.0, 2.0 * 3.0 * F * E);
+        ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream,
+                  M);
+        prof_end(0, 3.0 * F * E * 34.0 / 32.0, 2.0 * 3.0 * M * F * E);
       }
     }
     prof_sample = true;
+    if (M > 1) return;
     GemvArgs h{};
     h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
@@ -1142,6 +1149,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
+    if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
@@ -1573,7 +1581,7 @@ int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
   FA_HIP(hipEventSynchronize(e->ev_gen));
   const int n_seqs = (int)e->gen_seqs.size(), n_steps = e->gen_steps;
   e->prof_collect();
-  if (n_seqs == 1) e->check_fused_error();
+  if (n_seqs <= fa::FUSED_MAX_M) e->check_fused_error();
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = e->gen_seqs[i];

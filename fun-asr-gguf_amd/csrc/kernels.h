@@ -140,17 +140,18 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
 // projection, each with an in-launch group fan-in (see the kernels). FUSED_PARTS = partial vectors summed by the next
 // launch's prologue (8 kv heads for o, 8 groups of 384 act rows for down).
 constexpr int FUSED_PARTS = 8;
-constexpr int FUSED_CNT_LINES = 3 * FUSED_PARTS;
+constexpr int FUSED_MAX_M = 8;  // decode batch widths the two-launch layer takes (one grid slab per token)
+constexpr int FUSED_CNT_LINES = 3 * FUSED_MAX_M * FUSED_PARTS;
 struct FusedDecodeWork {
-  float* opart = nullptr;   // [FUSED_PARTS][E]
-  float* dpart = nullptr;   // [FUSED_PARTS][E]
-  float* act = nullptr;     // [2 F] act hand-off (F 8-byte granules; zeroed once)
-  float* xmid = nullptr;    // [E] residual stream after the attention block
+  float* opart = nullptr;   // [FUSED_MAX_M][FUSED_PARTS][E]
+  float* dpart = nullptr;   // [FUSED_MAX_M][FUSED_PARTS][E]
+  float* act = nullptr;     // [FUSED_MAX_M][2 F] act hand-off (F 8-byte granules per token; zeroed once)
+  float* xmid = nullptr;    // [FUSED_MAX_M][E] residual stream after the attention block
   unsigned* cnt = nullptr;  // [FUSED_CNT_LINES][CNT_LINE] ticket counters (zeroed once, never re-armed): o fan-in,
                             // down-group fan-in, q|k|v fan-in (two-launch layer), FUSED_PARTS lines each
   int* err = nullptr;       // set to 1 by a timed-out fan-in wait
-  float* pzero = nullptr;   // [FUSED_PARTS][E] zeros: layer 0's partials in the two-launch layer
-  unsigned long long* gqkv = nullptr;  // [(H + 2 KV) D] q|k|v granules of the two-launch layer (zeroed once)
+  float* pzero = nullptr;   // [FUSED_MAX_M][FUSED_PARTS][E] zeros: layer 0's partials in the two-launch layer
+  unsigned long long* gqkv = nullptr;  // [FUSED_MAX_M][(H + 2 KV) D] q|k|v granules of the two-launch layer (zeroed once)
 };
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
@@ -162,10 +163,13 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s);
+                      const FusedDecodeWork& fw, hipStream_t s, int M = 1);
+// M tokens (rows of x / xsum, slabs of the workspace); M = 1: the batch-1 layer
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
-               hipStream_t s);
+               hipStream_t s, int M = 1);
+// out[m] = xmid[m] + sum_p dpart[m][p] for m < M (a small batch's residual rows after its last fused layer)
+void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);
 // dst[i] = src[rows[i]] (n rows of E floats; row stride E both sides)
 void gather_rows(const float* src, const int* rows, int n, int E, float* dst, hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,

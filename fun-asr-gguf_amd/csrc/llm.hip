@@ -2632,11 +2632,30 @@ constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch lay
 // same wave_sum per row: bit-identical q|k|v values), publish them with sc1 stores and pass a 16-block fan-in;
 // then the attention + o slice of k_attn_o<false>, with the q|k|v inputs read back with sc1 loads. This replaces
 // a kernel boundary (A -> B) by a group-local fan-in whose producers are its consumers.
+// Token m = blockIdx.z of a small decode batch (two-launch layer, M <= FUSED_MAX_M): every per-token buffer and
+// ticket line is offset by m here, so the body reads as the batch-1 kernel (kernel-uniform pointer arithmetic).
 template <bool QKV>
-__global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a) {
+__global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   constexpr int D = 128, FS = ASPLIT;
   typedef float f4v __attribute__((ext_vector_type(4)));
-  const int g = blockIdx.x, sp = blockIdx.y;
+  const int g = blockIdx.x, sp = blockIdx.y, mt = blockIdx.z;
+  AttnOArgs a = a0;
+  {
+    const int nq = (a.H + 2 * a.KV) * D;
+    a.tok_pos += mt;
+    a.tok_seq += mt;
+    a.qkv += (int64_t)mt * nq;
+    a.opart += (int64_t)mt * a.KV * a.E;
+    a.cnt += mt * a.KV * CNT_LINE;
+    a.partials += (int64_t)mt * a.KV * FS * APART;
+    if constexpr (QKV) {
+      a.x += (int64_t)mt * 1024;
+      a.psum += (int64_t)mt * FUSED_PARTS * 1024;
+      if (a.xsum) a.xsum += (int64_t)mt * 1024;
+      a.cnt_qkv += mt * a.KV * CNT_LINE;
+      a.gqkv += (int64_t)mt * nq;
+    }
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   AttnQIn qpre;
   qpre.c = qpre.sn = 0.f;
@@ -2872,7 +2891,8 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s) {
+                      const FusedDecodeWork& fw, hipStream_t s, int M) {
+  FA_REQUIRE(M >= 1 && M <= FUSED_MAX_M && M <= wk.max_split_tokens, "qkv_attn_o_fused: 1 <= M <= FUSED_MAX_M");
   FA_REQUIRE(H == KV * GQ && KV == FUSED_PARTS && E == FO_ROWS * ASPLIT && E == 1024 &&
                  (GQ + 2) * 128 == FQ_ROWS * ASPLIT,
              "qkv_attn_o_fused: Qwen3-0.6B head layout");
@@ -2880,9 +2900,10 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
   FA_REQUIRE(psum || fw.pzero, "qkv_attn_o_fused: zero partials for layer 0");
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err,
-              x, psum ? psum : fw.pzero, psum ? xsum : nullptr, norm_w, wqkv_q, wqkv_d, fw.cnt + 2 * FUSED_PARTS * CNT_LINE, fw.gqkv};
+              x, psum ? psum : fw.pzero, psum ? xsum : nullptr, norm_w, wqkv_q, wqkv_d,
+              fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
-  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
+  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, M), dim3(AWV * 64), 0, s, a);
 }
 
 struct FfnArgs {
@@ -2917,9 +2938,21 @@ constexpr int FF_GROUP_BLOCKS = 32;                // blocks per down-projection
 constexpr int FF_GROUP_ROWS = FF_ROWS * FF_GROUP_BLOCKS;
 constexpr int FD_ROWS = 32;                        // down-projection rows per block (E / FF_GROUP_BLOCKS)
 
-__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
+// token m = blockIdx.y of a small decode batch: per-token buffers and ticket lines offset here (as k_attn_o)
+__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f0) {
   constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
   const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
+  FfnArgs f = f0;
+  {
+    const int mt = blockIdx.y;
+    f.x += (int64_t)mt * f.E;
+    f.opart += (int64_t)mt * FUSED_PARTS * f.E;
+    f.xmid += (int64_t)mt * f.E;
+    f.act += (int64_t)mt * 2 * f.F;  // F granules (8 B) per token
+    f.dpart += (int64_t)mt * FUSED_PARTS * f.E;
+    f.cnt += mt * FUSED_PARTS * CNT_LINE;
+    f.epoch += mt * FUSED_PARTS * CNT_LINE;  // the attention fan-in line of (token m, kv head 0)
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
   STAMP(0);
   __shared__ __attribute__((aligned(16))) int8_t s_q[K];
@@ -3065,15 +3098,36 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f) {
   STAMP(5);
 }
 
+// out[m] = xmid[m] + dpart[m][0] + ... + dpart[m][FUSED_PARTS - 1] (the order of the batch-1 partial-sum prologues):
+// the residual rows after a small batch's last fused layer, for the LM head
+__global__ __launch_bounds__(256) void k_psum_rows(const float* __restrict__ xmid, const float* __restrict__ dpart, int E,
+                                                   float* __restrict__ out) {
+  const int m = blockIdx.y, e = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e >= E) return;
+  float4 v = *reinterpret_cast<const float4*>(xmid + (int64_t)m * E + e);
+#pragma unroll
+  for (int p = 0; p < FUSED_PARTS; ++p) {
+    const float4 q = *reinterpret_cast<const float4*>(dpart + ((int64_t)m * FUSED_PARTS + p) * E + e);
+    v.x = v.x + q.x; v.y = v.y + q.y; v.z = v.z + q.z; v.w = v.w + q.w;
+  }
+  *reinterpret_cast<float4*>(out + (int64_t)m * E + e) = v;
+}
+
+void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s) {
+  FA_REQUIRE(E % 4 == 0, "psum_rows: E % 4");
+  hipLaunchKernelGGL(k_psum_rows, dim3(cdiv(E / 4, 256), M), dim3(256), 0, s, xmid, dpart, E, out);
+}
+
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
-               hipStream_t s) {
+               hipStream_t s, int M) {
+  FA_REQUIRE(M >= 1 && M <= FUSED_MAX_M, "ffn_fused: 1 <= M <= FUSED_MAX_M");
   FA_REQUIRE(E == 1024 && F == FF_GROUP_ROWS * FUSED_PARTS && E == FD_ROWS * FF_GROUP_BLOCKS,
              "ffn_fused: Qwen3-0.6B FFN shape (E 1024, F 3072)");
   FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
-  FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart, fw.cnt + FUSED_PARTS * CNT_LINE,
-            fw.err, E, F, fw.cnt};
-  hipLaunchKernelGGL(k_ffn_fused, dim3(F / FF_ROWS), dim3(256), 0, s, f);
+  FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart,
+            fw.cnt + FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.err, E, F, fw.cnt};
+  hipLaunchKernelGGL(k_ffn_fused, dim3(F / FF_ROWS, M), dim3(256), 0, s, f);
 }
 
 }  // namespace fa
