@@ -151,7 +151,11 @@ struct Engine {
   std::vector<int> logits_row;  // per sequence: its row of `logits` in the most recent forward (-1: none)
   AttnWork attn_wk;
   FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
-  int fused_max_m = FUSED_MAX_M;  // decode batches up to this width take the two-launch layer (FUNASR_FUSED_MAX_M)
+  // decode batches up to this width take the two-launch layer (FUNASR_FUSED_MAX_M, <= FUSED_MAX_M). Measured per step
+  // (scripts/prof_small_batch.py, full model): M 1-6 0.480 / 0.564 / 0.696 / 0.759 / 0.976 / 0.997 ms vs 0.601 / 0.713 /
+  // 0.812 / 0.935 / 1.004 / 1.042 ms on the 5-launch layer; M 7 / 8 1.236 / 1.312 vs 1.064 / 1.070 ms (the C launch's
+  // grid slabs no longer fit the chip at once)
+  int fused_max_m = 6;
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)

@@ -319,13 +319,14 @@ def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
 
 
 @pytest.mark.parametrize("M", [2, 6, 8])
-def test_two_launch_layer_small_batches(llm_tiny_oracle, M):
+def test_two_launch_layer_small_batches(llm_tiny_oracle, monkeypatch, M):
     """Decode batches of 2..8 sequences on the two-launch layer (one grid slab per token; sequences at different
     positions, non-contiguous ids) against the 5-launch layer and teacher-forced against the oracle; a token's logits
     equal its batch-1 logits on the same layer (bit-identical up to M = 5, where the LM head is the fused GEMV in both:
     per-token arithmetic does not depend on the batch)."""
     from fun_asr_gguf import _native
     m = llm_tiny_oracle
+    monkeypatch.setenv("FUNASR_FUSED_MAX_M", "8")  # the default stops at the measured crossover (6)
     eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=512, max_seqs=16), max_batch=1, max_samples=16000)
     eng.synthetic_weights(0)
     rng = np.random.default_rng(30 + M)
