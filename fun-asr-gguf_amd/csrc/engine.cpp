@@ -152,9 +152,9 @@ struct Engine {
   AttnWork attn_wk;
   FusedDecodeWork fdw;     // fused batch-1 decode layer (3 launches per layer)
   // decode batches up to this width take the two-launch layer (FUNASR_FUSED_MAX_M, <= FUSED_MAX_M). Measured per step
-  // (scripts/prof_small_batch.py, full model): M 1-6 0.480 / 0.564 / 0.696 / 0.759 / 0.976 / 0.997 ms vs 0.601 / 0.713 /
-  // 0.812 / 0.935 / 1.004 / 1.042 ms on the 5-launch layer; M 7 / 8 1.236 / 1.312 vs 1.064 / 1.070 ms (the C launch's
-  // grid slabs no longer fit the chip at once)
+  // (scripts/prof_small_batch.py, full model, two tokens per fused-FFN block from M = 4): M 1-6 0.486 / 0.566 / 0.694 /
+  // 0.698 / 0.933 / 0.915 ms vs 0.594 / 0.709 / 0.812 / 0.935 / 1.000 / 1.047 ms on the 5-launch layer; M 7 / 8 1.213 /
+  // 1.261 vs 1.070 / 1.073 ms (the AB launch's token slabs, 128 blocks each, no longer fit the chip at once)
   int fused_max_m = 6;
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
@@ -1154,6 +1154,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
+    fa::g_ffn_pair_min_m = 4;
+    if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");

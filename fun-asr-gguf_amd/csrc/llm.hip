@@ -2619,7 +2619,7 @@ struct AttnOArgs {
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
-// no drain, no ticket, no read-back (FA_FFN_GRANULE's hand-off). 0: sc1 rows + ticket fan-in + sc1 read-back.
+// no drain, no ticket, no read-back (the fused FFN's hand-off). 0: sc1 rows + ticket fan-in + sc1 read-back.
 #ifndef FA_QKV_GRANULE
 #define FA_QKV_GRANULE 1
 #endif
@@ -2918,64 +2918,65 @@ struct FfnArgs {
   const __half* ud;
   const int8_t* dq;     // down [E][F]
   const __half* dd;
-  float* act;           // [F] hand-off (FA_FFN_GRANULE: [F] 8-byte granules {value, launch tag})
+  float* act;           // [M][F] 8-byte granules {value, launch tag} (hand-off)
   float* dpart;         // [FUSED_PARTS][E]
   unsigned* cnt;        // [FUSED_PARTS][CNT_LINE]
   int* err;
   int E, F;
   const unsigned* epoch;  // the attention launch's fan-in counter of kv head 0: + ASPLIT per launch, never re-armed
 };
-// FA_FFN_GRANULE = 1: the group's act rows are handed over as data-tagged 8-byte granules {f32 value, tag} (one sc1
-// store each; tag = the attention launch's epoch, new every layer and step), and each consumer polls the granules it
-// needs until every tag matches: no drain, no ticket atomic, no read-back after the fan-in (MI355X_MICROARCH.md
-// handoff-1to1 vs handoff-flag). 0: sc1 rows + ticket fan-in + sc1 read-back.
-#ifndef FA_FFN_GRANULE
-#define FA_FFN_GRANULE 1
-#endif
+// The group's act rows are handed over as data-tagged 8-byte granules {f32 value, tag} (one sc1 store each; tag = the
+// attention launch's epoch, new every layer and step), and each consumer polls the granules it needs until every tag
+// matches: no drain, no ticket atomic, no read-back (MI355X_MICROARCH.md handoff-1to1 vs handoff-flag; measured C 6.08
+// -> 5.61 us against the sc1 rows + ticket fan-in + read-back form).
 
 constexpr int FF_ROWS = 12;                        // gate|up rows per block (3 per wave)
 constexpr int FF_GROUP_BLOCKS = 32;                // blocks per down-projection group: 384 act rows = 12 q8_0 blocks
 constexpr int FF_GROUP_ROWS = FF_ROWS * FF_GROUP_BLOCKS;
 constexpr int FD_ROWS = 32;                        // down-projection rows per block (E / FF_GROUP_BLOCKS)
 
-// token m = blockIdx.y of a small decode batch: per-token buffers and ticket lines offset here (as k_attn_o)
-__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f0) {
+// CT tokens per block (small decode batches: CT = 2 from 4 tokens on, so every block's weights serve two tokens and
+// the token slabs fit the chip at once); tokens m0 = CT blockIdx.y .. m0 + ct - 1 (ct = min(CT, M - m0), block-uniform).
+// Per token: x_mid = x + sum opart (block 0 stores it), rmsnorm + q8_0, gate|up + SwiGLU for the block's 12 rows, published
+// as granules {value, epoch} (the epoch of that token's attention launch); the group's 384 act rows polled, quantised
+// and multiplied into the block's 32-row slice of the down projection. Same arithmetic for every CT.
+template <int CT>
+__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
   constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
   const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
-  FfnArgs f = f0;
-  {
-    const int mt = blockIdx.y;
-    f.x += (int64_t)mt * f.E;
-    f.opart += (int64_t)mt * FUSED_PARTS * f.E;
-    f.xmid += (int64_t)mt * f.E;
-    f.act += (int64_t)mt * 2 * f.F;  // F granules (8 B) per token
-    f.dpart += (int64_t)mt * FUSED_PARTS * f.E;
-    f.cnt += mt * FUSED_PARTS * CNT_LINE;
-    f.epoch += mt * FUSED_PARTS * CNT_LINE;  // the attention fan-in line of (token m, kv head 0)
-  }
+  const int m0 = blockIdx.y * CT, ct = min(CT, M - m0);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, t = threadIdx.x;
   STAMP(0);
-  __shared__ __attribute__((aligned(16))) int8_t s_q[K];
-  __shared__ float s_d[NB];
-  __shared__ float s_red[4];
-  __shared__ float s_act[FF_ROWS];
-  __shared__ __attribute__((aligned(16))) int8_t s_aq[FF_GROUP_ROWS];
-  __shared__ float s_ad[GB];
-  // ---- activation loads (x, the 8 o partials, the norm weights), then every weight load of the block
-  float xv[PER], pv[FUSED_PARTS][PER], wv[PER];
-  {
-    const float4 a4 = *reinterpret_cast<const float4*>(f.x + t * PER);
-    xv[0] = a4.x; xv[1] = a4.y; xv[2] = a4.z; xv[3] = a4.w;
+  __shared__ __attribute__((aligned(16))) int8_t s_q[CT][K];
+  __shared__ float s_d[CT][NB];
+  __shared__ float s_red[CT][4];
+  __shared__ float s_act[CT][FF_ROWS];
+  __shared__ __attribute__((aligned(16))) int8_t s_aq[CT][FF_GROUP_ROWS];
+  __shared__ float s_ad[CT][GB];
+  // ---- activation loads (x, the 8 o partials per token; the norm weights), then every weight load of the block
+  float xv[CT][PER], pv[CT][FUSED_PARTS][PER], wv[PER];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int m = m0 + min(c, ct - 1);  // a missing second token loads the first's rows (unused)
+    const float4 a4 = *reinterpret_cast<const float4*>(f.x + (int64_t)m * f.E + t * PER);
+    xv[c][0] = a4.x; xv[c][1] = a4.y; xv[c][2] = a4.z; xv[c][3] = a4.w;
 #pragma unroll
     for (int g = 0; g < FUSED_PARTS; ++g) {
-      const float4 p4 = *reinterpret_cast<const float4*>(f.opart + g * f.E + t * PER);
-      pv[g][0] = p4.x; pv[g][1] = p4.y; pv[g][2] = p4.z; pv[g][3] = p4.w;
+      const float4 p4 = *reinterpret_cast<const float4*>(f.opart + ((int64_t)m * FUSED_PARTS + g) * f.E + t * PER);
+      pv[c][g][0] = p4.x; pv[c][g][1] = p4.y; pv[c][g][2] = p4.z; pv[c][g][3] = p4.w;
     }
+  }
+  {
     const float4 w4 = *reinterpret_cast<const float4*>(f.norm_w + t * PER);
     wv[0] = w4.x; wv[1] = w4.y; wv[2] = w4.z; wv[3] = w4.w;
   }
-  // the epoch: written by the previous launch's atomics (read past this CU's L1 and the XCD's L2 line)
-  const unsigned epoch_v = FA_FFN_GRANULE ? __hip_atomic_load(f.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  // the epochs: written by the attention launch's atomics (read past this CU's L1 and the XCD's L2 line); token m's
+  // attention fan-in line of kv head 0
+  unsigned ep[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+    ep[c] = __hip_atomic_load(f.epoch + (m0 + min(c, ct - 1)) * FUSED_PARTS * CNT_LINE, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT) / ASPLIT;  // >= 1 after the layer's attention launch
   __builtin_amdgcn_sched_barrier(0);
   GemvArgs a{};
   a.wq = f.gq; a.wd = f.gd; a.wq2 = f.uq; a.wd2 = f.ud; a.O = f.F; a.rpw = 3;
@@ -2995,23 +2996,29 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f0) {
     dsv[i] = __half2float(f.dd[(int64_t)drow * (f.F / 32) + GB * grp + 4 * i + (c8 >> 1)]);
   }
   __builtin_amdgcn_sched_barrier(0);
-  // ---- x_mid = x + sum_g opart[g]; rmsnorm + q8_0 into LDS
+  // ---- per token: x_mid = x + sum_g opart[g]; rmsnorm + q8_0 into LDS
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    float v = xv[j];
+  for (int c = 0; c < CT; ++c) {
 #pragma unroll
-    for (int g = 0; g < FUSED_PARTS; ++g) v = v + pv[g][j];
-    xv[j] = v;
+    for (int j = 0; j < PER; ++j) {
+      float v = xv[c][j];
+#pragma unroll
+      for (int g = 0; g < FUSED_PARTS; ++g) v = v + pv[c][g][j];
+      xv[c][j] = v;
+    }
+    if (b == 0 && c < ct)
+      *reinterpret_cast<float4*>(f.xmid + (int64_t)(m0 + c) * f.E + t * PER) =
+          make_float4(xv[c][0], xv[c][1], xv[c][2], xv[c][3]);
+    norm_quant_block_regs<PER>(xv[c], wv, true, f.eps, K, s_q[c], s_d[c], s_red[c]);
   }
-  if (b == 0) *reinterpret_cast<float4*>(f.xmid + t * PER) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-  norm_quant_block_regs<PER>(xv, wv, true, f.eps, K, s_q, s_d, s_red);
   __syncthreads();
   STAMP(1);
-  // ---- gate|up + SwiGLU for this wave's 3 rows (compute_group's arithmetic)
-  {
+  // ---- gate|up + SwiGLU for this wave's 3 rows (compute_group's arithmetic), per token
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
     float acc[3] = {0.f, 0.f, 0.f}, acc2[3] = {0.f, 0.f, 0.f};
-    const int4 xq = *reinterpret_cast<const int4*>(s_q + lane * 16);
-    const float xdv = s_d[lane >> 1];
+    const int4 xq = *reinterpret_cast<const int4*>(s_q[c] + lane * 16);
+    const float xdv = s_d[c][lane >> 1];
 #pragma unroll
     for (int rr = 0; rr < 3; ++rr) {
       int si = dot16(G.w[rr][0], xq, 0);
@@ -3024,29 +3031,33 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f0) {
 #pragma unroll
     for (int rr = 0; rr < 3; ++rr) {
       const float y = wave_sum(acc[rr]), y2 = wave_sum(acc2[rr]);
-      if (lane == 0) s_act[wave * 3 + rr] = (y / (1.0f + expf(-y))) * y2;
+      if (lane == 0) s_act[c][wave * 3 + rr] = (y / (1.0f + expf(-y))) * y2;
     }
   }
   __syncthreads();
   typedef float f4v __attribute__((ext_vector_type(4)));
-#if FA_FFN_GRANULE
-  // ---- publish the block's 12 act rows as granules tagged with this launch's epoch; poll the group's 384
-  const unsigned ep = epoch_v / ASPLIT;  // >= 1 after the layer's attention launch
-  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act, f.F * 8);
-  if (t < FF_ROWS)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(f.act) + FF_ROWS * b + t,
-                       ((unsigned long long)ep << 32) | __float_as_uint(s_act[t]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  // ---- publish each token's 12 act rows as granules tagged with its epoch; poll the group's 384 per token
+  // (thread t: token t / 96, granules 4 (t % 96) .. +4 of the group)
+  if (t < FF_ROWS * ct) {
+    const int c = t / FF_ROWS, r = t % FF_ROWS;
+    unsigned long long* gact = reinterpret_cast<unsigned long long*>(f.act) + (int64_t)(m0 + c) * f.F;
+    __hip_atomic_store(gact + FF_ROWS * b + r, ((unsigned long long)ep[c] << 32) | __float_as_uint(s_act[c][r]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   STAMP(2);
+  constexpr int QT = FF_GROUP_ROWS / 4;  // polling threads per token
+  const int pc = t / QT, pt = t % QT;
   f4v gv0 = {0.f, 0.f, 0.f, 0.f}, gv1 = gv0;
-  if (t < FF_GROUP_ROWS / 4) {
+  if (pc < ct) {
+    const unsigned e = pc == 0 ? ep[0] : ep[CT - 1];
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act + (int64_t)(m0 + pc) * 2 * f.F, f.F * 8);
     unsigned spins = 0;
-    const int off = (FF_GROUP_ROWS * grp + 4 * t) * 8;
+    const int off = (FF_GROUP_ROWS * grp + 4 * pt) * 8;
     for (;;) {
       gv0 = ld_sc1_f4(ra, off);
       gv1 = ld_sc1_f4(ra, off + 16);
-      if (__float_as_uint(gv0.y) == ep && __float_as_uint(gv0.w) == ep && __float_as_uint(gv1.y) == ep &&
-          __float_as_uint(gv1.w) == ep)
+      if (__float_as_uint(gv0.y) == e && __float_as_uint(gv0.w) == e && __float_as_uint(gv1.y) == e &&
+          __float_as_uint(gv1.w) == e)
         break;
       if (++spins > (1u << 22)) {
         __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3056,45 +3067,34 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f0) {
     }
   }
   STAMP(3);
-  // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
-  if (t < FF_GROUP_ROWS / 4) {
+  // ---- each token's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
+  if (pc < CT) {
     const f4v v = {gv0.x, gv0.z, gv1.x, gv1.z};
-#else
-  // ---- publish the block's 12 act rows (write-through), group fan-in
-  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act, f.F * 4);
-  if (t < FF_ROWS / 4) {
-    const f4v v = {s_act[4 * t], s_act[4 * t + 1], s_act[4 * t + 2], s_act[4 * t + 3]};
-    st_sc1_f4(v, ra, (FF_ROWS * b + 4 * t) * 4);
-  }
-  STAMP(2);
-  fanin_wait(f.cnt + grp * CNT_LINE, FF_GROUP_BLOCKS, f.err);
-  STAMP(3);
-  // ---- the group's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
-  if (t < FF_GROUP_ROWS / 4) {
-    const f4v v = ld_sc1_f4(ra, (FF_GROUP_ROWS * grp + 4 * t) * 4);
-#endif
     const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     const float d = am / 127.0f;
     const float id = d != 0.0f ? 1.0f / d : 0.0f;
     const int q0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, q1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
     const int q2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, q3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
-    *reinterpret_cast<int32_t*>(s_aq + 4 * t) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
-    if ((t & 7) == 0) s_ad[t >> 3] = __half2float(__float2half_rn(d));
+    *reinterpret_cast<int32_t*>(s_aq[pc] + 4 * pt) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
+    if ((pt & 7) == 0) s_ad[pc][pt >> 3] = __half2float(__float2half_rn(d));
   }
   __syncthreads();
   STAMP(4);
-  // ---- down slice: row drow over the group's 12 q8_0 blocks, 4 per load (8 lanes), loads summed in order
-  float v = 0.f;
+  // ---- down slice: row drow over the group's 12 q8_0 blocks, 4 per load (8 lanes), loads summed in order; per token
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    int si = dot16(dwv[i], *reinterpret_cast<const int4*>(s_aq + 16 * (8 * i + c8)), 0);
-    si += dpp_i<DPP_XOR1>(si);  // the block's two halves: exact integer block dot in both lanes of the pair
-    float u = (float)si * (dsv[i] * s_ad[4 * i + (c8 >> 1)]);
-    u += dpp_f<DPP_XOR2>(u);  // 4 blocks (pairs hold duplicates: no xor-1 step)
-    u += dpp_f<DPP_HALF_MIRROR>(u);
-    v += u;
+  for (int c = 0; c < CT; ++c) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      int si = dot16(dwv[i], *reinterpret_cast<const int4*>(s_aq[c] + 16 * (8 * i + c8)), 0);
+      si += dpp_i<DPP_XOR1>(si);  // the block's two halves: exact integer block dot in both lanes of the pair
+      float u = (float)si * (dsv[i] * s_ad[c][4 * i + (c8 >> 1)]);
+      u += dpp_f<DPP_XOR2>(u);  // 4 blocks (pairs hold duplicates: no xor-1 step)
+      u += dpp_f<DPP_HALF_MIRROR>(u);
+      v += u;
+    }
+    if (c8 == 0 && c < ct) f.dpart[((int64_t)(m0 + c) * FUSED_PARTS + grp) * f.E + drow] = v;
   }
-  if (c8 == 0) f.dpart[(int64_t)grp * f.E + drow] = v;
   STAMP(5);
 }
 
@@ -3118,6 +3118,8 @@ void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, 
   hipLaunchKernelGGL(k_psum_rows, dim3(cdiv(E / 4, 256), M), dim3(256), 0, s, xmid, dpart, E, out);
 }
 
+int g_ffn_pair_min_m = 4;  // decode batches from this width run the fused FFN with two tokens per block
+
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s, int M) {
@@ -3127,7 +3129,10 @@ void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq,
   FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
   FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart,
             fw.cnt + FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.err, E, F, fw.cnt};
-  hipLaunchKernelGGL(k_ffn_fused, dim3(F / FF_ROWS, M), dim3(256), 0, s, f);
+  if (M >= g_ffn_pair_min_m)
+    hipLaunchKernelGGL(k_ffn_fused<2>, dim3(F / FF_ROWS, cdiv(M, 2)), dim3(256), 0, s, f, M);
+  else
+    hipLaunchKernelGGL(k_ffn_fused<1>, dim3(F / FF_ROWS, M), dim3(256), 0, s, f, M);
 }
 
 }  // namespace fa
