@@ -19,7 +19,7 @@ from collections import defaultdict
 QKV, O, GU, DOWN = 4096 * 1024 * 34 / 32, 1024 * 2048 * 34 / 32, 2 * 3072 * 1024 * 34 / 32, 1024 * 3072 * 34 / 32
 ALGO = {
     "k_gemv_q8<1, 1, true, 0, true>": QKV,      # A: q|k|v (fused layer)
-    "k_ffn_fused(": GU + DOWN,                 # C: gate|up + down (fused layer)
+    "k_ffn_fused<": GU + DOWN,                 # C: gate|up + down (fused layer; <1> batch 1, <2> two tokens per block)
     "k_attn_o<true>": QKV + O,                 # AB: q|k|v rows + o projection slice weights (two-launch layer)
     "k_attn_o<false>": O,                      # B: o projection slice weights (three-launch layer)
     "k_gemv_q8<1, 1, true, 0, false>": QKV,     # 5-launch layer
@@ -31,7 +31,7 @@ ALGO = {
 }
 # the bench's dominant class "q8_0 GEMV/GEMM (decoder layers)" = the weight-streaming layer launches AB and C (or A
 # and C; B is the "decode attention" class): their mean is what roofline.traffic reports
-LAYER_CLASS = ("k_attn_o<true>", "k_gemv_q8<1, 1, true, 0, true>", "k_ffn_fused(", "k_gemv_q8<1, 1, true, 0, false>",
+LAYER_CLASS = ("k_attn_o<true>", "k_gemv_q8<1, 1, true, 0, true>", "k_ffn_fused<", "k_gemv_q8<1, 1, true, 0, false>",
                "k_gemv_q8<1, 1, true, 2, false>", "k_gemv_q8<2, 1, true, 1, false>", "k_gemv_q8<3, 1, true, 1, false>")
 
 
