@@ -111,10 +111,11 @@ int fa_set_encoder_fp16(fa_engine* e, int32_t on);
  * 0 = exact-f32 MFMA (v_mfma_f32_32x32x2_f32). Env FUNASR_ENC_GEMM=f32 selects 0 at engine creation. The split
  * weight copies are built on the next encode. No effect in fp16 mode. */
 int fa_set_encoder_gemm(fa_engine* e, int32_t mode);
-/* Batch-1 decode layer structure: 1 (default) = 2 launches per layer (q|k|v GEMV + attention + a split o
- * projection with in-launch group fan-ins; gate|up + a split down projection); 2 = 3 launches (the q|k|v GEMV as
- * its own launch; bit-identical to 1); 0 = the 5-launch layer every batch width uses. Same numerics contract
- * (ggml q8_0), different f32 summation order of the o / down projections between 0 and 1/2. */
+/* Decode layer structure: 1 (default) = 2 launches per layer (q|k|v GEMV + attention + a split o projection with
+ * in-launch group hand-offs; gate|up + a split down projection) for batch 1 and for decode batches up to
+ * FUNASR_FUSED_MAX_M (default 6) sequences; 2 = 3 launches at batch 1 (the q|k|v GEMV as its own launch;
+ * bit-identical to 1); 0 = the 5-launch layer (what wider batches always use). Same numerics contract (ggml q8_0),
+ * different f32 summation order of the o / down projections between 0 and 1/2. */
 int fa_set_decode_fused(fa_engine* e, int32_t on);
 int fa_set_debug(fa_engine* e, int32_t flags);
 int fa_encode_tap(fa_engine* e, int32_t which, float* out, int64_t n);
