@@ -573,3 +573,39 @@ def test_two_launch_layer_long_context():
         assert _cos(l1[k], l2[k]) > 0.99999
         ref = m.forward(m.embed_tokens([t1[k]]), prompt.shape[0] + k)
         _check_step(l1[k], ref)
+
+
+def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
+    """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
+    slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
+    exactly the tokens they give alone on the two-launch layer (per-token arithmetic is batch-independent up to 5 rows,
+    where the LM head is the fused GEMV for every width)."""
+    from fun_asr_gguf import _native
+    m = llm_tiny_oracle
+    eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=6), max_batch=1, max_samples=16000)
+    eng.synthetic_weights(0)
+    rng = np.random.default_rng(77)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, 5 + 7 * i)) for i in range(5)]
+    n_steps = 6
+    singles = []
+    for p in prompts:
+        eng.llm_reset(0)
+        t = eng.llm_prefill(0, p)
+        singles.append([t] + list(eng.llm_generate([0], n_steps)[0]))
+    got = {}
+    for q, p in enumerate(prompts):
+        eng.llm_reset(q)
+        got[q] = [eng.llm_prefill(q, p)]
+    schedule = [[0, 1, 2, 3, 4], [3, 1], [4, 0, 2], [2], [1, 4, 3, 0], [0, 2, 4, 1, 3], [3, 1], [4, 0, 2],
+                [1, 3, 0, 2, 4], [0], [3, 4, 1, 2], [4, 2], [1, 3, 0], [2, 4, 3, 1, 0]]
+    for seqs in schedule:
+        seqs = [q for q in seqs if len(got[q]) <= n_steps]
+        if not seqs:
+            continue
+        out = eng.llm_generate(seqs, 1)
+        for q, t in zip(seqs, out):
+            got[q].append(int(t[0]))
+    eng.close()
+    for q in range(5):
+        assert len(got[q]) == n_steps + 1, (q, len(got[q]))
+        assert got[q] == singles[q], q
