@@ -1155,6 +1155,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
     fa::g_ffn_pair_min_m = 4;
+    fa::g_gemm_bf3_pf = 2;
+    if (const char* g = getenv("FUNASR_BF3_PF")) fa::g_gemm_bf3_pf = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation

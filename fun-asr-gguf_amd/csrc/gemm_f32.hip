@@ -586,6 +586,7 @@ static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N,
 // the f16 kernel's, so the same epilogues apply.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ahead (1 or 2; FUNASR_BF3_PF)
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves
 
 template <int WM, int WN, int KB>
@@ -649,7 +650,10 @@ __device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<W
 // KW = 2 (few-tile shapes): two groups of 4 waves per block split K in halves, each with its own LDS stages; group 1
 // hands its accumulators to group 0 through LDS (fixed order) and group 0 runs the epilogue. Twice the waves per CU
 // and half the dependent k-steps per wave, with no cross-block split-K seam.
-template <class AL, class EPI, int WM, int WN, int KB, int KW = 1>
+// PF = 2: the global loads run two k-steps ahead (two register sets, the k loop unrolled by two), so a k-step's
+// tile has two steps of compute to land instead of one: few-tile shapes (one clip) have too little work per step to
+// cover the load latency.
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1>
 __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
                                                        int64_t ldw, int M, int N, int K, EPI epi) {
   using T = TileB3<WM, WN, KB>;
@@ -675,11 +679,9 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
   store_b3<WM, WN, KB>(sh, ra, rh, rl, t);
   __syncthreads();
   const int nk = (kq + KB - 1) / KB;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
-    const __bf16* a = sh + cur * T::STAGE + (wr * 32 * WM + r) * LDK + 8 * h;
-    const __bf16* b = sh + cur * T::STAGE + 2 * T::PA + (wc * 32 * WN + r) * LDK + 8 * h;
+  auto compute = [&](const __bf16* stage) {
+    const __bf16* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
+    const __bf16* b = stage + 2 * T::PA + (wc * 32 * WN + r) * LDK + 8 * h;
 #pragma unroll
     for (int kk = 0; kk < KB / 16; ++kk) {
       bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
@@ -702,8 +704,33 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
-    __syncthreads();
+  };
+  if constexpr (PF == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
+      compute(sh + cur * T::STAGE);
+      if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
+      __syncthreads();
+    }
+  } else {
+    // set A (ra, rh, rl) carries the odd k-steps, set B the even ones from step 2 on; step j is loaded right after
+    // step j - 2's set was stored, i.e. two compute steps before it is stored itself
+    float4 rb[T::NA];
+    uint4 rhb[T::NB], rlb[T::NB];
+    if (nk > 1) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rh, rl, t);
+    if (nk > 2) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + 2 * KB, M, N, ke, rb, rhb, rlb, t);
+    for (int kt = 0; kt < nk; kt += 2) {
+      compute(sh);  // step kt (stage 0)
+      if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + T::STAGE, ra, rh, rl, t);
+      if (kt + 3 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 3) * KB, M, N, ke, ra, rh, rl, t);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      compute(sh + T::STAGE);  // step kt + 1 (stage 1)
+      if (kt + 2 < nk) store_b3<WM, WN, KB>(sh, rb, rhb, rlb, t);
+      if (kt + 4 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 4) * KB, M, N, ke, rb, rhb, rlb, t);
+      __syncthreads();
+    }
   }
   if constexpr (KW > 1) {
     float* xs = smem;  // [wave][i][j][16][64]: group 1's accumulators
@@ -736,7 +763,7 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
 // No K splits: the bf16x3 body is fast enough that the split-K seam (publish + ticket + combine, 5-13 us:
 // MI355X_MICROARCH.md splitk-seam) costs more than it saves (one clip, measured: out N 512 K 512 10.8 -> 19.8 us,
 // ffn2 N 512 K 2048 32.6 -> 57 us with 2-4 splits).
-template <class AL, class EPI, int WM, int WN, int KB, int KW = 1>
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1>
 static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                            hipStream_t s) {
   using T = TileB3<WM, WN, KB>;
@@ -746,11 +773,11 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
   const size_t lds = std::max<size_t>(KW * 2 * T::STAGE * 2, 1024);  // >= EpiArgmax scratch
   static bool attr = false;
   if (!attr && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW>), grid, dim3(256 * KW), lds, s, al,
+  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF>), grid, dim3(256 * KW), lds, s, al,
                      reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
@@ -770,10 +797,14 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   const int f = g_gemm_bf3_force;
   const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
   const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64);
+  const bool pf = g_gemm_bf3_pf > 1;
   if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
   else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32>(al, w, ldw, M, N, K, epi, s);
-  else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) launch_gemm_b3<AL, EPI, 1, 1, 64, 2>(al, w, ldw, M, N, K, epi, s);
-  else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
+    if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2>(al, w, ldw, M, N, K, epi, s);
+    else launch_gemm_b3<AL, EPI, 1, 1, 64, 2>(al, w, ldw, M, N, K, epi, s);
+  } else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2>(al, w, ldw, M, N, K, epi, s);
+  else if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 2>(al, w, ldw, M, N, K, epi, s);
   else launch_gemm_b3<AL, EPI, 1, 1, 64>(al, w, ldw, M, N, K, epi, s);
 }
 

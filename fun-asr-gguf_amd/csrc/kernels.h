@@ -168,6 +168,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s, int M = 1);
+extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
 extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 4)
 // out[m] = xmid[m] + sum_p dpart[m][p] for m < M (a small batch's residual rows after its last fused layer)
 void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);
