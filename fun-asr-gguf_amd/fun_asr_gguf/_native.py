@@ -133,6 +133,7 @@ class Engine:
         self.max_batch = max_batch
         self.max_samples = max_samples
         self.lib = lib
+        self.weights_gen = 0  # bumped by every weight change (host-side caches of weight-derived rows key on it)
 
     def close(self):
         if getattr(self, "h", None):
@@ -162,14 +163,17 @@ class Engine:
 
     def synthetic_weights(self, seed=0):
         _check(self.lib.fa_weights_synthetic(self.h, seed), "fa_weights_synthetic")
+        self.weights_gen += 1
 
     def set_tensor(self, name, arr):
         a = np.ascontiguousarray(arr, dtype=np.float32)
         _check(self.lib.fa_set_tensor_f32(self.h, name.encode(), _ptr(a), a.size), f"fa_set_tensor_f32({name})")
+        self.weights_gen += 1
 
     def set_tensor_q8_0(self, name, blocks):
         b = np.ascontiguousarray(blocks, dtype=np.uint8)
         _check(self.lib.fa_set_tensor_q8_0(self.h, name.encode(), _ptr(b), b.size), f"fa_set_tensor_q8_0({name})")
+        self.weights_gen += 1
 
     def get_tensor_q8_0(self, name, n_elements):
         out = np.empty(n_elements // 32 * 34, np.uint8)
@@ -183,6 +187,7 @@ class Engine:
 
     def load_gguf(self, path):
         _check(self.lib.fa_load_gguf(self.h, os.fspath(path).encode()), "fa_load_gguf")
+        self.weights_gen += 1
 
     # ---- encoder
     @staticmethod

@@ -29,6 +29,9 @@ class PromptBuilder:
         self.vocab = vocab
         self.engine = engine
         self.fixed_ids = None  # benchmark protocol: (prefix_ids, suffix_ids) pinned when no tokenizer exists
+        # embedding rows of recent prompts (a batch's streams usually share one prompt): keyed by the token ids and
+        # the engine's weight generation, so a weight change never serves stale rows
+        self._embd_cache = {}
 
     def build_ids(self, hotwords=None, language=None, context=None):
         p, s = prompt_texts(hotwords, language, context)
@@ -39,6 +42,13 @@ class PromptBuilder:
     def build_prompt(self, hotwords=None, language=None, context=None):
         """-> (prefix_embd, suffix_embd, n_prefix, n_suffix, prefix_text), like the reference."""
         pi, si, p = self.build_ids(hotwords, language, context)
-        pe = self.engine.embd_rows(np.array(pi, np.int32), fp16_round=True) if pi else np.zeros((0, 1024), np.float32)
-        se = self.engine.embd_rows(np.array(si, np.int32), fp16_round=True) if si else np.zeros((0, 1024), np.float32)
+        key = (getattr(self.engine, "weights_gen", None), tuple(pi), tuple(si))
+        hit = self._embd_cache.get(key)
+        if hit is None:
+            pe = self.engine.embd_rows(np.array(pi, np.int32), fp16_round=True) if pi else np.zeros((0, 1024), np.float32)
+            se = self.engine.embd_rows(np.array(si, np.int32), fp16_round=True) if si else np.zeros((0, 1024), np.float32)
+            if len(self._embd_cache) >= 64:
+                self._embd_cache.clear()
+            hit = self._embd_cache[key] = (pe, se)
+        pe, se = hit
         return pe, se, len(pi), len(si), p
