@@ -1148,7 +1148,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     // tokens per fused-GEMV block (1 or 2: the instantiated and tested variants)
     {  // process-wide decode-path knob: re-read (or reset to the default 5) at every engine creation
       const char* g = getenv("FUNASR_GEMV_SMALL");
-      fa::g_gemv_small_max = g ? std::min(7, std::max(0, atoi(g))) : 5;
+      fa::g_gemv_small_max = g ? std::min(7, std::max(0, atoi(g))) : 6;
     }
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
@@ -1251,6 +1251,31 @@ int fa_get_tensor_f32(fa_engine* h, const char* name, float* out, int64_t n) {
   FA_REQUIRE(s.kind == 0 && n == s.n, "fa_get_tensor_f32: size/kind");
   FA_HIP(hipMemcpyAsync(out, s.f, n * 4, hipMemcpyDeviceToHost, e->stream));
   FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_weights_mark_unset(fa_engine* h, const char* prefix) {
+  FA_API_BEGIN
+  const std::string p = prefix ? prefix : "";
+  for (auto& kv : h->e->slots)
+    if (kv.first.compare(0, p.size(), p) == 0) kv.second.set = false;
+  FA_API_END
+}
+
+int fa_tensor_names(fa_engine* h, const char* prefix, int32_t only_unset, char* buf, int64_t cap, int64_t* needed) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  const std::string p = prefix ? prefix : "";
+  std::string out;
+  for (const std::string& name : e->spec_order) {
+    if (name.compare(0, p.size(), p) != 0) continue;
+    if (only_unset && e->slots[name].set) continue;
+    if (!out.empty()) out += '\n';
+    out += name;
+  }
+  if (needed) *needed = (int64_t)out.size() + 1;
+  FA_REQUIRE(buf == nullptr || cap >= (int64_t)out.size() + 1, "fa_tensor_names: buffer too small");
+  if (buf) memcpy(buf, out.c_str(), out.size() + 1);
   FA_API_END
 }
 
@@ -1608,6 +1633,29 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
   const int rc = fa_llm_generate_begin(h, seqs, n_seqs, n_steps, s);
   if (rc != FA_OK) return rc;
   return fa_llm_generate_end(h, tokens_out);
+}
+
+int fa_llm_invariant_width(fa_engine* h, int32_t* out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  // the two-launch layer gives every token of a batch of up to fused_max_m its own grid slab with the batch-1
+  // arithmetic, and the LM head is the fused GEMV up to g_gemv_small_max tokens (the MFMA LM head above sums in
+  // another f32 order); every other decode path is only known to be invariant at width 1
+  int w = 1;
+  if (e->use_fused == 1 && e->fused_shape_ok()) w = std::max(1, std::min(e->fused_max_m, fa::g_gemv_small_max));
+  *out = w;
+  FA_API_END
+}
+
+int fa_llm_set_token(fa_engine* h, int32_t seq, int32_t token) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
+  FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
+  FA_REQUIRE(e->n_past[seq] > 0, "fa_llm_set_token: prefill the sequence first");
+  FA_REQUIRE(token >= 0 && token < e->lc.n_vocab, "fa_llm_set_token: token out of range");
+  e->last_tok[seq] = token;
+  FA_API_END
 }
 
 int fa_llm_logits(fa_engine* h, int32_t seq, float* out) {

@@ -20,6 +20,8 @@ EXPORTS = [
     "fa_profile_read", "fa_synchronize", "fa_align_timestamps", "fa_pcm_upload", "fa_set_encoder_fp16",
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
+    "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
+    "fa_llm_invariant_width",
 ]
 
 
@@ -66,6 +68,8 @@ def load():
     lib.fa_set_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_get_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_get_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_weights_mark_unset.argtypes = [P, ctypes.c_char_p]
+    lib.fa_tensor_names.argtypes = [P, ctypes.c_char_p, I32, P, I64, ctypes.POINTER(I64)]
     lib.fa_load_gguf.argtypes = [P, ctypes.c_char_p]
     lib.fa_encode.argtypes = [P, P, P, I32, I64, P, I64, P, I64, P, P, P]
     lib.fa_encode_device.argtypes = [P, P, P, I32, I64]
@@ -84,6 +88,8 @@ def load():
     lib.fa_llm_generate_end.argtypes = [P, P]
     lib.fa_llm_prefill_batch.argtypes = [P, P, I32, P, P, ctypes.POINTER(Sampling), P]
     lib.fa_llm_logits.argtypes = [P, I32, P]
+    lib.fa_llm_set_token.argtypes = [P, I32, I32]
+    lib.fa_llm_invariant_width.argtypes = [P, ctypes.c_void_p]
     lib.fa_llm_n_past.argtypes = [P, I32, P]
     lib.fa_profile_enable.argtypes = [P, I32]
     lib.fa_profile_read.argtypes = [P, I32, P, P, P, P]
@@ -184,6 +190,22 @@ class Engine:
         out = np.empty(n_elements, np.float32)
         _check(self.lib.fa_get_tensor_f32(self.h, name.encode(), _ptr(out), out.size), "fa_get_tensor_f32")
         return out
+
+    def mark_unset(self, prefix=""):
+        """Clear the loaded mark of every tensor under `prefix` (fa_weights_mark_unset)."""
+        _check(self.lib.fa_weights_mark_unset(self.h, prefix.encode()), "fa_weights_mark_unset")
+
+    def tensor_names(self, prefix="", only_unset=False):
+        """Engine tensor names under `prefix` in registration order; only those not loaded since the last
+        mark_unset() when only_unset (fa_tensor_names)."""
+        need = ctypes.c_int64()
+        _check(self.lib.fa_tensor_names(self.h, prefix.encode(), int(only_unset), None, 0, ctypes.byref(need)),
+               "fa_tensor_names")
+        buf = ctypes.create_string_buffer(need.value)
+        _check(self.lib.fa_tensor_names(self.h, prefix.encode(), int(only_unset), buf, need.value, ctypes.byref(need)),
+               "fa_tensor_names")
+        s = buf.value.decode()
+        return s.split("\n") if s else []
 
     def load_gguf(self, path):
         _check(self.lib.fa_load_gguf(self.h, os.fspath(path).encode()), "fa_load_gguf")
@@ -317,6 +339,16 @@ class Engine:
         out = np.empty(self._gen_shape, np.int32)
         _check(self.lib.fa_llm_generate_end(self.h, _ptr(out)), "fa_llm_generate_end")
         return out
+
+    def llm_invariant_width(self):
+        """Largest decode batch width with single-sequence arithmetic per token (fa_llm_invariant_width)."""
+        v = ctypes.c_int32()
+        _check(self.lib.fa_llm_invariant_width(self.h, ctypes.byref(v)), "fa_llm_invariant_width")
+        return v.value
+
+    def llm_set_token(self, seq, token):
+        """Feed `token` as the sequence's next generate input instead of its own last draw (teacher forcing)."""
+        _check(self.lib.fa_llm_set_token(self.h, seq, int(token)), "fa_llm_set_token")
 
     def llm_logits(self, seq=0):
         """Logits of `seq`'s row in the most recent forward (prefill or generate step) that included it."""

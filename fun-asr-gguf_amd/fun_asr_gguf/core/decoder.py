@@ -83,6 +83,22 @@ class _SeqState:
         return 0 if self.done else self.n_predict - self.sampled
 
 
+def invariant_width(eng):
+    """Largest decode batch width whose tokens equal decoding each sequence alone (fa_llm_invariant_width)."""
+    f = getattr(eng, "llm_invariant_width", None)
+    return f() if f is not None else 1
+
+
+def prefill_group(eng, seqs, embds, samp):
+    """Prefill `embds` into slots `seqs` -> first tokens. One prompt: llama_decode of its batch. Several: within the
+    engine's invariant width each prompt is prefilled alone (so every sequence gets exactly its single-sequence
+    tokens, as the reference decodes every segment alone, core/decoder.py:70-123); wider groups share forwards
+    (one weight pass per forward, fa_llm_prefill_batch; agreement to the q8_0 noise floor)."""
+    if len(embds) == 1 or len(embds) <= invariant_width(eng):
+        return [eng.llm_prefill(q, e, **samp) for q, e in zip(seqs, embds)]
+    return eng.llm_prefill_batch(list(seqs), embds, **samp)
+
+
 class LLMDecoder:
     def __init__(self, models):
         self.models = models
@@ -100,14 +116,13 @@ class LLMDecoder:
         t0 = time.perf_counter()
         for s in range(len(embds)):
             eng.llm_reset(s)
-        # one prompt: llama_decode of its batch; several: their prompts share forwards (one weight pass per forward)
-        firsts = [eng.llm_prefill(0, embds[0], **samp)] if len(embds) == 1 else \
-            eng.llm_prefill_batch(list(range(len(embds))), embds, **samp)
+        firsts = prefill_group(eng, list(range(len(embds))), embds, samp)
         t_inject = (time.perf_counter() - t0) / len(embds)
         for s, first in enumerate(firsts):
             r = LLMDecodeResult()
             r.t_inject = t_inject
-            st = _SeqState(self.models.vocab, n_predict, self.models.eos_token, cfg.ignore_eos,
+            n_p = n_predict[s] if isinstance(n_predict, (list, tuple)) else n_predict
+            st = _SeqState(self.models.vocab, n_p, self.models.eos_token, cfg.ignore_eos,
                            reporter if stream_output and len(embds) == 1 else None)
             st.feed([first])
             states.append(st)
@@ -116,31 +131,44 @@ class LLMDecoder:
         stop_ids = np.array(sorted({self.models.eos_token} | set(STOP_TOKENS)), np.int64)
         active = [s for s, st in enumerate(states) if not st.done]
         chunk = min(GEN_CHUNK, max(states[s].remaining() for s in active)) if active else 0
-        if active:
-            eng.llm_generate_begin(active, chunk, **samp)
-        while active:
-            toks = eng.llm_generate_end()
-            # the sequences this chunk leaves unfinished, from the token ids alone (stop ids, n_predict), go into the
-            # next chunk, which is enqueued BEFORE the host detokenises this one (the host work overlaps the GPU's);
-            # a sequence the repetition breaker cuts during feed() rides along one chunk and its tokens are ignored
-            nxt, left_after = [], []
-            for row, s in enumerate(active):
-                st = states[s]
-                left = st.remaining()
-                if left <= 0:
-                    continue
-                used = toks[row][:min(chunk, left)]
-                if not st.ignore_eos and np.isin(used, stop_ids).any():
-                    continue
-                if left > chunk:
-                    nxt.append(s)
-                    left_after.append(left - chunk)
-            nchunk = min(GEN_CHUNK, max(left_after)) if nxt else 0
-            if nxt:
-                eng.llm_generate_begin(nxt, nchunk, **samp)
-            for row, s in enumerate(active):
-                states[s].feed(toks[row])
-            active, chunk = nxt, nchunk
+        in_flight = False
+        try:
+            if active:
+                eng.llm_generate_begin(active, chunk, **samp)
+                in_flight = True
+            while active:
+                toks = eng.llm_generate_end()
+                in_flight = False
+                # the sequences this chunk leaves unfinished, from the token ids alone (stop ids, n_predict), go into
+                # the next chunk, which is enqueued BEFORE the host detokenises this one (the host work overlaps the
+                # GPU's); a sequence the repetition breaker cuts during feed() rides along one chunk, tokens ignored
+                nxt, left_after = [], []
+                for row, s in enumerate(active):
+                    st = states[s]
+                    left = st.remaining()
+                    if left <= 0:
+                        continue
+                    used = toks[row][:min(chunk, left)]
+                    if not st.ignore_eos and np.isin(used, stop_ids).any():
+                        continue
+                    if left > chunk:
+                        nxt.append(s)
+                        left_after.append(left - chunk)
+                nchunk = min(GEN_CHUNK, max(left_after)) if nxt else 0
+                if nxt:
+                    eng.llm_generate_begin(nxt, nchunk, **samp)
+                    in_flight = True
+                for row, s in enumerate(active):
+                    states[s].feed(toks[row])
+                active, chunk = nxt, nchunk
+        finally:
+            # host code between begin and end (detokenising, the reporter) may raise: land the chunk in flight so
+            # the engine is not left refusing every later call with "a generate call is in flight"
+            if in_flight:
+                try:
+                    eng.llm_generate_end()
+                except Exception:
+                    pass
         dt = time.perf_counter() - t_gen
         for st, r in zip(states, res):
             st.ps.flush()
@@ -164,7 +192,8 @@ class LLMDecoder:
         final = [None] * B
         pending = list(range(B))
         for attempt in range(attempts):
-            rs = self.decode_many([embds[b] for b in pending], n_predict, temps[pending[0]], top_p, top_k, reporter,
+            n_p = [n_predict[b] for b in pending] if isinstance(n_predict, (list, tuple)) else n_predict
+            rs = self.decode_many([embds[b] for b in pending], n_p, temps[pending[0]], top_p, top_k, reporter,
                                   stream_output)
             nxt = []
             for b, r in zip(pending, rs):
@@ -190,9 +219,10 @@ class StreamDecoder:
                       temperature=0.3, top_p=1.0, top_k=50) -> DecodeResult:
         return self.decode_streams([stream], language, context, verbose, reporter, temperature, top_p, top_k)[0]
 
-    def decode_streams(self, streams: List[RecognitionStream], language=None, context=None, verbose=True,
-                       reporter=None, temperature=0.3, top_p=1.0, top_k=50, resident=None) -> List[DecodeResult]:
-        """resident: handle from engine.upload() holding these streams' PCM in HBM (benchmark path)."""
+    def front(self, streams: List[RecognitionStream], language=None, context=None, resident=None):
+        """Steps 1-3 for a group of streams: encode (+ CTC head / argmax) as one device batch, CTC collapse + host
+        token map + hotwords, prompt rows. -> list of dicts (embd, ctc_results, hotwords, n_p, n_s, audio_embd,
+        timings)."""
         m = self.models
         eng = m.engine
         B = len(streams)
@@ -218,30 +248,40 @@ class StreamDecoder:
             tm.ctc = tm.ctc_decode = dt / B
         # 3. prompt
         t = time.perf_counter()
-        embds, n_ps = [], []
+        jobs = []
         for b in range(B):
             pe, se, n_p, n_s, _ = m.prompt_builder.build_prompt(hotwords[b], language, context)
-            embds.append(np.concatenate([pe, out["audio_embd"][b].astype(np.float32), se], 0))
-            n_ps.append((n_p, n_s))
+            jobs.append(dict(embd=np.concatenate([pe, out["audio_embd"][b].astype(np.float32), se], 0),
+                             ctc_results=ctc_results[b], hotwords=hotwords[b], n_p=n_p, n_s=n_s,
+                             audio_embd=out["audio_embd"][b], timings=timings[b]))
         dt = time.perf_counter() - t
         for tm in timings:
             tm.prepare = dt / B
+        return jobs
+
+    @staticmethod
+    def back(stream, job, r):
+        """Step 5 for one stream: alignment of the LLM text to the CTC tokens -> DecodeResult."""
+        text = r.text.strip()
+        tm = job["timings"]
+        tm.inject, tm.llm_generate = r.t_inject, r.t_gen
+        t = time.perf_counter()
+        aligned = align_timestamps(job["ctc_results"], text) if job["ctc_results"] else None
+        tm.align = time.perf_counter() - t
+        toks = [a["char"] for a in aligned] if aligned else []
+        ts = [a["start"] for a in aligned] if aligned else []
+        if stream is not None:
+            stream.set_result(text=text, timestamps=ts, tokens=toks)
+        return DecodeResult(text=text, ctc_results=job["ctc_results"], aligned=aligned, audio_embd=job["audio_embd"],
+                            n_prefix=job["n_p"], n_suffix=job["n_s"], n_gen=r.n_gen, timings=tm,
+                            hotwords=job["hotwords"], is_aborted=r.is_aborted)
+
+    def decode_streams(self, streams: List[RecognitionStream], language=None, context=None, verbose=True,
+                       reporter=None, temperature=0.3, top_p=1.0, top_k=50, resident=None) -> List[DecodeResult]:
+        """One group of streams: encode batch, then all sequences decode together (no admission).
+        resident: handle from engine.upload() holding these streams' PCM in HBM (benchmark path)."""
+        jobs = self.front(streams, language, context, resident)
         # 4. LLM with the reference's retry policy (decoder.py:201-211), per sequence
-        final = self.llm_decoder.decode_with_retry(embds, m.config.n_predict, temperature, top_p, top_k, reporter,
-                                                   verbose)
-        results = []
-        for b in range(B):
-            r = final[b]
-            text = r.text.strip()
-            tm = timings[b]
-            tm.inject, tm.llm_generate = r.t_inject, r.t_gen
-            t = time.perf_counter()
-            aligned = align_timestamps(ctc_results[b], text) if ctc_results[b] else None
-            tm.align = time.perf_counter() - t
-            toks = [a["char"] for a in aligned] if aligned else []
-            ts = [a["start"] for a in aligned] if aligned else []
-            streams[b].set_result(text=text, timestamps=ts, tokens=toks)
-            results.append(DecodeResult(text=text, ctc_results=ctc_results[b], aligned=aligned,
-                                        audio_embd=out["audio_embd"][b], n_prefix=n_ps[b][0], n_suffix=n_ps[b][1],
-                                        n_gen=r.n_gen, timings=tm, hotwords=hotwords[b], is_aborted=r.is_aborted))
-        return results
+        final = self.llm_decoder.decode_with_retry([j["embd"] for j in jobs], self.models.config.n_predict,
+                                                   temperature, top_p, top_k, reporter, verbose)
+        return [self.back(st, j, r) for st, j, r in zip(streams, jobs, final)]

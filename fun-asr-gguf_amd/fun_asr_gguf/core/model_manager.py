@@ -1,13 +1,15 @@
 """Engine initialisation (ModelManager.initialize, /root/reference/fun_asr_gguf/core/model_manager.py:36-100).
 
 Creates the device-bound native engine and fills its weights:
-  * "synthetic" (or a missing path) -> the repo's deterministic synthetic weights (oracle/synth.py spec);
+  * "synthetic" -> the repo's deterministic synthetic weights (oracle/synth.py spec);
   * encoder/CTC: the reference's ONNX files (fun_asr_gguf.onnx_weights: initializers of
     Fun-ASR-Nano-Encoder-Adaptor.*.onnx and Fun-ASR-Nano-CTC.*.onnx), or a PyTorch/safetensors state dict
     (model.pt keys audio_encoder.*, audio_adaptor.*, ctc_decoder.*, ctc.ctc_lo.* -> ctc_proj.ctc_lo.*, as
     HybridSenseVoice.load_weights, model_definition.py:231-238), loaded with weights_only=True;
   * decoder: a GGUF file (q8_0/f16/f32 tensors + tokenizer metadata) through fa_load_gguf.
-Any failure returns False (the reference swallows init exceptions the same way, :98-100).
+Any failure returns False (the reference swallows init exceptions the same way, :98-100): a model path that does
+not exist, and a model file that leaves any tensor of its part of the graph unfilled (the engine keeps a per-tensor
+loaded mark: fa_weights_mark_unset / fa_tensor_names), are failures, never a silent synthetic fallback.
 """
 import logging
 import os
@@ -26,7 +28,14 @@ def _is_synthetic(p):
     return p is None or str(p).startswith("synthetic")
 
 
-def load_encoder_state_dict(engine, path):
+ENCODER_GROUPS = ("audio_encoder.", "audio_adaptor.")
+CTC_GROUPS = ("ctc_decoder.", "ctc_proj.")
+LLM_GROUPS = ("token_embd.", "blk.", "output_norm.")
+
+
+def state_dict_file(path):
+    """model.pt / safetensors -> {engine tensor name: f32 array} for the encoder, adaptor and CTC parts
+    (HybridSenseVoice state_dict keys; ctc.ctc_lo.* -> ctc_proj.ctc_lo.*). torch.load with weights_only=True."""
     if str(path).endswith(".safetensors"):
         from safetensors.numpy import load_file
         sd = load_file(path)
@@ -36,28 +45,33 @@ def load_encoder_state_dict(engine, path):
         if "state_dict" in sd:
             sd = sd["state_dict"]
         sd = {k: v.float().numpy() for k, v in sd.items() if hasattr(v, "float")}
-    n = 0
+    out = {}
     for k, v in sd.items():
-        if k.startswith(("audio_encoder.", "audio_adaptor.", "ctc_decoder.")):
-            name = k
+        if k.startswith(ENCODER_GROUPS + ("ctc_decoder.",)):
+            out[k] = v
         elif k.startswith("ctc.ctc_lo."):
-            name = k.replace("ctc.ctc_lo", "ctc_proj.ctc_lo")
-        else:
-            continue
-        engine.set_tensor(name, v)
-        n += 1
-    return n
+            out[k.replace("ctc.ctc_lo", "ctc_proj.ctc_lo")] = v
+    if not out:
+        raise ValueError(f"{path}: no encoder / adaptor / CTC tensors found")
+    return out
 
 
-def load_encoder_onnx(engine, path):
-    """Initializers of an encoder-adaptor or CTC ONNX file (onnx_weights.state_dict_from_onnx) -> engine tensors."""
+def onnx_state_dict(path):
+    """Initializers of an encoder-adaptor or CTC ONNX file (onnx_weights.state_dict_from_onnx)."""
     from ..onnx_weights import state_dict_from_onnx
     sd = state_dict_from_onnx(path)
     if not sd:
         raise ValueError(f"{path}: no encoder / adaptor / CTC initializers found")
-    for k, v in sd.items():
-        engine.set_tensor(k, v)
-    return len(sd)
+    return sd
+
+
+def require_loaded(engine, prefix, path):
+    """Raise naming the tensors under `prefix` that the model file at `path` left unfilled."""
+    missing = engine.tensor_names(prefix, only_unset=True)
+    if missing:
+        shown = ", ".join(missing[:8]) + (f", ... ({len(missing)} in all)" if len(missing) > 8 else "")
+        log.error("%s does not fill %d %s* tensors: %s", path, len(missing), prefix, shown)
+        raise ValueError(f"{path}: model file does not hold {len(missing)} tensor(s) under '{prefix}': {shown}")
 
 
 class ModelManager:
@@ -80,6 +94,10 @@ class ModelManager:
         try:
             t0 = time.perf_counter()
             c = self.config
+            for role, p in (("encoder", c.encoder_onnx_path), ("ctc", getattr(c, "ctc_onnx_path", None)),
+                            ("decoder", c.decoder_gguf_path), ("tokens", c.tokens_path)):
+                if not _is_synthetic(p) and not os.path.exists(str(p)):
+                    raise FileNotFoundError(f"{role} model file not found: {p}")
             enc_cfg, llm_cfg = MODELS[c.model]
             self.enc_cfg = dict(enc_cfg)
             self.llm_cfg = dict(llm_cfg, n_ctx=c.n_ctx, max_seqs=max(1, c.max_batch))
@@ -94,24 +112,41 @@ class ModelManager:
             self.engine.synthetic_weights(c.synthetic_seed)
             self.engine.set_encoder_fp16(c.encoder_fp16())
             # encoder/adaptor + CTC weights: the reference's ONNX files (initializers read without `onnx`), or a
-            # model.pt / safetensors state dict (HybridSenseVoice.load_weights, model_definition.py:231-238)
-            for p in (c.encoder_onnx_path, getattr(c, "ctc_onnx_path", None)):
-                if _is_synthetic(p) or not os.path.exists(str(p)):
+            # model.pt / safetensors state dict (HybridSenseVoice.load_weights, model_definition.py:231-238).
+            # Fail loudly like the reference (a missing file makes the ORT session raise, model_manager.py:98-100):
+            # a path that does not exist, or a file that leaves any tensor of its part of the graph unfilled.
+            expect = []
+            for role, p in (("encoder", c.encoder_onnx_path), ("ctc", getattr(c, "ctc_onnx_path", None))):
+                if _is_synthetic(p):
                     continue
+                groups = ENCODER_GROUPS if role == "encoder" else CTC_GROUPS
                 if str(p).endswith(".onnx"):
-                    load_encoder_onnx(self.engine, p)
+                    sd = onnx_state_dict(p)
                 else:
-                    load_encoder_state_dict(self.engine, p)
+                    sd = state_dict_file(p)
+                if role == "encoder" and any(k.startswith(CTC_GROUPS) for k in sd):
+                    groups = groups + CTC_GROUPS  # one model.pt holds the whole HybridSenseVoice
+                for g in groups:
+                    self.engine.mark_unset(g)
+                for k, v in sd.items():
+                    self.engine.set_tensor(k, v)
+                expect += [(g, p) for g in groups]
+            for g, p in expect:
+                require_loaded(self.engine, g, p)
             if gguf_kv is not None:
+                for g in LLM_GROUPS:
+                    self.engine.mark_unset(g)
                 self.engine.load_gguf(c.decoder_gguf_path)
+                for g in LLM_GROUPS:
+                    require_loaded(self.engine, g, c.decoder_gguf_path)
                 self.vocab = GGUFVocab(c.decoder_gguf_path)
             else:
                 self.vocab = SyntheticVocab(self.llm_cfg["n_vocab"])
             self.eos_token = self.vocab.eos
-            if _is_synthetic(c.tokens_path) or not os.path.exists(c.tokens_path):
+            if _is_synthetic(c.tokens_path):
                 self.ctc_id2token = CTCSyntheticTokens(self.enc_cfg["ctc_vocab"])
             else:
-                self.ctc_id2token = load_ctc_tokens(c.tokens_path)
+                self.ctc_id2token = load_ctc_tokens(c.tokens_path)  # raises on a missing file (nano_ctc.py:12-36)
             self.prompt_builder = PromptBuilder(self.vocab, self.engine)
             if c.hotwords_path and os.path.exists(c.hotwords_path):
                 # phoneme hotword retrieval (hotword/manager.py + hot_phoneme.py), reloaded when hot.txt changes
@@ -124,6 +159,9 @@ class ModelManager:
             return True
         except Exception as e:  # same contract as the reference: report and return False
             log.exception("initialize failed")
+            if self.engine is not None:  # a half-initialised engine would hold its HBM until process exit
+                self.engine.close()
+                self.engine = None
             if verbose:
                 print(f"✗ 初始化失败: {e}")
             return False

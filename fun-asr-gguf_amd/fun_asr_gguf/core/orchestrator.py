@@ -2,8 +2,8 @@
 /root/reference/fun_asr_gguf/core/orchestrator.py:20-189).
 
 Long audio is cut into [t, t+segment) windows with step segment-overlap (:123-136). The reference decodes
-them one after another; here all segments of one file go through StreamDecoder.decode_streams as one
-device batch (up to max_batch), or are sharded across ranks by fun_asr_gguf.parallel. Results are merged
+them one after another; here the segments of one file decode together on the engine's sequence slots with continuous
+batching (core/scheduler.py), or are sharded across ranks by fun_asr_gguf.parallel. Results are merged
 with the same difflib rule (text_merge.py). timings.total excludes audio loading (:62, :72).
 """
 import os
@@ -78,20 +78,15 @@ class TranscriptionOrchestrator:
         if d.ctc_results:
             result.ctc_text = "".join(r.text for r in d.ctc_results)
 
-    def decode_segments(self, chunks, language, context, verbose, temperature, top_p, top_k):
-        """Decode a list of PCM chunks in device batches of max_batch; -> [DecodeResult]."""
-        sr = self.models.config.sample_rate
-        mb = max(1, self.models.config.max_batch)
-        out = []
-        for i in range(0, len(chunks), mb):
-            streams = []
-            for c in chunks[i:i + mb]:
-                s = RecognitionStream()
-                s.accept_waveform(sr, c)
-                streams.append(s)
-            out.extend(self.decoder.decode_streams(streams, language, context, verbose, None, temperature, top_p,
-                                                   top_k))
-        return out
+    def decode_segments(self, chunks, language, context, verbose, temperature, top_p, top_k, n_predicts=None):
+        """Decode a list of PCM chunks with continuous batching over the engine's max_batch sequence slots
+        (core/scheduler.py: a finished sequence's slot is refilled with the next waiting chunk); -> [DecodeResult]
+        in input order."""
+        from .scheduler import ContinuousBatcher
+        if not chunks:
+            return []
+        self.batcher = ContinuousBatcher(self.decoder)
+        return self.batcher.run(chunks, language, context, temperature, top_p, top_k, n_predicts=n_predicts)
 
     def _long(self, audio, result, language, context, verbose, segment_size, overlap, base, temperature, top_p,
               top_k, ranks):

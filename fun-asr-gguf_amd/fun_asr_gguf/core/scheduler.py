@@ -1,0 +1,189 @@
+"""Continuous batching of many segments / clips on one engine (configs[2]: "encoder batching + decoder continuous
+batch").
+
+The reference decodes segments one after another (core/orchestrator.py:139-171; per segment
+StreamDecoder.decode_stream, core/decoder.py:132-246). Here the engine's sequence slots (max_batch of them) decode
+together, and a slot freed by a finished sequence (stop token, n_predict, repetition breaker) is refilled with the
+next waiting clip: its encode + CTC + prompt run as one encoder batch with the other clips admitted at the same
+time, its prompt is prefilled into the free slot, and it joins the running decode at the next chunk. The per-segment
+rules are the reference's: stop ids and the breaker replayed on the host in token order (decoder.py:91-114), a cut
+attempt retried at temperature + 0.3 up to 6 attempts (decoder.py:201-211; retries run as one group after the
+queue drains, since one generate call shares one sampler setting).
+
+Results per clip do not depend on admission order when max_batch <= the engine's invariant width
+(fa_llm_invariant_width: every clip then decodes with its single-sequence arithmetic and is prefilled alone);
+wider batches agree to the q8_0 noise floor.
+"""
+import time
+from typing import List, Optional
+
+import numpy as np
+
+from ..nano_dataclass import LLMDecodeResult, RecognitionStream
+from .decoder import ABORT_MARK, GEN_CHUNK, STOP_TOKENS, _SeqState, prefill_group
+
+RETRY_ATTEMPTS = 6  # decoder.py:201-211: the first attempt + 5 retries
+
+
+class _Job:
+    __slots__ = ("idx", "stream", "front", "state", "res", "t0", "slot")
+
+    def __init__(self, idx, stream, front):
+        self.idx, self.stream, self.front = idx, stream, front
+        self.state = self.res = self.t0 = self.slot = None
+
+
+class ContinuousBatcher:
+    """decode_segments with slot reuse. admit_min: free slots that trigger an admission while clips wait (an
+    admission runs one encoder batch; admitting one clip at a time would pay the batch-1 encode per clip)."""
+
+    def __init__(self, decoder, admit_min=None):
+        self.decoder = decoder
+        self.models = decoder.models
+        self.admit_min = admit_min
+        self.stats = {}
+
+    @staticmethod
+    def _begin(eng, jobs, queue, samp):
+        # short chunks while clips wait (a freed slot is refilled soon), else up to GEN_CHUNK steps
+        rem = [j.state.remaining() for j in jobs]
+        chunk = min(GEN_CHUNK, max(rem) if not queue else max(4, min(rem)))
+        eng.llm_generate_begin([j.slot for j in jobs], chunk, **samp)
+        return list(jobs), chunk
+
+    @staticmethod
+    def _continues(j, row, chunk, stop_ids):
+        st = j.state
+        if st.done:
+            return False
+        left = st.remaining()
+        if left <= chunk:
+            return False
+        return st.ignore_eos or not np.isin(row[:chunk], stop_ids).any()
+
+    def run(self, chunks: List[np.ndarray], language=None, context=None, temperature=0.3, top_p=1.0, top_k=50,
+            n_predicts: Optional[List[int]] = None, reporter=None):
+        """chunks: PCM clips (each <= segment_size + 2 s). n_predicts: per-clip decode-length caps (default
+        config.n_predict each; the variable-length benchmark protocol pins them). -> [DecodeResult] in input order."""
+        m = self.models
+        eng = m.engine
+        cfg = m.config
+        sr = cfg.sample_rate
+        S = max(1, cfg.max_batch)
+        admit_min = self.admit_min or max(1, S // 4)
+        n_pred = list(n_predicts) if n_predicts is not None else [cfg.n_predict] * len(chunks)
+        samp = self.decoder.llm_decoder._sampling(temperature, top_p, top_k)
+        stop_ids = np.array(sorted({m.eos_token} | set(STOP_TOKENS)), np.int64)
+        queue = list(range(len(chunks)))
+        free = list(range(S))
+        active = []          # jobs decoding, in slot-admission order
+        done = {}            # idx -> (job, LLMDecodeResult)
+        retry = []           # jobs cut by the breaker: retried after the queue drains
+        n_admit = n_encode_batches = 0
+        t_enc = t_pre = 0.0
+
+        def admit(k):
+            nonlocal n_admit, n_encode_batches, t_enc, t_pre
+            idxs = [queue.pop(0) for _ in range(k)]
+            streams = []
+            for i in idxs:
+                st = RecognitionStream()
+                st.accept_waveform(sr, chunks[i])
+                streams.append(st)
+            t = time.perf_counter()
+            fronts = self.decoder.front(streams, language, context)
+            t_enc += time.perf_counter() - t
+            n_encode_batches += 1
+            jobs = [_Job(i, st, f) for i, st, f in zip(idxs, streams, fronts)]
+            slots = [free.pop(0) for _ in jobs]
+            t = time.perf_counter()
+            for q in slots:
+                eng.llm_reset(q)
+            firsts = prefill_group(eng, slots, [j.front["embd"] for j in jobs], samp)
+            dt = time.perf_counter() - t
+            t_pre += dt
+            now = time.perf_counter()
+            for j, q, first in zip(jobs, slots, firsts):
+                j.slot = q
+                j.state = _SeqState(m.vocab, n_pred[j.idx], m.eos_token, cfg.ignore_eos, None)
+                j.res = LLMDecodeResult()
+                j.res.t_inject = dt / len(jobs)
+                j.t0 = now
+                j.state.feed([first])
+                if j.state.done:
+                    finish(j)
+                else:
+                    active.append(j)
+            n_admit += len(jobs)
+
+        def finish(j):
+            st = j.state
+            st.ps.flush()
+            j.res.text, j.res.n_gen = st.ps.generated_text, st.ps.tokens_generated
+            j.res.t_gen, j.res.is_aborted = time.perf_counter() - j.t0, st.aborted
+            free.append(j.slot)
+            if st.aborted:
+                retry.append(j)
+            else:
+                done[j.idx] = (j, j.res)
+
+        def want_admit():
+            if not queue or not free:
+                return 0
+            if len(free) >= min(admit_min, len(queue)) or not active:
+                return min(len(free), len(queue), eng.max_batch if hasattr(eng, "max_batch") else S)
+            return 0
+
+        pending = None  # (jobs, chunk) of the generate call in flight
+        try:
+            while True:
+                if pending is None:
+                    k = want_admit()
+                    if k:
+                        admit(k)
+                        continue
+                    if not active:
+                        break
+                    pending = self._begin(eng, active, queue, samp)
+                jobs, chunk = pending
+                toks = eng.llm_generate_end()
+                pending = None
+                # sequences this chunk leaves unfinished, decided from the token ids alone (stop ids, n_predict), get
+                # the next chunk enqueued BEFORE the host detokenises this one (host work overlaps the GPU's) -- unless
+                # the slots it frees are due for an admission (a prefill cannot run while a chunk is in flight). A
+                # sequence the repetition breaker cuts during feed() rides along one chunk; its tokens are ignored.
+                cont = [j for row, j in enumerate(jobs) if self._continues(j, toks[row], chunk, stop_ids)]
+                n_free = len(free) + len(jobs) - len(cont)
+                if cont and not (queue and n_free >= min(admit_min, len(queue))):
+                    pending = self._begin(eng, cont, queue, samp)
+                cs = set(id(j) for j in cont)
+                for row, j in enumerate(jobs):
+                    j.state.feed(toks[row][:chunk])
+                    if pending is None or id(j) not in cs:
+                        if j.state.done:
+                            finish(j)
+                active = [j for j in jobs if (pending is not None and id(j) in cs) or not j.state.done]
+        finally:
+            if pending is not None:  # host code raised between begin and end: land the chunk, keep the engine usable
+                try:
+                    eng.llm_generate_end()
+                except Exception:
+                    pass
+        # the reference retries a cut segment at temperature + 0.3, up to 6 attempts (decoder.py:201-211)
+        if retry:
+            embds = [j.front["embd"] for j in retry]
+            rs = self.decoder.llm_decoder.decode_with_retry(embds, [n_pred[j.idx] for j in retry],
+                                                            temperature + 0.3, top_p, top_k, None, False,
+                                                            attempts=RETRY_ATTEMPTS - 1)
+            for j, r in zip(retry, rs):
+                done[j.idx] = (j, r)
+        self.stats = dict(admissions=n_admit, encode_batches=n_encode_batches, retried=len(retry),
+                          encode_s=t_enc, prefill_s=t_pre)
+        out = []
+        for i in range(len(chunks)):
+            j, r = done[i]
+            out.append(self.decoder.back(j.stream, j.front, r))
+        return out
+
+
+__all__ = ["ContinuousBatcher", "ABORT_MARK"]

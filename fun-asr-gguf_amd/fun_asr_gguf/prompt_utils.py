@@ -29,8 +29,8 @@ class PromptBuilder:
         self.vocab = vocab
         self.engine = engine
         self.fixed_ids = None  # benchmark protocol: (prefix_ids, suffix_ids) pinned when no tokenizer exists
-        # embedding rows of recent prompts (a batch's streams usually share one prompt): keyed by the token ids and
-        # the engine's weight generation, so a weight change never serves stale rows
+        # embedding rows of recent prompts (a batch's streams usually share one prompt): keyed by the engine object,
+        # its weight generation and the token ids, so a weight change or a new engine never serves stale rows
         self._embd_cache = {}
 
     def build_ids(self, hotwords=None, language=None, context=None):
@@ -42,13 +42,19 @@ class PromptBuilder:
     def build_prompt(self, hotwords=None, language=None, context=None):
         """-> (prefix_embd, suffix_embd, n_prefix, n_suffix, prefix_text), like the reference."""
         pi, si, p = self.build_ids(hotwords, language, context)
-        key = (getattr(self.engine, "weights_gen", None), tuple(pi), tuple(si))
-        hit = self._embd_cache.get(key)
+        gen = getattr(self.engine, "weights_gen", None)
+        key = (id(self.engine), gen, tuple(pi), tuple(si))
+        hit = self._embd_cache.get(key) if gen is not None else None
         if hit is None:
-            pe = self.engine.embd_rows(np.array(pi, np.int32), fp16_round=True) if pi else np.zeros((0, 1024), np.float32)
-            se = self.engine.embd_rows(np.array(si, np.int32), fp16_round=True) if si else np.zeros((0, 1024), np.float32)
-            if len(self._embd_cache) >= 64:
-                self._embd_cache.clear()
-            hit = self._embd_cache[key] = (pe, se)
+            E = int(self.engine.llm_cfg["n_embd"]) if hasattr(self.engine, "llm_cfg") else 1024
+            pe = self.engine.embd_rows(np.array(pi, np.int32), fp16_round=True) if pi else np.zeros((0, E), np.float32)
+            se = self.engine.embd_rows(np.array(si, np.int32), fp16_round=True) if si else np.zeros((0, E), np.float32)
+            pe.flags.writeable = False  # shared by every caller of this prompt: read-only
+            se.flags.writeable = False
+            hit = (pe, se)
+            if gen is not None:  # an engine without a weight generation cannot tell stale rows: no caching
+                if len(self._embd_cache) >= 64:
+                    self._embd_cache.clear()
+                self._embd_cache[key] = hit
         pe, se = hit
         return pe, se, len(pi), len(si), p

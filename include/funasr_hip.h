@@ -77,6 +77,14 @@ int fa_load_gguf(fa_engine* e, const char* path);
 int fa_get_tensor_q8_0(fa_engine* e, const char* name, uint8_t* out, int64_t n_bytes);
 /* Copy an f32 tensor (encoder / norm weights) back (test hook). */
 int fa_get_tensor_f32(fa_engine* e, const char* name, float* out, int64_t n);
+/* Load-completeness bookkeeping (the reference's init fails when a model file cannot fill its graph:
+ * ORT/llama.cpp raise, model_manager.py:98-100 -> asr_engine.py:135). Every upload (fa_set_tensor_*,
+ * fa_load_gguf) marks its tensor as loaded; fa_weights_mark_unset clears that mark for every tensor whose
+ * name starts with `prefix` ("" = all); fa_tensor_names lists the tensors under `prefix` in registration
+ * order ('\n'-separated, NUL-terminated into buf of cap bytes; *needed = bytes required including the NUL),
+ * only the ones not loaded since the last mark when only_unset != 0. */
+int fa_weights_mark_unset(fa_engine* e, const char* prefix);
+int fa_tensor_names(fa_engine* e, const char* prefix, int32_t only_unset, char* buf, int64_t cap, int64_t* needed);
 
 /* ---- encoder operator (replaces encoder_sess.run_with_ort_values + ctc_sess.run)
  * pcm: batch clips, clip b at pcm + b*stride with n_samples[b] valid samples (16 kHz f32).
@@ -153,6 +161,15 @@ int fa_llm_generate_end(fa_engine* e, int32_t* tokens_out);
 /* Logits [n_vocab] of sequence `seq` from the most recent forward (fa_llm_prefill, or the last step of
  * fa_llm_generate) when that forward included it; FA_ERR_ARG otherwise (test hook; llama_get_logits_ith). */
 int fa_llm_logits(fa_engine* e, int32_t seq, float* out);
+/* Largest decode batch width whose per-token arithmetic is bit-identical to decoding that sequence alone (the
+ * reference decodes every segment alone, core/decoder.py:70-123): sequences decoded together in batches up to this
+ * width, each prefilled alone, produce exactly their single-sequence tokens. Wider batches agree to the q8_0 noise
+ * floor. */
+int fa_llm_invariant_width(fa_engine* e, int32_t* out);
+/* Make `token` the input of the sequence's next generate step in place of the token it sampled last: the
+ * caller-chosen token of the reference loop's llama_decode(batch{token, pos}) (decoder.py:91-98, llama.py:490-498),
+ * used for teacher-forced parity runs. */
+int fa_llm_set_token(fa_engine* e, int32_t seq, int32_t token);
 /* Current length (n_past) of a sequence slot. */
 int fa_llm_n_past(fa_engine* e, int32_t seq, int32_t* out);
 

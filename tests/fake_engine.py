@@ -22,6 +22,8 @@ class FakeEngine:
         self.seqs = {}
 
     def encode(self, clips, want_enc=False, resident=None):
+        self._idle("encode")
+        self.n_encodes = getattr(self, "n_encodes", 0) + 1
         self.last = [np.asarray(c, np.float32) for c in clips]
         out = dict(audio_embd=[], ctc_ids=[])
         for c in self.last:
@@ -52,9 +54,11 @@ class FakeEngine:
         return np.repeat(np.asarray(ids, np.float32)[:, None] / N_VOCAB, 1024, 1)
 
     def llm_reset(self, s):
+        self._idle("llm_reset")
         self.seqs.pop(s, None)
 
     def llm_prefill(self, s, embd, **samp):
+        self._idle("llm_prefill")
         h = int(np.abs(embd).sum() * 1000) % 100003
         self.seqs[s] = h
         return 1000 + h % 20
@@ -71,11 +75,20 @@ class FakeEngine:
         return out
 
     def llm_generate_begin(self, seqs, n, **samp):
+        self._idle("llm_generate_begin")
         self._pending = self.llm_generate(seqs, n, **samp)
+        self.max_width = max(getattr(self, "max_width", 0), len(seqs))
 
     def llm_generate_end(self):
+        if getattr(self, "_pending", None) is None:
+            raise RuntimeError("no generate call in flight")
         out, self._pending = self._pending, None
         return out
+
+    def _idle(self, what):
+        # the native engine refuses every other decoder call while a generate call is in flight
+        if getattr(self, "_pending", None) is not None:
+            raise RuntimeError(f"{what}: a generate call is in flight")
 
 
 def fake_models(max_batch=4, n_predict=24):

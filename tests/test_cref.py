@@ -100,3 +100,19 @@ def test_cref_decoder_tiny_vs_numpy_oracle():
         if s[-1] - s[-2] > 0.25:
             assert int(np.argmax(a)) == int(np.argmax(b))
         tok, pos = int(np.argmax(b)), pos + 1
+
+
+def test_cref_decoder_full_vs_hf():
+    """cref's decoder at full dims (28 layers, vocab 151936, GQA 16/8, RoPE theta 1e6 at positions 204-215) against
+    HF Qwen3 on the configs[1] prompt, teacher-forced on HF's greedy ids (tests/hf_full.py for the bars)."""
+    import hf_full
+    g, adaptor = hf_full.load()
+    c = cref.CQwen3(synth.LLM_FULL, n_ctx=512)
+    try:
+        hf_full.check(g, 0, c.forward(hf_full.prompt(g, adaptor, c.embed_prompt), 0))
+        pos = 204
+        for i, t in enumerate(g["greedy"]):
+            hf_full.check(g, i + 1, c.forward(c.embed_tokens([int(t)]), pos))
+            pos += 1
+    finally:
+        c.close()

@@ -275,3 +275,154 @@ def test_c4_300s_long_audio_full_model(cenc):
                            r["ctc_ids"], r["ctc_margin"], f"segment {b}")
     finally:
         api.cleanup()
+
+
+def test_llm_full_vs_hf_anchor(eng):
+    """The GPU decoder at full dims against the independent anchor (tests/golden/qwen3_full_hf.npz: HF Qwen3 on the
+    configs[1] prompt, 204 rows): prefill last-row logits, then 12 decode steps through the production step (the
+    fused two-launch layer, graph-replayed) teacher-forced on HF's greedy ids (fa_llm_set_token) at positions
+    204-215. Bars in tests/hf_full.py (the q8_0 activation noise floor)."""
+    import hf_full
+    g, adaptor = hf_full.load()
+    p = hf_full.prompt(g, adaptor, lambda ids: eng.embd_rows(np.asarray(ids, np.int32)))
+    eng.llm_reset(0)
+    _, lg = eng.llm_prefill(0, p, want_logits=True)
+    cos = [hf_full.check(g, 0, lg)]
+    for i, t in enumerate(g["greedy"]):
+        eng.llm_set_token(0, int(t))
+        eng.llm_generate([0], 1)
+        cos.append(hf_full.check(g, i + 1, eng.llm_logits(0)))
+    print("GPU vs HF full-dims cosines", np.round(cos, 6))
+
+
+def _bench_prompts(eng, adaptor, n):
+    """configs[2] prompts: n x (73 prefix + 126 adaptor rows + 5 suffix) = n x 204 rows, each its own prefix ids."""
+    out = []
+    for i in range(n):
+        rng = np.random.default_rng(500 + i)
+        out.append(np.concatenate([eng.embd_rows(rng.integers(0, 151933, 73).astype(np.int32)), adaptor,
+                                   eng.embd_rows(rng.integers(0, 151933, 5).astype(np.int32))], 0).astype(np.float32))
+    return out
+
+
+def test_llm_full_c3_bench_shape_vs_oracle(eng, cllm, g60):
+    """configs[2] at its benchmarked shape: 32 x 204 rows = 6528 rows prefilled by one fa_llm_prefill_batch (the tiled
+    q8_0 GEMM and query-tiled prefill attention), then 8 decode steps at M = 32 (int8 MFMA GEMMs, batched attention,
+    the batched LM head) at n_past 204-211; prompts 0, 15 and 31 against the oracle run of that prompt alone."""
+    prompts = _bench_prompts(eng, g60["adaptor"].astype(np.float32), 32)
+    seqs = list(range(32))
+    for s in seqs:
+        eng.llm_reset(s)
+    firsts = eng.llm_prefill_batch(seqs, prompts)
+    lg0 = {s: eng.llm_logits(s) for s in (0, 15, 31)}
+    steps, lgs = [], []
+    for _ in range(8):
+        steps.append(eng.llm_generate(seqs, 1)[:, 0])
+        lgs.append({s: eng.llm_logits(s) for s in (0, 15, 31)})
+    for s in (0, 15, 31):
+        ref = cllm.forward(prompts[s], 0)
+        _check_step(lg0[s], ref)
+        assert firsts[s] == int(np.argmax(lg0[s]))
+        tok, pos = firsts[s], 204
+        for k in range(8):
+            ref = cllm.forward(cllm.embed_tokens([tok]), pos)
+            _check_step(lgs[k][s], ref)
+            assert int(steps[k][s]) == int(np.argmax(lgs[k][s]))
+            tok, pos = int(steps[k][s]), pos + 1
+
+
+def _single_runs(eng, prompts, K):
+    """Each prompt decoded alone in slot 0 (the reference decodes every segment alone): first token + K greedy steps,
+    logits of every step."""
+    out = []
+    for p in prompts:
+        eng.llm_reset(0)
+        t, lg = eng.llm_prefill(0, p, want_logits=True)
+        toks, lgs = [t], [lg]
+        for _ in range(K):
+            toks.append(int(eng.llm_generate([0], 1)[0][0]))
+            lgs.append(eng.llm_logits(0))
+        out.append((toks, np.stack(lgs)))
+    return out
+
+
+def test_llm_full_invariant_width_batch_equals_single(eng, g60):
+    """Within the engine's invariant width (6: the two-launch layer gives every token its own grid slab, the LM head is
+    the fused GEMV) a batch of full-dims sequences, each prefilled alone, decodes with exactly the arithmetic of each
+    sequence alone: bit-identical logits and tokens over 16 free-running greedy steps. This is what makes C4's
+    6-segment batch (and any rank's share of segments) give the reference's one-segment-at-a-time results."""
+    from fun_asr_gguf.core.decoder import prefill_group
+    W = eng.llm_invariant_width()
+    assert W >= 6
+    prompts = _bench_prompts(eng, g60["adaptor"].astype(np.float32), W)
+    K = 16
+    single = _single_runs(eng, prompts, K)
+    seqs = list(range(W))
+    for s in seqs:
+        eng.llm_reset(s)
+    firsts = prefill_group(eng, seqs, prompts, dict(temperature=0.0))
+    toks = [list(firsts)]
+    for k in range(K):
+        toks.append([int(t) for t in eng.llm_generate(seqs, 1)[:, 0]])
+        if k == K - 1:
+            for s in seqs:
+                assert np.array_equal(eng.llm_logits(s), single[s][1][K]), f"seq {s}: logits differ from alone"
+    for s in seqs:
+        assert [t[s] for t in toks] == single[s][0], f"seq {s}: tokens differ from decoding it alone"
+
+
+def test_llm_full_batch32_vs_single_streams_bound(eng, g60):
+    """Above the invariant width (configs[2]: 32 streams at M = 32 on the int8 MFMA GEMMs with producer-side
+    quantisation and the batched LM head, prefilled as one 6528-row batch) a stream's logits differ from decoding it
+    alone by f32 summation order, amplified by q8_0 activation rounding flips: 32 streams x 16 steps, teacher-forced
+    on each stream's single-stream tokens (fa_llm_set_token). Bound: cosine >= 0.9995 per vector and the same argmax
+    wherever the single-stream top-2 margin exceeds 0.15 (two q8_0 noise floors, tests/hf_full.py)."""
+    prompts = _bench_prompts(eng, g60["adaptor"].astype(np.float32), 32)
+    K = 16
+    single = _single_runs(eng, prompts, K)
+    seqs = list(range(32))
+    for s in seqs:
+        eng.llm_reset(s)
+    eng.llm_prefill_batch(seqs, prompts)
+    worst_cos, diffs, flips = 1.0, [], []
+    for k in range(K + 1):
+        if k > 0:
+            for s in seqs:
+                eng.llm_set_token(s, single[s][0][k - 1])
+            eng.llm_generate(seqs, 1)
+        for s in seqs:
+            lg, ref = eng.llm_logits(s), single[s][1][k]
+            c = _cos(lg, ref)
+            worst_cos = min(worst_cos, c)
+            diffs.append(float(np.abs(lg - ref).max()))
+            top2 = np.sort(ref)[-2:]
+            if int(np.argmax(lg)) != int(np.argmax(ref)):
+                flips.append(float(top2[1] - top2[0]))
+            assert c >= 0.9995, f"seq {s} step {k}: cosine {c}"
+            if top2[1] - top2[0] > 0.15:
+                assert int(np.argmax(lg)) == int(np.argmax(ref)), f"seq {s} step {k}: argmax at margin {top2[1] - top2[0]}"
+    d = np.array(diffs)
+    print(f"batch-32 vs single: worst cos {worst_cos:.6f}, max|diff| p50 {np.median(d):.4f} p99 "
+          f"{np.quantile(d, 0.99):.4f} max {d.max():.4f}; bit-identical vectors {(d == 0).mean():.3f}; argmax flips "
+          f"{len(flips)} / {d.size} at margins {np.round(sorted(flips), 4).tolist()[:12]}")
+
+
+def test_c4_batch_of_6_equals_sequential_segments():
+    """configs[3] on one GPU: the six segments of the 300 s file decoded as one continuous batch (max_batch 6, the
+    invariant width) give exactly the text and char timestamps of six one-segment calls (the reference decodes the
+    segments one after another, orchestrator.py:139-171)."""
+    from fun_asr_gguf import create_asr_engine
+    from fun_asr_gguf.synthetic import synth_audio
+    api = create_asr_engine("synthetic", "synthetic", "synthetic", "synthetic", verbose=False, model="full",
+                            max_batch=6, n_ctx=512, n_predict=253, ignore_eos=True)
+    try:
+        audio = synth_audio(300 * SR, 4000)
+        wins = octc.segments_info(300.0, 60.0, 4.0)
+        chunks = [audio[int(s * SR):int(e * SR)] for s, e in wins]
+        batch = api.transcribe_batch(chunks, temperature=0.0)
+        for c, b in zip(chunks, batch):
+            one = api.transcribe_batch([c], temperature=0.0)[0]
+            assert b.n_gen == one.n_gen == 253
+            assert b.text == one.text and b.aligned == one.aligned
+    finally:
+        api.cleanup()

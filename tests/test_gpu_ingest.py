@@ -104,3 +104,45 @@ def test_api_onnx_encoder_and_gguf_tokenizer(gguf_path, tmp_path):
         api.cleanup()
         api_st.cleanup()
         ref.close()
+
+
+def test_incomplete_model_files_fail_init(tmp_path):
+    """A model file that leaves any tensor of its part of the graph unfilled fails initialisation (the reference's ORT /
+    llama.cpp loaders raise, model_manager.py:98-100 -> asr_engine.py:135) and names the missing tensors."""
+    import logging
+    from fun_asr_gguf import create_asr_engine
+    W = synth.make_weights(synth.encoder_tensors(synth.ENC_TINY), seed=0)
+    enc_sd = {k: v for k, v in W.items() if k.startswith(("audio_encoder.", "audio_adaptor."))}
+    ctc_sd = {k: v for k, v in W.items() if k.startswith(("ctc_decoder.", "ctc_proj."))}
+    drop_enc, drop_ctc = "audio_encoder.encoders.1.feed_forward.w_2.bias", "ctc_decoder.blocks.0.norm1.weight"
+    assert drop_enc in enc_sd and drop_ctc in ctc_sd
+    enc_p, ctc_p = tmp_path / "enc.onnx", tmp_path / "ctc.onnx"
+    enc_bad, ctc_bad = tmp_path / "enc_bad.onnx", tmp_path / "ctc_bad.onnx"
+    write_onnx(str(enc_p), enc_sd, prefix="hybrid_model.")
+    write_onnx(str(ctc_p), ctc_sd)
+    write_onnx(str(enc_bad), {k: v for k, v in enc_sd.items() if k != drop_enc}, prefix="hybrid_model.")
+    write_onnx(str(ctc_bad), {k: v for k, v in ctc_sd.items() if k != drop_ctc})
+    # a GGUF missing one decoder matrix
+    Wl = synth.make_weights(synth.llm_tensors(LLM_V), seed=0)
+    g_bad = tmp_path / "bad.gguf"
+    from fun_asr_gguf.vocab import read_gguf_metadata
+    kv = {k: v for k, v in read_gguf_metadata(os.path.join(GOLDEN, "tokenizer_qwen2_synth.gguf")).items()
+          if k.startswith("tokenizer.")}
+    write_gguf(str(g_bad), kv,
+               [(n, w, GGML_Q8_0 if w.ndim == 2 else GGML_F32) for n, w in Wl.items() if n != "blk.1.ffn_up.weight"])
+    kw = dict(verbose=False, model="tiny", max_batch=1, n_ctx=256, n_predict=4)
+    ok = create_asr_engine(str(enc_p), str(ctc_p), "synthetic", "synthetic", **kw)  # complete files load
+    ok.cleanup()
+    for args, missing in (((str(enc_bad), str(ctc_p), "synthetic", "synthetic"), drop_enc),
+                          ((str(enc_p), str(ctc_bad), "synthetic", "synthetic"), drop_ctc),
+                          (("synthetic", "synthetic", str(g_bad), "synthetic"), "blk.1.ffn_up.weight")):
+        records = []
+        h = logging.Handler()
+        h.emit = records.append
+        logging.getLogger("fun_asr_gguf").addHandler(h)
+        try:
+            with pytest.raises(RuntimeError):
+                create_asr_engine(*args, **kw)
+        finally:
+            logging.getLogger("fun_asr_gguf").removeHandler(h)
+        assert any(missing in r.getMessage() or (r.exc_info and missing in str(r.exc_info[1])) for r in records), missing

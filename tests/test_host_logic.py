@@ -84,3 +84,19 @@ def test_srt_writer():
         p = generate_srt_file(segs, os.path.join(td, "a.srt"))
         s = open(p, encoding="utf-8").read()
     assert s.startswith("1\n00:00:00,000 --> ") and "你好。" in s and "世界！" in s
+
+
+def test_init_fails_loudly_on_missing_model_files(tmp_path):
+    """A model path that does not exist fails initialisation (model_manager.py:98-100 returns False, asr_engine.py:135
+    raises) instead of running on synthetic weights; checked before any device work, so this runs without a GPU."""
+    import pytest
+    from fun_asr_gguf import FunASREngine, create_asr_engine
+    missing = str(tmp_path / "Fun-ASR-Nano-Encoder-Adaptor.typo.onnx")
+    for args in ((missing, "synthetic", "synthetic", "synthetic"), ("synthetic", missing, "synthetic", "synthetic"),
+                 ("synthetic", "synthetic", str(tmp_path / "q8.gguf"), "synthetic"),
+                 ("synthetic", "synthetic", "synthetic", str(tmp_path / "tokens.txt"))):
+        eng = FunASREngine(*args, model="tiny")
+        assert eng.initialize(verbose=False) is False
+        assert eng.models.engine is None
+        with pytest.raises(RuntimeError):
+            create_asr_engine(*args, verbose=False, model="tiny")

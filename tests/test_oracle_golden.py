@@ -122,3 +122,14 @@ def test_fp16_graph_oracle_tracks_fp32_reference():
     assert np.abs(r["audio_embd"] - g["adaptor"]).max() < 3e-2 * np.abs(g["adaptor"]).max()
     # every output is an fp16 value
     assert (r["audio_embd"].astype(np.float16).astype(np.float32) == r["audio_embd"]).all()
+
+
+def test_qwen3_oracle_full_vs_hf():
+    """The numpy decoder oracle at full dims against HF Qwen3 on the configs[1] prompt + 4 teacher-forced steps
+    (tests/hf_full.py for the bars; cref runs all 12 steps in test_cref.py)."""
+    import hf_full
+    g, adaptor = hf_full.load()
+    m = qwen3.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_FULL)), synth.LLM_FULL, n_ctx=256)
+    hf_full.check(g, 0, m.forward(hf_full.prompt(g, adaptor, m.embed_prompt), 0))
+    for i in range(4):
+        hf_full.check(g, i + 1, m.forward(m.embed_tokens([int(g["greedy"][i])]), 204 + i))
