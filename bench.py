@@ -140,6 +140,69 @@ def c3_leg(batch, steps, warmup, device, model, barrier, dist):
             "stage_ms": {k: round(v / steps * 1e3, 2) for k, v in zip(["encode", "prefill", "generate", "align"], stage)}}
 
 
+def c3_varlen_leg(n_clips, batch, device, model, barrier, dist):
+    """configs[2] with variable decode lengths: n_clips x 60 s clips on `batch` sequence slots, each clip's decode
+    length pinned to a seeded draw from U[128, 384] tokens (mean 256 ~ the README's 253; stands in for EOS, which
+    synthetic weights do not emit). Continuous batching (core/scheduler.py: a finished clip's slot is refilled with the
+    next waiting clip, admitted as an encoder batch + prefill) against static groups of `batch` clips that each run
+    to their longest member. The PCM goes host -> HBM inside the call (PCIe-inclusive)."""
+    from fun_asr_gguf import FunASREngine
+    from fun_asr_gguf.nano_dataclass import RecognitionStream
+    from fun_asr_gguf.synthetic import synth_audio
+    eng = FunASREngine("synthetic", "synthetic", "synthetic", "synthetic", n_predict=384, device=device,
+                       model=model, ignore_eos=True, max_batch=batch, n_ctx=640)
+    if not eng.initialize(verbose=False):
+        raise RuntimeError("C3 varlen engine init failed")
+    m = eng.models
+    rng = np.random.default_rng(1234)
+    m.prompt_builder.fixed_ids = (list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_PREFIX)),
+                                  list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_SUFFIX)))
+    rank = dist.get_rank() if dist is not None else 0
+    clips = [synth_audio(int(CLIP_S * SR), 3000 + rank * n_clips + i) for i in range(n_clips)]
+    lens = [int(x) for x in np.random.default_rng(77 + rank).integers(128, 385, n_clips)]
+    orch = eng.orchestrator
+
+    def continuous():
+        return orch.decode_segments(clips, None, None, False, 0.0, 1.0, 50, n_predicts=lens)
+
+    def static():
+        out = []
+        for i in range(0, n_clips, batch):
+            sts = []
+            for c in clips[i:i + batch]:
+                st = RecognitionStream()
+                st.accept_waveform(SR, c)
+                sts.append(st)
+            out += orch.decoder.decode_streams(sts, verbose=False, temperature=0.0, n_predicts=lens[i:i + batch])
+        return out
+
+    res = {}
+    for name, fn in (("continuous", continuous), ("static", static)):
+        rs = fn()  # warm-up (graphs for every batch width)
+        assert [r.n_gen for r in rs] == lens
+        m.engine.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        fn()
+        m.engine.synchronize()
+        dt = time.perf_counter() - t0
+        barrier()
+        if dist is not None:
+            import torch
+            tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        world = dist.get_world_size() if dist is not None else 1
+        res[name] = {"value": round(CLIP_S * n_clips * world / dt, 2), "ms": round(dt * 1e3, 2)}
+    st = orch.batcher.stats if hasattr(orch, "batcher") else {}
+    eng.cleanup()
+    return {"workload": f"configs[2] variable length: {n_clips} x 60 s clips per GPU on {batch} slots, decode lengths "
+                        f"U[128, 384] (mean {np.mean(lens):.0f} tokens, pinned per clip)", "unit": "audio_s/s",
+            "continuous": res["continuous"], "static": res["static"],
+            "speedup": round(res["continuous"]["value"] / res["static"]["value"], 3),
+            "admissions": st.get("admissions"), "encode_batches": st.get("encode_batches")}
+
+
 def c4_leg(steps, warmup, device, model, barrier, dist):
     """configs[3] (C4): one 300 s file, segment_size 60 / overlap 4 -> 6 segments {0-60, 56-116, ..., 280-300}
     (orchestrator.py:123-136) through the public FunASREngine.transcribe long path. N=1: all segments as one
@@ -197,6 +260,7 @@ def main():
     ap.add_argument("--c3-batch", type=int, default=32, help="clips per step of the C3 leg (0 = skip)")
     ap.add_argument("--c3-steps", type=int, default=2)
     ap.add_argument("--c4-steps", type=int, default=2)
+    ap.add_argument("--c3-varlen", type=int, default=64, help="clips of the variable-length C3 leg (0 = skip)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (300 s long-audio) leg")
     args = ap.parse_args()
 
@@ -303,6 +367,27 @@ def main():
                              "value": round(CLIP_S * args.steps / dts, 3), "unit": "audio_s/s",
                              "ms_per_step": round(dts / args.steps * 1e3, 3),
                              "generate_ms": round(gen_s / args.steps * 1e3, 3)}
+    # exact-f32 leg: the same clip with the encoder GEMMs and attention on v_mfma_f32_32x32x2_f32 (fa_set_encoder_gemm(0),
+    # the reference graph's arithmetic without the bf16x3 operand split)
+    m.engine.set_encoder_gemm("f32")
+    step()
+    m.engine.synchronize()
+    barrier()
+    tf = time.perf_counter()
+    stf = np.zeros(6)
+    for _ in range(args.steps):
+        tm = step().timings
+        stf += [tm.encode, tm.ctc, tm.prepare, tm.inject, tm.llm_generate, tm.align]
+    m.engine.synchronize()
+    dtf = time.perf_counter() - tf
+    m.engine.set_encoder_gemm("bf16x3")
+    if rank == 0:
+        out["c2_exact_f32"] = {"workload": "configs[1] clip with exact-f32 MFMA encoder GEMMs / attention "
+                                           "(fa_set_encoder_gemm(0))",
+                               "value": round(CLIP_S * args.steps / dtf, 3), "unit": "audio_s/s",
+                               "ms_per_step": round(dtf / args.steps * 1e3, 3),
+                               "stage_ms": {k: round(v / args.steps * 1e3, 3) for k, v in zip(
+                                   ["encode", "ctc", "prompt", "prefill", "generate", "align"], stf)}}
     if rank == 0:
         out["c5"] = {"workload": "configs[4] on 1 GPU: single 60 s clip, fp16 encoder graph + q8_0 LLM, 73-token prefix",
                      "value": round(CLIP_S * args.steps / dt5, 3), "unit": "audio_s/s",
@@ -315,6 +400,11 @@ def main():
             out["c3"] = c3_leg(args.c3_batch, args.c3_steps, 1, local, args.model, barrier, dist)
         except Exception as e:  # reported, never fatal for the headline number
             out["c3"] = {"value": None, "error": str(e)[:300]}
+    if args.c3_varlen > 0:
+        try:
+            out["c3_varlen"] = c3_varlen_leg(args.c3_varlen, args.c3_batch or 32, local, args.model, barrier, dist)
+        except Exception as e:  # reported, never fatal for the headline number
+            out["c3_varlen"] = {"value": None, "error": str(e)[:300]}
     if not args.no_c4:
         try:
             out["c4"] = c4_leg(args.c4_steps, 1, local, args.model, barrier, dist)

@@ -277,11 +277,14 @@ class StreamDecoder:
                             hotwords=job["hotwords"], is_aborted=r.is_aborted)
 
     def decode_streams(self, streams: List[RecognitionStream], language=None, context=None, verbose=True,
-                       reporter=None, temperature=0.3, top_p=1.0, top_k=50, resident=None) -> List[DecodeResult]:
+                       reporter=None, temperature=0.3, top_p=1.0, top_k=50, resident=None,
+                       n_predicts=None) -> List[DecodeResult]:
         """One group of streams: encode batch, then all sequences decode together (no admission).
-        resident: handle from engine.upload() holding these streams' PCM in HBM (benchmark path)."""
+        resident: handle from engine.upload() holding these streams' PCM in HBM (benchmark path).
+        n_predicts: per-stream decode-length caps (default config.n_predict)."""
         jobs = self.front(streams, language, context, resident)
         # 4. LLM with the reference's retry policy (decoder.py:201-211), per sequence
-        final = self.llm_decoder.decode_with_retry([j["embd"] for j in jobs], self.models.config.n_predict,
+        n_p = list(n_predicts) if n_predicts is not None else self.models.config.n_predict
+        final = self.llm_decoder.decode_with_retry([j["embd"] for j in jobs], n_p,
                                                    temperature, top_p, top_k, reporter, verbose)
         return [self.back(st, j, r) for st, j, r in zip(streams, jobs, final)]

@@ -10,9 +10,11 @@ rules are the reference's: stop ids and the breaker replayed on the host in toke
 attempt retried at temperature + 0.3 up to 6 attempts (decoder.py:201-211; retries run as one group after the
 queue drains, since one generate call shares one sampler setting).
 
-Results per clip do not depend on admission order when max_batch <= the engine's invariant width
-(fa_llm_invariant_width: every clip then decodes with its single-sequence arithmetic and is prefilled alone);
-wider batches agree to the q8_0 noise floor.
+Results per clip do not depend on grouping or admission order when max_batch <= the engine's invariant width
+(fa_llm_invariant_width): every clip is then encoded alone, prefilled alone and decodes with its single-sequence
+arithmetic, so a batch gives exactly the one-segment-at-a-time results of the reference's loop, and a segment set
+sharded over N GPUs gives exactly the 1-GPU results. Wider batches (padded encoder batches, shared prefill forwards,
+the M > 6 decode kernels) agree to the fp32 / q8_0 noise floors.
 """
 import time
 from typing import List, Optional
@@ -20,7 +22,7 @@ from typing import List, Optional
 import numpy as np
 
 from ..nano_dataclass import LLMDecodeResult, RecognitionStream
-from .decoder import ABORT_MARK, GEN_CHUNK, STOP_TOKENS, _SeqState, prefill_group
+from .decoder import ABORT_MARK, GEN_CHUNK, STOP_TOKENS, _SeqState, invariant_width, prefill_group
 
 RETRY_ATTEMPTS = 6  # decoder.py:201-211: the first attempt + 5 retries
 
@@ -79,6 +81,9 @@ class ContinuousBatcher:
         active = []          # jobs decoding, in slot-admission order
         done = {}            # idx -> (job, LLMDecodeResult)
         retry = []           # jobs cut by the breaker: retried after the queue drains
+        # within the engine's invariant width every clip is encoded and prefilled alone and decodes with its
+        # single-sequence arithmetic: results are exactly the one-clip-at-a-time results, whatever the grouping
+        alone = S <= invariant_width(eng)
         n_admit = n_encode_batches = 0
         t_enc = t_pre = 0.0
 
@@ -91,7 +96,10 @@ class ContinuousBatcher:
                 st.accept_waveform(sr, chunks[i])
                 streams.append(st)
             t = time.perf_counter()
-            fronts = self.decoder.front(streams, language, context)
+            if alone:  # single-clip encoder arithmetic (the padded-batch GEMM tiling / key splits differ in f32 order)
+                fronts = [f for st in streams for f in self.decoder.front([st], language, context)]
+            else:
+                fronts = self.decoder.front(streams, language, context)
             t_enc += time.perf_counter() - t
             n_encode_batches += 1
             jobs = [_Job(i, st, f) for i, st, f in zip(idxs, streams, fronts)]

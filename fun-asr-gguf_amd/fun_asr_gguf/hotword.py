@@ -17,8 +17,11 @@
     (hash order, not reproducible across processes); here it is ordered by first appearance (matchs, similars).
 Thresholds as ModelManager (model_manager.py:82-88): threshold 1.0, similar_threshold = config.similar_threshold.
 The hot.txt watchdog thread (manager.py) becomes an mtime check per call.
-Parity: unpinned — pypinyin and numba are absent, so the reference modules cannot be imported here; the DPs are
-tested against line-by-line restatements (tests/test_hotword.py).
+Parity: pinned to the reference's own hotword modules (algo_phoneme / algo_calc / rag_fast / hot_phoneme imported
+by tests/golden/make_hotword_golden.py with a fixed pinyin table in pypinyin's module slot, and in the reference's
+no-pypinyin degraded mode): phonemes, the constrained fine search, FastRAG.search and PhonemeCorrector.correct equal
+the reference's outputs (tests/test_hotword.py::test_hotword_path_vs_reference_golden). pypinyin itself stays
+absent (its tables are not restated: any implementation with its interface plugs in as `pinyin` / `Style`).
 """
 import os
 import threading

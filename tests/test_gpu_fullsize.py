@@ -426,3 +426,20 @@ def test_c4_batch_of_6_equals_sequential_segments():
             assert b.text == one.text and b.aligned == one.aligned
     finally:
         api.cleanup()
+
+
+def test_encoder_batch_vs_alone_f32_order(eng):
+    """The padded encoder batch (configs[3]'s six segments in one encode) against each segment encoded alone: equal to
+    the fp32 bar (a different GEMM tiling / key-split order, not other math); reports how far from bit-identical."""
+    from fun_asr_gguf.synthetic import synth_audio
+    audio = synth_audio(300 * SR, 4000)
+    wins = octc.segments_info(300.0, 60.0, 4.0)
+    chunks = [audio[int(s * SR):int(e * SR)] for s, e in wins]
+    out = eng.encode(chunks, want_enc=True)
+    worst, same = 0.0, []
+    for b, c in enumerate(chunks):
+        one = eng.encode([c], want_enc=True)
+        worst = max(worst, _rel(out["audio_embd"][b], one["audio_embd"][0]))
+        same.append(bool(np.array_equal(out["audio_embd"][b], one["audio_embd"][0])))
+        assert _rel(out["enc"][b], one["enc"][0]) < ENC_ATOL
+    print(f"encoder batch-6 vs alone: audio_embd max-abs/max {worst:.2e}, bit-identical per segment {same}")

@@ -1,8 +1,8 @@
-"""Hotword phoneme retrieval (fun_asr_gguf.hotword). Parity unpinned: pypinyin and numba are
-absent, so the reference's hotword package cannot be imported; its algorithms are restated below line by line as
-the test oracle (rag_fast.py:291-313 `_python_distance`) and exercised on hand-built phoneme sequences, in the
-reference's own degraded mode (one phoneme per character, algo_phoneme.py:194-195) and through a pinyin path fed by
-a small fixed table standing in for pypinyin."""
+"""Hotword phoneme retrieval (fun_asr_gguf.hotword), pinned to the reference's own hotword modules
+(tests/golden/hotword_golden.json from make_hotword_golden.py: pypinyin is absent, so a fixed pinyin table with its
+interface, tests/golden/fake_pinyin.py, fills its slot for both sides; and the reference's no-pypinyin degraded mode).
+numba is absent: the reference's pure-Python FastRAG distance (rag_fast.py:291-313) is restated below as the oracle of
+the native DP."""
 import numpy as np
 import pytest
 
@@ -111,3 +111,55 @@ def test_engine_hotword_list_into_prompt(tmp_path, monkeypatch):
     d1 = StreamDecoder(m).decode_stream(st, verbose=False, temperature=0.0)
     assert d1.hotwords == [ctc[2:5]]
     assert d1.n_prefix > d0.n_prefix  # the prompt grew by the 热词列表 line
+
+
+def _approx(a, b):
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        return len(a) == len(b) and all(_approx(x, y) for x, y in zip(a, b))
+    if isinstance(a, float) or isinstance(b, float):
+        return abs(float(a) - float(b)) <= 1e-9
+    return a == b
+
+
+@pytest.mark.parametrize("mode", ["pinyin_table", "degraded"])
+def test_hotword_path_vs_reference_golden(monkeypatch, mode):
+    """Pinned to the reference's own hotword modules (tests/golden/hotword_golden.json, make_hotword_golden.py): the
+    phoneme sequences (algo_phoneme.get_phoneme_info), the boundary-constrained fine search
+    (algo_calc.fuzzy_substring_search_constrained), FastRAG.search and PhonemeCorrector.correct on a hot.txt, with the
+    same fixed pinyin table standing in for pypinyin, and in the reference's no-pypinyin degraded mode."""
+    import json
+    import os
+    import sys
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import fake_pinyin
+    gold = json.load(open(os.path.join(GOLDEN, "hotword_golden.json"), encoding="utf-8"))
+    g = gold[mode]
+    if mode == "pinyin_table":
+        monkeypatch.setattr(hwm, "pinyin", fake_pinyin.pinyin)
+        monkeypatch.setattr(hwm, "Style", fake_pinyin.Style)
+    else:
+        monkeypatch.setattr(hwm, "pinyin", None)
+    for t, ph in g["phonemes"].items():
+        assert [list(p.info) for p in hwm.get_phoneme_info(t)] == ph, t
+    for case in g["search"]:
+        hwi = [p.info[:5] for p in hwm.get_phoneme_info(case["hotword"])]
+        inp = [p.info for p in hwm.get_phoneme_info(case["text"])]
+        got = [list(r) for r in hwm.fuzzy_substring_search_constrained(hwi, inp, case["threshold"])]
+        assert _approx(got, case["result"]), (case["hotword"], case["text"], got, case["result"])
+    lines = [ln.strip() for ln in gold["hot"].splitlines() if ln.strip() and not ln.strip().startswith("#")]
+    rag = hwm.FastRAG(threshold=0.5)
+    rag.add_hotwords({hw: hwm.get_phoneme_info(hw) for hw in lines})
+    for t, res in g["fastrag"].items():
+        got = [list(r) for r in rag.search(hwm.get_phoneme_info(t), top_k=10)]
+        assert _approx(got, res), (t, got, res)
+    correctors = {}
+    for case in g["correct"]:
+        key = (case["threshold"], case["similar_threshold"])
+        if key not in correctors:
+            correctors[key] = hwm.PhonemeCorrector(threshold=key[0], similar_threshold=key[1])
+            assert correctors[key].update_hotwords(gold["hot"]) == case["n_hotwords"]
+        r = correctors[key].correct(case["text"], k=10)
+        assert r.text == case["out"], (key, case["text"], r.text, case["out"])
+        assert _approx([list(x) for x in r.matchs], case["matchs"]), (key, case["text"], r.matchs, case["matchs"])
+        assert _approx([list(x) for x in r.similars], case["similars"]), (key, case["text"], r.similars, case["similars"])
