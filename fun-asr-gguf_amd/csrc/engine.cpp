@@ -156,6 +156,8 @@ struct Engine {
   // 0.698 / 0.933 / 0.915 ms vs 0.594 / 0.709 / 0.812 / 0.935 / 1.000 / 1.047 ms on the 5-launch layer; M 7 / 8 1.213 /
   // 1.261 vs 1.070 / 1.073 ms (the AB launch's token slabs, 128 blocks each, no longer fit the chip at once)
   int fused_max_m = 6;
+  // decode steps per captured graph (FUNASR_GRAPH_STEPS): chunks replay graphs of this many steps, then single steps
+  int graph_steps = 1;
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
@@ -1050,17 +1052,19 @@ struct Engine {
 
   // hipGraph of one decode step (all per-step state, the sampler parameters included, lives in device memory;
   // grids are n_past-independent), one per batch width
-  hipGraphExec_t step_graph(int n) {
-    auto it = step_graphs.find(n);
+  // k > 1: k consecutive steps in one graph (one replay instead of k: no inter-graph gap between the steps)
+  hipGraphExec_t step_graph(int n, int k = 1) {
+    const int key = n * 1024 + k;
+    auto it = step_graphs.find(key);
     if (it != step_graphs.end()) return it->second;
     hipGraph_t g;
     hipGraphExec_t ex;
     FA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    decode_step(n);
+    for (int i = 0; i < k; ++i) decode_step(n);
     FA_HIP(hipStreamEndCapture(stream, &g));
     FA_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
     FA_HIP(hipGraphDestroy(g));
-    return step_graphs[n] = ex;
+    return step_graphs[key] = ex;
   }
 
   void gemv(const GemvArgs& a0, int K, int epi) {
@@ -1152,6 +1156,11 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     }
     if (const char* g = getenv("FUNASR_GEMV_MT")) fa::g_gemv_mt = atoi(g) >= 2 ? 2 : 1;
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
+    {  // process-wide split-K shape knob: re-read (or reset) at every engine creation
+      const char* g = getenv("FUNASR_SK_MIN_BLOCKS");
+      fa::g_sk_min_blocks = g ? std::max(1, atoi(g)) : 256;
+    }
+    if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
     fa::g_ffn_pair_min_m = 4;
@@ -1589,8 +1598,15 @@ int fa_llm_generate_begin(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int
   // the sampler reads its parameters from device memory, so the captured step graph serves every setting.
   // Profiling runs eager (event nodes inside graphs do not time individual nodes on ROCm 7.2).
   if (e->use_graphs && !e->prof) {
-    const hipGraphExec_t ex = e->step_graph(n_seqs);
-    for (int st = 0; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, e->stream));
+    int st = 0;
+    if (e->graph_steps > 1 && n_steps >= e->graph_steps) {
+      const hipGraphExec_t exk = e->step_graph(n_seqs, e->graph_steps);
+      for (; st + e->graph_steps <= n_steps; st += e->graph_steps) FA_HIP(hipGraphLaunch(exk, e->stream));
+    }
+    if (st < n_steps) {
+      const hipGraphExec_t ex = e->step_graph(n_seqs);
+      for (; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, e->stream));
+    }
   } else {
     for (int st = 0; st < n_steps; ++st) {
       e->prof_pos = ps[0] + st;  // the profiled fused layer's K/V bytes (batch 1)

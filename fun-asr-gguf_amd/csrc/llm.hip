@@ -1254,6 +1254,7 @@ int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, F
 // split-K shape: NBW q8_0 blocks per wave (8, 4 or 2: one load round trip) and KS = nb / (waves per matrix x NBW)
 // splits; the largest NBW whose split count fills the chip (>= 256 blocks), else the most splits. lm_head's argmax
 // needs whole sums: one split.
+int g_sk_min_blocks = 256;  // split-K: the fewest blocks a shape must reach before fewer splits are preferred
 void gemm_sk_shape(int O, int M, int K, int epi, int* nbw, int* ks) {
   const int tiles = cdiv(O, 32) * cdiv(M, 32), nb = K / 32, wpm = epi == 2 ? 2 : 4;
   *nbw = 0;
@@ -1264,7 +1265,7 @@ void gemm_sk_shape(int O, int M, int K, int epi, int* nbw, int* ks) {
     if (k > (epi == 2 ? 4 : 16) || (epi == 3 && k != 1)) continue;
     *nbw = c;
     *ks = k;
-    if (tiles * k >= 256) return;
+    if (tiles * k >= g_sk_min_blocks) return;
   }
 }
 
