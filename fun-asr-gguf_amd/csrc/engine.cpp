@@ -158,6 +158,7 @@ struct Engine {
   int fused_max_m = 6;
   // decode steps per captured graph (FUNASR_GRAPH_STEPS): chunks replay graphs of this many steps, then single steps
   int graph_steps = 1;
+  int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after a fused fan-in timeout
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
@@ -986,7 +987,7 @@ struct Engine {
         prof_begin(0, &ev);
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
-                         w.o.q, w.o.d, E, attn_wk, fdw, stream, M);
+                         w.o.q, w.o.d, E, attn_wk, fdw, stream, M, (debug_flags & 2) ? 1 : 0);
         prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0 + (M == 1 ? 4.0 * KV * D * (prof_pos + 1.0) : 0.0),
                  2.0 * M * (E * H * D + (double)QKV * E));
       } else {
@@ -1026,15 +1027,67 @@ struct Engine {
     gemv(h, E, 3);
   }
 
-  // fused-decode fan-in timeouts are reported, never silent (the step's outputs are garbage then)
-  void check_fused_error() {
+  // a fused-decode fan-in timeout (a group not co-resident: another kernel held CUs) leaves the chunk's outputs
+  // garbage; -> true (flag cleared) when one happened
+  bool fused_error() {
     int err = 0;
     FA_HIP(hipMemcpy(&err, fdw.err, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) {
-      FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
-      set_error("fused decode: an in-launch fan-in timed out (a block was not resident?)");
-      throw hip_failure();
+    if (err) FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
+    return err != 0;
+  }
+
+  // enqueue n_steps decode steps for seqs from the host state (n_past, last_tok): fa_llm_generate_begin's body, also
+  // the re-run of a chunk whose fused layer timed out
+  void enqueue_steps(const int32_t* seqs, int n_seqs, int n_steps) {
+    std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0);
+    for (int i = 0; i < n_seqs; ++i) {
+      sq[i] = seqs[i];
+      ps[i] = n_past[seqs[i]];
+      cur[i] = last_tok[seqs[i]];
     }
+    FA_HIP(hipMemcpyAsync(d_tok_seq, sq.data(), n_seqs * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tok_pos, ps.data(), n_seqs * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tok_cur, cur.data(), n_seqs * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, stream));
+    // input row of the first step (later steps get theirs from the sampler launch)
+    fa::embed_rows(tok_embd.q, tok_embd.d, d_tok_cur, n_seqs, lc.n_embd, 0, lx, stream);
+    // the sampler reads its parameters from device memory, so the captured step graph serves every setting.
+    // Profiling runs eager (event nodes inside graphs do not time individual nodes on ROCm 7.2).
+    if (use_graphs && !prof) {
+      int st = 0;
+      if (graph_steps > 1 && n_steps >= graph_steps) {
+        const hipGraphExec_t exk = step_graph(n_seqs, graph_steps);
+        for (; st + graph_steps <= n_steps; st += graph_steps) FA_HIP(hipGraphLaunch(exk, stream));
+      }
+      if (st < n_steps) {
+        const hipGraphExec_t ex = step_graph(n_seqs);
+        for (; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, stream));
+      }
+    } else {
+      for (int st = 0; st < n_steps; ++st) {
+        prof_pos = ps[0] + st;  // the profiled fused layer's K/V bytes (batch 1)
+        decode_step(n_seqs);
+      }
+    }
+    // the sampled tokens land in pinned host memory; fa_llm_generate_end waits for them (the host may work meanwhile)
+    FA_HIP(hipMemcpyAsync(h_hist, d_tok_hist, (size_t)n_seqs * hist_max * 4, hipMemcpyDeviceToHost, stream));
+    FA_HIP(hipEventRecord(ev_gen, stream));
+  }
+
+  // the landed chunk ran on the fused layer and a fan-in timed out: switch this engine to the 5-launch layer for good
+  // and decode the chunk again from the same host state (positions and input tokens were not advanced; the re-run
+  // overwrites the chunk's K/V rows before any step reads them, and its draws are keyed on the same (seed, seq, pos))
+  void recover_fused_chunk() {
+    log(3, "fused decode: an in-launch fan-in timed out (a group was not co-resident); re-running the chunk on the "
+           "5-launch layer and keeping it for this engine");
+    use_fused = 0;
+    debug_flags &= ~2;
+    for (auto& g : step_graphs) FA_HIP(hipGraphExecDestroy(g.second));
+    step_graphs.clear();  // captured steps bake the layer structure in
+    ++fused_recoveries;
+    enqueue_steps(gen_seqs.data(), (int)gen_seqs.size(), gen_steps);
+    FA_HIP(hipEventSynchronize(ev_gen));
+    FA_REQUIRE(!fused_error(), "decode chunk re-run: error flag set on the 5-launch layer");
   }
 
   // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
@@ -1437,7 +1490,13 @@ int fa_set_decode_fused(fa_engine* h, int32_t on) {
 
 int fa_set_debug(fa_engine* h, int32_t flags) {
   FA_API_BEGIN
-  h->e->debug_flags = flags;
+  Engine* e = h->e;
+  FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
+  if ((e->debug_flags ^ flags) & 2) {  // the fused-layer hook is a launch argument: captured steps must be re-made
+    for (auto& g : e->step_graphs) FA_HIP(hipGraphExecDestroy(g.second));
+    e->step_graphs.clear();
+  }
+  e->debug_flags = flags;
   FA_API_END
 }
 
@@ -1575,7 +1634,6 @@ int fa_llm_generate_begin(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int
   Engine* e = h->e;
   FA_REQUIRE(!e->gen_pending, "a generate call is already in flight (fa_llm_generate_end first)");
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs && n_steps >= 1 && n_steps <= e->hist_max, "generate args");
-  std::vector<int> sq(n_seqs), ps(n_seqs), cur(n_seqs), zero(n_seqs, 0);
   std::vector<char> seen(e->lc.max_seqs, 0);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = seqs[i];
@@ -1584,39 +1642,10 @@ int fa_llm_generate_begin(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int
     seen[q] = 1;
     FA_REQUIRE(e->last_tok[q] >= 0, "sequence has no sampled token (prefill first)");
     FA_REQUIRE(e->n_past[q] + n_steps <= e->lc.n_ctx, "generate exceeds n_ctx");
-    sq[i] = q;
-    ps[i] = e->n_past[q];
-    cur[i] = e->last_tok[q];
   }
-  FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
-  FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
-  FA_HIP(hipMemcpyAsync(e->d_tok_cur, cur.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
-  FA_HIP(hipMemcpyAsync(e->d_step, zero.data(), n_seqs * 4, hipMemcpyHostToDevice, e->stream));
-  // input row of the first step (later steps get theirs from the sampler launch)
-  fa::embed_rows(e->tok_embd.q, e->tok_embd.d, e->d_tok_cur, n_seqs, e->lc.n_embd, 0, e->lx, e->stream);
   e->set_sampling(s);
-  // the sampler reads its parameters from device memory, so the captured step graph serves every setting.
-  // Profiling runs eager (event nodes inside graphs do not time individual nodes on ROCm 7.2).
-  if (e->use_graphs && !e->prof) {
-    int st = 0;
-    if (e->graph_steps > 1 && n_steps >= e->graph_steps) {
-      const hipGraphExec_t exk = e->step_graph(n_seqs, e->graph_steps);
-      for (; st + e->graph_steps <= n_steps; st += e->graph_steps) FA_HIP(hipGraphLaunch(exk, e->stream));
-    }
-    if (st < n_steps) {
-      const hipGraphExec_t ex = e->step_graph(n_seqs);
-      for (; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, e->stream));
-    }
-  } else {
-    for (int st = 0; st < n_steps; ++st) {
-      e->prof_pos = ps[0] + st;  // the profiled fused layer's K/V bytes (batch 1)
-      e->decode_step(n_seqs);
-    }
-  }
-  // the sampled tokens land in pinned host memory; fa_llm_generate_end waits for them (the host may work meanwhile)
-  FA_HIP(hipMemcpyAsync(e->h_hist, e->d_tok_hist, (size_t)n_seqs * e->hist_max * 4, hipMemcpyDeviceToHost, e->stream));
-  FA_HIP(hipEventRecord(e->ev_gen, e->stream));
-  e->gen_seqs = sq;
+  e->enqueue_steps(seqs, n_seqs, n_steps);
+  e->gen_seqs.assign(seqs, seqs + n_seqs);
   e->gen_steps = n_steps;
   e->gen_pending = true;
   FA_API_END
@@ -1630,7 +1659,7 @@ int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
   FA_HIP(hipEventSynchronize(e->ev_gen));
   const int n_seqs = (int)e->gen_seqs.size(), n_steps = e->gen_steps;
   e->prof_collect();
-  if (n_seqs <= fa::FUSED_MAX_M) e->check_fused_error();
+  if (n_seqs <= fa::FUSED_MAX_M && e->fused_error()) e->recover_fused_chunk();
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = e->gen_seqs[i];

@@ -164,7 +164,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s, int M = 1);
+                      const FusedDecodeWork& fw, hipStream_t s, int M = 1, int dbg_drop = 0);
 // M tokens (rows of x / xsum, slabs of the workspace); M = 1: the batch-1 layer
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,

@@ -2563,6 +2563,25 @@ void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s) {
 // 1.5-1.9 us plus the weight stream's first-byte latency (profiles/); the fan-ins here are 16 / 32 blocks
 // deep and the slices' weights are already in registers when their inputs arrive. Every block of a launch is
 // resident (128 / 256 blocks, at most 2 per CU); every spin is bounded: a timeout sets *err and falls through.
+// Every in-launch wait is bounded by time, not spin count: SPIN_TICKS of the 100 MHz reference clock (10 ms) from
+// the first poll (checked every 16 polls). A group that is not co-resident (another kernel holding CUs) then costs a
+// few ms per wait instead of seconds; the timed-out block sets *err and falls through, and fa_llm_generate_end re-runs
+// the chunk on the 5-launch layer (engine.cpp, recover_fused_chunk).
+constexpr uint64_t SPIN_TICKS = 1000000;
+struct SpinDeadline {
+  uint64_t t0 = 0;
+  unsigned n = 0;
+  __device__ __forceinline__ bool expired() {
+    if ((++n & 15) != 1) return false;
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (n == 1) {
+      t0 = t;
+      return false;
+    }
+    return t - t0 > SPIN_TICKS;
+  }
+};
+
 __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) {
   __shared__ unsigned s_target;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 payload stores
@@ -2574,10 +2593,10 @@ __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) 
   __syncthreads();
   if (threadIdx.x < 64) {
     const unsigned target = s_target;
-    unsigned spins = 0;
+    SpinDeadline dl;
     while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
+      if (dl.expired()) {
         if (threadIdx.x == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -2617,6 +2636,7 @@ struct AttnOArgs {
   const __half* wqkv_d;
   unsigned* cnt_qkv;   // [KV][CNT_LINE]
   unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
+  int dbg_drop;        // test hook (fa_set_debug bit 1): block (0, 0) publishes no q|k|v granules -> fan-in timeout
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
@@ -2650,9 +2670,9 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     a.cnt += mt * a.KV * CNT_LINE;
     a.partials += (int64_t)mt * a.KV * FS * APART;
     if constexpr (QKV) {
-      a.x += (int64_t)mt * 1024;
-      a.psum += (int64_t)mt * FUSED_PARTS * 1024;
-      if (a.xsum) a.xsum += (int64_t)mt * 1024;
+      a.x += (int64_t)mt * a.E;
+      a.psum += (int64_t)mt * FUSED_PARTS * a.E;
+      if (a.xsum) a.xsum += (int64_t)mt * a.E;
       a.cnt_qkv += mt * a.KV * CNT_LINE;
       a.gqkv += (int64_t)mt * nq;
     }
@@ -2672,7 +2692,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     xv[0] = x4.x; xv[1] = x4.y; xv[2] = x4.z; xv[3] = x4.w;
 #pragma unroll
     for (int p = 0; p < FUSED_PARTS; ++p) {  // layer 0: a zero block (no branch around the loads)
-      const float4 f = *reinterpret_cast<const float4*>(a.psum + p * 1024 + threadIdx.x * 4);
+      const float4 f = *reinterpret_cast<const float4*>(a.psum + p * a.E + threadIdx.x * 4);
       pv[p][0] = f.x; pv[p][1] = f.y; pv[p][2] = f.z; pv[p][3] = f.w;
     }
     const float4 w4 = *reinterpret_cast<const float4*>(a.norm_w + threadIdx.x * 4);
@@ -2767,7 +2787,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       float yv = y[0];
 #pragma unroll
       for (int r = 1; r < QR; ++r) yv = lane == r ? y[r] : yv;
-      if (lane < QR)
+      if (lane < QR && !(a.dbg_drop && g == 0 && sp == 0))
         __hip_atomic_store(a.gqkv + qrow0 + QR * wave + lane, ((unsigned long long)ep_qkv << 32) | __float_as_uint(yv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -2779,11 +2799,11 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       const int grow = (sg < GQ ? (g * GQ + sg) * D : sg == GQ ? (a.H + g) * D : (a.H + a.KV + g) * D) + lr % D;
       const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.gqkv, (a.H + 2 * a.KV) * D * 8);
       f4v gv;
-      unsigned spins = 0;
+      SpinDeadline dl;
       for (;;) {
         gv = ld_sc1_f4(rg, grow * 8);
         if (__float_as_uint(gv.y) == ep_qkv && __float_as_uint(gv.w) == ep_qkv) break;
-        if (++spins > (1u << 22)) {
+        if (dl.expired()) {
           __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
@@ -2892,7 +2912,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s, int M) {
+                      const FusedDecodeWork& fw, hipStream_t s, int M, int dbg_drop) {
   FA_REQUIRE(M >= 1 && M <= FUSED_MAX_M && M <= wk.max_split_tokens, "qkv_attn_o_fused: 1 <= M <= FUSED_MAX_M");
   FA_REQUIRE(H == KV * GQ && KV == FUSED_PARTS && E == FO_ROWS * ASPLIT && E == 1024 &&
                  (GQ + 2) * 128 == FQ_ROWS * ASPLIT,
@@ -2902,7 +2922,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err,
               x, psum ? psum : fw.pzero, psum ? xsum : nullptr, norm_w, wqkv_q, wqkv_d,
-              fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv};
+              fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, M), dim3(AWV * 64), 0, s, a);
 }
@@ -3052,7 +3072,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
   if (pc < ct) {
     const unsigned e = pc == 0 ? ep[0] : ep[CT - 1];
     const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act + (int64_t)(m0 + pc) * 2 * f.F, f.F * 8);
-    unsigned spins = 0;
+    SpinDeadline dl;
     const int off = (FF_GROUP_ROWS * grp + 4 * pt) * 8;
     for (;;) {
       gv0 = ld_sc1_f4(ra, off);
@@ -3060,7 +3080,7 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
       if (__float_as_uint(gv0.y) == e && __float_as_uint(gv0.w) == e && __float_as_uint(gv1.y) == e &&
           __float_as_uint(gv1.w) == e)
         break;
-      if (++spins > (1u << 22)) {
+      if (dl.expired()) {
         __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

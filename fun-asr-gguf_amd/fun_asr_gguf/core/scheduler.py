@@ -45,12 +45,15 @@ class ContinuousBatcher:
         self.admit_min = admit_min
         self.stats = {}
 
-    @staticmethod
-    def _begin(eng, jobs, queue, samp):
-        # short chunks while clips wait (a freed slot is refilled soon), else up to GEN_CHUNK steps
-        rem = [j.state.remaining() for j in jobs]
-        chunk = min(GEN_CHUNK, max(rem) if not queue else max(4, min(rem)))
+    def _begin(self, eng, jobs, queue, n_free, admit_min, samp, landed=0):
+        # while clips wait: a chunk that ends when enough slots have reached their length cap for the next admission
+        # (stop tokens can end sequences sooner: seen at the chunk's end); otherwise up to GEN_CHUNK steps
+        rem = sorted(j.state.remaining() - landed for j in jobs)  # landed: steps fed to no state yet
+        need = min(admit_min, len(queue)) - n_free if queue else 0
+        chunk = rem[min(need, len(rem)) - 1] if need > 0 else rem[-1]
+        chunk = max(1, min(GEN_CHUNK, chunk))
         eng.llm_generate_begin([j.slot for j in jobs], chunk, **samp)
+        self.n_chunks += 1
         return list(jobs), chunk
 
     @staticmethod
@@ -85,7 +88,9 @@ class ContinuousBatcher:
         # single-sequence arithmetic: results are exactly the one-clip-at-a-time results, whatever the grouping
         alone = S <= invariant_width(eng)
         n_admit = n_encode_batches = 0
-        t_enc = t_pre = 0.0
+        t_enc = t_pre = t_wait = 0.0
+        self.n_chunks = 0
+        t_run = time.perf_counter()
 
         def admit(k):
             nonlocal n_admit, n_encode_batches, t_enc, t_pre
@@ -152,9 +157,11 @@ class ContinuousBatcher:
                         continue
                     if not active:
                         break
-                    pending = self._begin(eng, active, queue, samp)
+                    pending = self._begin(eng, active, queue, len(free), admit_min, samp)
                 jobs, chunk = pending
+                t = time.perf_counter()
                 toks = eng.llm_generate_end()
+                t_wait += time.perf_counter() - t
                 pending = None
                 # sequences this chunk leaves unfinished, decided from the token ids alone (stop ids, n_predict), get
                 # the next chunk enqueued BEFORE the host detokenises this one (host work overlaps the GPU's) -- unless
@@ -163,7 +170,7 @@ class ContinuousBatcher:
                 cont = [j for row, j in enumerate(jobs) if self._continues(j, toks[row], chunk, stop_ids)]
                 n_free = len(free) + len(jobs) - len(cont)
                 if cont and not (queue and n_free >= min(admit_min, len(queue))):
-                    pending = self._begin(eng, cont, queue, samp)
+                    pending = self._begin(eng, cont, queue, n_free, admit_min, samp, landed=chunk)
                 cs = set(id(j) for j in cont)
                 for row, j in enumerate(jobs):
                     j.state.feed(toks[row][:chunk])
@@ -185,8 +192,9 @@ class ContinuousBatcher:
                                                             attempts=RETRY_ATTEMPTS - 1)
             for j, r in zip(retry, rs):
                 done[j.idx] = (j, r)
-        self.stats = dict(admissions=n_admit, encode_batches=n_encode_batches, retried=len(retry),
-                          encode_s=t_enc, prefill_s=t_pre)
+        self.stats = dict(admissions=n_admit, encode_batches=n_encode_batches, retried=len(retry), chunks=self.n_chunks,
+                          encode_s=round(t_enc, 4), prefill_s=round(t_pre, 4), generate_wait_s=round(t_wait, 4),
+                          total_s=round(time.perf_counter() - t_run, 4))
         out = []
         for i in range(len(chunks)):
             j, r = done[i]

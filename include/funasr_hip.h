@@ -109,7 +109,9 @@ int fa_encode_fetch(fa_engine* e, float* audio_embd_out, int64_t tgt_stride, int
 int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* frames_out, int64_t out_stride,
                     int32_t* n_out);
 /* Debug hooks (tests): flags bit 0 keeps clip 0's embedded LFR features (x*sqrt(512)+PE, [T, d_in]) of
- * the next fa_encode; fa_encode_tap(e, 0, out, n) copies them out. */
+ * the next fa_encode; fa_encode_tap(e, 0, out, n) copies them out. Bit 1 makes one block of the fused decode layer
+ * withhold its q|k|v hand-off, forcing the in-launch fan-in timeout (10 ms per wait): fa_llm_generate_end then
+ * re-runs the chunk on the 5-launch layer, which the engine keeps from then on (the bit clears itself). */
 /* Encoder precision: 0 = fp32 graph (Fun-ASR-Nano-Encoder-Adaptor.fp32.onnx / CTC.fp32.onnx), 1 = the float16
  * graphs of 02-Quantize-ONNX.py:13-27 (fp16 weights and op outputs, LayerNorm in fp32, fp16 input audio;
  * replaces the dtype switch of nano_onnx.py:84,101). The fp16 weight copies are built on the next encode. */
@@ -158,6 +160,9 @@ int fa_llm_generate(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n
  * in between (the llama_decode loop of decoder.py:91-98 has no such overlap: its sampling is on the host). */
 int fa_llm_generate_begin(fa_engine* e, const int32_t* seqs, int32_t n_seqs, int32_t n_steps, const fa_sampling* s);
 int fa_llm_generate_end(fa_engine* e, int32_t* tokens_out);
+/* (fa_llm_generate_end: when the chunk ran on the fused small-batch layer and one of its in-launch fan-ins timed out --
+ * a group of blocks not co-resident because another kernel held CUs -- the chunk is decoded again on the 5-launch layer
+ * from the same positions and input tokens, and the engine keeps that layer; the tokens returned are the re-run's.) */
 /* Logits [n_vocab] of sequence `seq` from the most recent forward (fa_llm_prefill, or the last step of
  * fa_llm_generate) when that forward included it; FA_ERR_ARG otherwise (test hook; llama_get_logits_ith). */
 int fa_llm_logits(fa_engine* e, int32_t seq, float* out);

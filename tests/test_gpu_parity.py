@@ -609,3 +609,35 @@ def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     for q in range(5):
         assert len(got[q]) == n_steps + 1, (q, len(got[q]))
         assert got[q] == singles[q], q
+
+
+def test_fused_timeout_recovers_on_five_launch_layer():
+    """A fan-in timeout in the fused decode layer (forced: fa_set_debug bit 1 makes one block withhold its q|k|v
+    hand-off; every wait is bounded at 10 ms) is not an error to the caller: fa_llm_generate_end re-runs the chunk on the
+    5-launch layer from the same positions and tokens, and the engine keeps that layer (invariant width drops to 1).
+    The tokens and logits equal a run on the 5-launch layer from the start."""
+    from fun_asr_gguf import _native
+    from oracle import qwen3 as oq
+    cfg = dict(synth.LLM_TINY, n_ctx=256, max_seqs=2)
+    m = oq.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=256)
+    rng = np.random.default_rng(77)
+    prompt = m.embed_prompt(rng.integers(0, 4096, 40))
+    runs = []
+    for forced in (True, False):
+        eng = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)
+        eng.synthetic_weights(0)
+        if not forced:
+            eng.set_decode_fused(0)
+        eng.llm_reset(0)
+        first = eng.llm_prefill(0, prompt)
+        if forced:
+            assert eng.llm_invariant_width() > 1
+            eng.lib.fa_set_debug(eng.h, 2)
+        toks = [int(t) for t in eng.llm_generate([0], 3)[0]]
+        lg = eng.llm_logits(0)
+        more = [int(t) for t in eng.llm_generate([0], 2)[0]]
+        runs.append((first, toks, lg, more, eng.llm_invariant_width()))
+        eng.close()
+    (f1, t1, l1, m1, w1), (f0, t0, l0, m0, w0) = runs
+    assert w1 == 1 and f1 == f0 and t1 == t0 and m1 == m0
+    assert np.array_equal(l1, l0)
