@@ -200,7 +200,7 @@ def c3_varlen_leg(n_clips, batch, device, model, barrier, dist):
                         f"U[128, 384] (mean {np.mean(lens):.0f} tokens, pinned per clip)", "unit": "audio_s/s",
             "continuous": res["continuous"], "static": res["static"],
             "speedup": round(res["continuous"]["value"] / res["static"]["value"], 3),
-            "admissions": st.get("admissions"), "encode_batches": st.get("encode_batches")}
+            "scheduler": st}
 
 
 def c4_leg(steps, warmup, device, model, barrier, dist):
@@ -260,7 +260,7 @@ def main():
     ap.add_argument("--c3-batch", type=int, default=32, help="clips per step of the C3 leg (0 = skip)")
     ap.add_argument("--c3-steps", type=int, default=2)
     ap.add_argument("--c4-steps", type=int, default=2)
-    ap.add_argument("--c3-varlen", type=int, default=64, help="clips of the variable-length C3 leg (0 = skip)")
+    ap.add_argument("--c3-varlen", type=int, default=192, help="clips of the variable-length C3 leg (0 = skip)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (300 s long-audio) leg")
     args = ap.parse_args()
 

@@ -156,7 +156,9 @@ struct Engine {
   // 0.698 / 0.933 / 0.915 ms vs 0.594 / 0.709 / 0.812 / 0.935 / 1.000 / 1.047 ms on the 5-launch layer; M 7 / 8 1.213 /
   // 1.261 vs 1.070 / 1.073 ms (the AB launch's token slabs, 128 blocks each, no longer fit the chip at once)
   int fused_max_m = 6;
-  // decode steps per captured graph (FUNASR_GRAPH_STEPS): chunks replay graphs of this many steps, then single steps
+  // decode steps per captured graph (FUNASR_GRAPH_STEPS): chunks replay graphs of this many steps, then single steps.
+  // Measured (graph-replayed, full model): 1 / 8 / 32 steps per graph -> batch 1 0.489 / 0.499 / 0.525 ms per step,
+  // batch 32 1.223 / 1.239 / 1.358 ms: one step per graph replay stays the default
   int graph_steps = 1;
   int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after a fused fan-in timeout
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
@@ -1211,7 +1213,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMM_F32_SPLIT")) fa::g_gemm_f32_split = atoi(g) != 0;
     {  // process-wide split-K shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_SK_MIN_BLOCKS");
-      fa::g_sk_min_blocks = g ? std::max(1, atoi(g)) : 256;
+      fa::g_sk_min_blocks = g ? std::max(1, atoi(g)) : 128;
     }
     if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));

@@ -1254,7 +1254,10 @@ int g_gemm_q8_kw = 1;  // 0: split-K block kernel for every shape (A/B switch, F
 // split-K shape: NBW q8_0 blocks per wave (8, 4 or 2: one load round trip) and KS = nb / (waves per matrix x NBW)
 // splits; the largest NBW whose split count fills the chip (>= 256 blocks), else the most splits. lm_head's argmax
 // needs whole sums: one split.
-int g_sk_min_blocks = 256;  // split-K: the fewest blocks a shape must reach before fewer splits are preferred
+// split-K: the fewest blocks a shape must reach before fewer splits are preferred. Measured (graph-replayed decode
+// step, full model): 256 / 192 / 128 / 96 -> batch 32 1.213 / 1.191 / 1.186 / 1.202 ms, batch 16 1.101 / 1.084 /
+// 1.068 / 1.084 ms: q|k|v and gate|up take one split fewer (the split-K seam costs more than the emptier chip)
+int g_sk_min_blocks = 128;
 void gemm_sk_shape(int O, int M, int K, int epi, int* nbw, int* ks) {
   const int tiles = cdiv(O, 32) * cdiv(M, 32), nb = K / 32, wpm = epi == 2 ? 2 : 4;
   *nbw = 0;
@@ -1350,7 +1353,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   if (a.ssp) {  // batched decode (M <= 32): inputs quantised by the previous residual epilogue, rstd applied here
     switch (epi * 1000 + NBW * 100 + ksm) {
 #define SKN(E, N, Q) case E * 1000 + N * 100 + Q: hipLaunchKernelGGL((k_gemm_q8_sk<E, N, Q, true>), grid, dim3(256), 0, s, a, K, KS); return;
-      SKN(0, 4, 4) SKN(0, 8, 1) SKN(2, 4, 4) SKN(3, 8, 1)
+      SKN(0, 4, 4) SKN(0, 8, 1) SKN(2, 4, 4) SKN(2, 8, 4) SKN(3, 8, 1)
 #undef SKN
       default: FA_REQUIRE(false, "gemm_q8: normalised-input shape not instantiated");
     }
