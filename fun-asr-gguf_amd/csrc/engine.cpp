@@ -1200,7 +1200,18 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     FA_REQUIRE(llm->head_dim == 128 && llm->n_head == 2 * llm->n_head_kv, "decoder head layout");
     FA_REQUIRE(llm->n_embd % 1024 == 0 && llm->n_ff % 1024 == 0, "decoder widths must be multiples of 1024");
     FA_HIP(hipSetDevice(device));
-    FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    if (const char* m = getenv("FUNASR_CU_MASK")) {  // experiment hook: comma-separated hex 32-bit CU mask words
+      std::vector<uint32_t> words;
+      for (const char* p = m; *p;) {
+        char* end = nullptr;
+        words.push_back((uint32_t)strtoul(p, &end, 16));
+        if (!end || end == p) break;
+        p = *end == ',' ? end + 1 : end;
+      }
+      FA_HIP(hipExtStreamCreateWithCUMask(&e->stream, (uint32_t)words.size(), words.data()));
+    } else {
+      FA_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    }
     if (const char* g = getenv("FUNASR_GRAPHS")) e->use_graphs = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_KW")) fa::g_gemm_q8_kw = atoi(g) != 0;
     // A/B knobs of the decode GEMV: fused-GEMV batch limit (0..7; lm_head partials are sized for <= 7) and
@@ -1214,6 +1225,10 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     {  // process-wide split-K shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_SK_MIN_BLOCKS");
       fa::g_sk_min_blocks = g ? std::max(1, atoi(g)) : 128;
+    }
+    {
+      const char* g = getenv("FUNASR_LM_HEAD_MT6");
+      fa::g_lm_head_mt6 = g ? atoi(g) != 0 : 1;
     }
     if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));

@@ -107,6 +107,7 @@ int lm_head_parts(int O, int M);
 int gemm_k_splits(int O, int M, int K, int epi);  // K splits of the split-K GEMM form for this shape
 extern int g_attn_lean;    // -1 auto, 0/1 force the 128-VGPR attention variant (A/B)
 extern int g_attn_blocks;  // attention key-split target (blocks per launch), 1024 by default
+extern int g_lm_head_mt6;    // LM head of 3-6 token batches in one block row (default 1)
 extern int g_sk_min_blocks;  // split-K shape choice: fewest blocks before fewer splits are preferred (default 256)
 extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 5); MFMA GEMM above
 extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)

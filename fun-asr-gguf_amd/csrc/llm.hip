@@ -1295,6 +1295,7 @@ int gemv_rows_per_wave(int O) {
 // work per block than the saved weight re-reads (MT 4 / 8: slower).
 int g_gemv_small_max = 5;
 int g_gemv_mt = 2;
+int g_lm_head_mt6 = 1;  // LM head of 3-6 token batches: one block row for every token (FUNASR_LM_HEAD_MT6=0: pairs)
 
 bool gemv_small(int M) { return M <= g_gemv_small_max; }
 
@@ -1318,7 +1319,13 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
   if (gemv_small(a.M) && fused) {
     FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemv_q8: n_part");
-    // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens)
+    // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens). The LM head
+    // (165 MB of rows) takes all of a 3-6 token batch in one block row: re-streaming it per token pair cost 86 us per
+    // launch at 6 tokens. A token's arithmetic does not depend on MT (compute_group runs it per token).
+    if (epi == 3 && K == 1024 && a.M >= 3 && a.M <= 6 && g_lm_head_mt6) {
+      launch_gemv<1, 6, true, 3>(a, s);
+      return;
+    }
     const int mt = a.M <= 2 ? 1 : std::min(g_gemv_mt, a.M);
     if (mt <= 1) launch_gemv_fused<1>(K, epi, a, s);
     else launch_gemv_fused<2>(K, epi, a, s);

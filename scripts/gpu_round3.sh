@@ -22,7 +22,7 @@ python3 scripts/pmc_traffic.py gpurun_out/pmc/pmc_results.db gpurun_out/pmc_gemv
 rm -rf gpurun_out/pmc
 for mode in bf16x3 f32; do
   rm -rf gpurun_out/pmcm
-  FUNASR_ENC_GEMM=$mode timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
+  FUNASR_GRAPHS=0 FUNASR_ENC_GEMM=$mode timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE \
     -d gpurun_out/pmcm -o pmc -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --c3-batch 32 --c3-steps 1 --no-c4 --c3-varlen 0 \
     > gpurun_out/pmcm_$mode.log 2>&1 || { echo "pmc mfma pass failed rc=$?"; tail -30 gpurun_out/pmcm_$mode.log; exit 1; }
   db=$(find gpurun_out/pmcm -name "*results.db" | head -1)
