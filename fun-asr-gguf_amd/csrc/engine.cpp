@@ -196,7 +196,14 @@ struct Engine {
     return (T*)p;
   }
   ~Engine() {
+    for (auto& l : enc_lanes)
+      if (l.s) hipStreamSynchronize(l.s);
     if (stream) hipStreamSynchronize(stream);
+    for (auto& l : enc_lanes) {
+      if (l.done) hipEventDestroy(l.done);
+      if (l.s) hipStreamDestroy(l.s);
+    }
+    if (ev_fork) hipEventDestroy(ev_fork);
     for (auto& g : step_graphs) hipGraphExecDestroy(g.second);
     for (auto& e : ev_pool) {
       hipEventDestroy(e.first);
@@ -771,6 +778,101 @@ struct Engine {
       enc_lin(hbuf, d_out, b.w1, b.b1, ffn, d_out / 4, rows, d_out / 4, d_out, 1);
       enc_lin(ffn, d_out / 4, b.w2, b.b2, out, d_out, rows, d_out, d_out / 4, 0, out, d_out);
     }
+  }
+
+  // ---- independent-clip encodes (fa_set_encode_mode(1)): every clip runs the single-clip encode (its own row count,
+  // tiles, key splits: the arithmetic of encoding it alone) in a lane of its own -- rows [b tl_max, +tl_max) of the
+  // batch arenas, its own split-K / attention workspaces, its own HIP stream -- so up to kEncLanes one-clip encodes
+  // (each too small to fill the chip) run concurrently. The fetch / collapse calls then read clip b at row b tl_max.
+  static constexpr int kEncLanes = 8;
+  struct EncBind {
+    hipStream_t stream;
+    AttnF32Work attn;
+    GemmF32Work gemm;
+    float *xp, *mean_part, *power, *mel, *xa, *hbuf, *qkv, *att, *mem, *ffn, *enc, *ad, *cbuf, *ctc_pval;
+    int *ctc_pidx, *ctc_ids;
+    int64_t* d_nsamp;
+    int *d_tmel, *d_tlfr, *d_tgt, *d_ctclen;
+  };
+  struct EncLane {
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    AttnF32Work attn;
+    GemmF32Work gemm;
+  };
+  std::vector<EncLane> enc_lanes;
+  int encode_mode = 0;  // 0: padded batch; 1: independent clips in concurrent lanes
+  hipEvent_t ev_fork = nullptr;
+
+  EncBind enc_bind() const {
+    return EncBind{stream, enc_attn_wk, enc_gemm_wk, xp, mean_part, power, mel, xa, hbuf, qkv, att, mem, ffn, enc, ad, cbuf,
+                   ctc_pval, ctc_pidx, ctc_ids, d_nsamp, d_tmel, d_tlfr, d_tgt, d_ctclen};
+  }
+  void enc_rebind(const EncBind& b) {
+    stream = b.stream; enc_attn_wk = b.attn; enc_gemm_wk = b.gemm; xp = b.xp; mean_part = b.mean_part; power = b.power;
+    mel = b.mel; xa = b.xa; hbuf = b.hbuf; qkv = b.qkv; att = b.att; mem = b.mem; ffn = b.ffn; enc = b.enc; ad = b.ad;
+    cbuf = b.cbuf; ctc_pval = b.ctc_pval; ctc_pidx = b.ctc_pidx; ctc_ids = b.ctc_ids; d_nsamp = b.d_nsamp;
+    d_tmel = b.d_tmel; d_tlfr = b.d_tlfr; d_tgt = b.d_tgt; d_ctclen = b.d_ctclen;
+  }
+  EncLane& enc_lane(int i) {
+    if ((int)enc_lanes.size() <= i) enc_lanes.resize(i + 1);
+    EncLane& l = enc_lanes[i];
+    if (!l.s) {
+      FA_HIP(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
+      FA_HIP(hipEventCreateWithFlags(&l.done, hipEventDisableTiming));
+      l.attn = enc_attn_wk;
+      l.attn.part = alloc<float>(l.attn.part_n);
+      l.attn.cnt = alloc<int>(l.attn.cnt_n * CNT_LINE);
+      FA_HIP(hipMemset(l.attn.cnt, 0, l.attn.cnt_n * CNT_LINE * sizeof(int)));
+      l.gemm = enc_gemm_wk;
+      l.gemm.part = alloc<float>(l.gemm.part_n);
+      l.gemm.cnt = alloc<int>(l.gemm.cnt_n * CNT_LINE);
+      FA_HIP(hipMemset(l.gemm.cnt, 0, l.gemm.cnt_n * CNT_LINE * sizeof(int)));
+    }
+    return l;
+  }
+
+  void encode_independent(const float* pcm, const int64_t* n_samples, int batch, int64_t stride) {
+    FA_REQUIRE(batch >= 1 && batch <= max_batch, "batch out of range");
+    if (enc_fp16) prepare_fp16();
+    else if (enc_gemm) prepare_bf3();
+    if (!ev_fork) FA_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    FA_HIP(hipEventRecord(ev_fork, stream));
+    const EncBind base = enc_bind();
+    const int d = ec.d_model, wmax = std::max({ec.d_in, ec.d_llm, d}), nt = cdiv(ec.ctc_vocab, 64);
+    const size_t T = tl_max;
+    std::vector<int> tl(batch), tg(batch), cl(batch);
+    try {
+      for (int b = 0; b < batch; ++b) {
+        EncLane& l = enc_lane(b % kEncLanes);
+        if (b >= kEncLanes) FA_HIP(hipStreamWaitEvent(l.s, l.done, 0));  // the lane's previous clip (same workspaces)
+        FA_HIP(hipStreamWaitEvent(l.s, ev_fork, 0));
+        EncBind lb = base;
+        lb.stream = l.s; lb.attn = l.attn; lb.gemm = l.gemm;
+        lb.xp += b * xp_stride_max; lb.mean_part += b * 64; lb.power += b * (size_t)tm_max * 204;
+        lb.mel += b * (size_t)tm_max * ec.n_mels; lb.xa += b * T * wmax; lb.hbuf += b * T * wmax;
+        lb.qkv += b * T * 3 * std::max(d, ec.d_llm); lb.att += b * T * std::max(d, ec.d_llm); lb.mem += b * T * d;
+        lb.ffn += b * T * std::max({ec.d_ffn, ec.adaptor_ffn, ec.ctc_ffn}); lb.enc += b * T * d; lb.ad += b * T * ec.d_llm;
+        lb.cbuf += b * T * d; lb.ctc_pval += b * T * nt; lb.ctc_pidx += b * T * nt; lb.ctc_ids += b * T;
+        lb.d_nsamp += b; lb.d_tmel += b; lb.d_tlfr += b; lb.d_tgt += b; lb.d_ctclen += b;
+        enc_rebind(lb);
+        encode_device(pcm + (size_t)b * stride, n_samples + b, 1, stride);
+        FA_HIP(hipEventRecord(l.done, l.s));
+        tl[b] = h_tlfr[0];
+        tg[b] = h_tgt[0];
+        cl[b] = h_ctclen[0];
+        enc_rebind(base);
+      }
+    } catch (...) {
+      enc_rebind(base);
+      throw;
+    }
+    for (int i = 0; i < std::min(batch, kEncLanes); ++i) FA_HIP(hipStreamWaitEvent(stream, enc_lanes[i].done, 0));
+    h_tlfr = tl;
+    h_tgt = tg;
+    h_ctclen = cl;
+    last_batch = batch;
+    last_tstride = tl_max;  // clip b's rows start at b tl_max
   }
 
   void encode_device(const float* pcm, const int64_t* n_samples, int batch, int64_t stride) {
@@ -1395,7 +1497,8 @@ int fa_encode_device(fa_engine* h, const float* d_pcm, const int64_t* n_samples,
     FA_REQUIRE((int64_t)batch * stride <= e->pcm_uploaded, "fa_encode_device(NULL): upload the PCM first");
     d_pcm = e->d_pcm;
   }
-  e->encode_device(d_pcm, n_samples, batch, stride);
+  if (e->encode_mode == 1 && batch > 1) e->encode_independent(d_pcm, n_samples, batch, stride);
+  else e->encode_device(d_pcm, n_samples, batch, stride);
   FA_API_END
 }
 
@@ -1449,7 +1552,8 @@ int fa_encode(fa_engine* h, const float* pcm, const int64_t* n_samples, int32_t 
   FA_REQUIRE(stride <= std::max<int64_t>(e->max_samples, 16000), "stride > max_samples");
   FA_HIP(hipMemcpyAsync(e->d_pcm, pcm, (size_t)batch * stride * 4, hipMemcpyHostToDevice, e->stream));
   e->pcm_uploaded = (int64_t)batch * stride;
-  e->encode_device(e->d_pcm, n_samples, batch, stride);
+  if (e->encode_mode == 1 && batch > 1) e->encode_independent(e->d_pcm, n_samples, batch, stride);
+  else e->encode_device(e->d_pcm, n_samples, batch, stride);
   int r = fa_encode_fetch(h, audio_embd_out, tgt_stride, ctc_ids_out, ids_stride, t_lfr_out, target_len_out, enc_out);
   if (r != FA_OK) return r;
   FA_API_END
@@ -1476,6 +1580,13 @@ int fa_ctc_collapse(fa_engine* h, int32_t blank_id, int32_t* ids_out, int32_t* f
     n_out[b] = n[b];
   }
   FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_set_encode_mode(fa_engine* h, int32_t mode) {
+  FA_API_BEGIN
+  FA_REQUIRE(mode == 0 || mode == 1, "encode mode must be 0 (padded batch) or 1 (independent clips)");
+  h->e->encode_mode = mode;
   FA_API_END
 }
 

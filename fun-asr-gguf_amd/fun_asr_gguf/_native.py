@@ -21,7 +21,7 @@ EXPORTS = [
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
-    "fa_llm_invariant_width",
+    "fa_llm_invariant_width", "fa_set_encode_mode",
 ]
 
 
@@ -79,6 +79,7 @@ def load():
     lib.fa_set_encoder_fp16.argtypes = [P, I32]
     lib.fa_set_decode_fused.argtypes = [P, I32]
     lib.fa_set_encoder_gemm.argtypes = [P, I32]
+    lib.fa_set_encode_mode.argtypes = [P, I32]
     lib.fa_encode_tap.argtypes = [P, I32, P, I64]
     lib.fa_embd_rows.argtypes = [P, P, I32, I32, P]
     lib.fa_llm_reset.argtypes = [P, I32]
@@ -236,9 +237,16 @@ class Engine:
         _check(self.lib.fa_pcm_upload(self.h, _ptr(pcm), pcm.size), "fa_pcm_upload")
         return dict(ns=ns, stride=pcm.shape[1])
 
-    def encode(self, clips, want_enc=False, debug_lfr=False, resident=None):
+    def encode(self, clips, want_enc=False, debug_lfr=False, resident=None, independent=False):
         """clips: list of 1-D float32 arrays (or resident=upload() handle, clips = their lengths only).
-        Returns dict(audio_embd=[...], ctc_ids=[...], t_lfr, target_len[, enc, lfr_embedded])."""
+        independent: every clip gets its single-clip encode (concurrent lanes, fa_set_encode_mode(1)) instead of one
+        padded batch. Returns dict(audio_embd=[...], ctc_ids=[...], t_lfr, target_len[, enc, lfr_embedded])."""
+        if independent:
+            _check(self.lib.fa_set_encode_mode(self.h, 1), "fa_set_encode_mode")
+            try:
+                return self.encode(clips, want_enc, debug_lfr, resident)
+            finally:
+                _check(self.lib.fa_set_encode_mode(self.h, 0), "fa_set_encode_mode")
         if resident is not None:
             ns, stride, pcm = resident["ns"], resident["stride"], None
         else:

@@ -219,17 +219,19 @@ class StreamDecoder:
                       temperature=0.3, top_p=1.0, top_k=50) -> DecodeResult:
         return self.decode_streams([stream], language, context, verbose, reporter, temperature, top_p, top_k)[0]
 
-    def front(self, streams: List[RecognitionStream], language=None, context=None, resident=None):
-        """Steps 1-3 for a group of streams: encode (+ CTC head / argmax) as one device batch, CTC collapse + host
-        token map + hotwords, prompt rows. -> list of dicts (embd, ctc_results, hotwords, n_p, n_s, audio_embd,
-        timings)."""
+    def front(self, streams: List[RecognitionStream], language=None, context=None, resident=None, independent=False):
+        """Steps 1-3 for a group of streams: encode (+ CTC head / argmax) as one device batch (independent: every clip
+        its single-clip encode, in concurrent lanes), CTC collapse + host token map + hotwords, prompt rows. -> list of
+        dicts (embd, ctc_results, hotwords, n_p, n_s, audio_embd, timings)."""
         m = self.models
         eng = m.engine
         B = len(streams)
         timings = [Timings() for _ in range(B)]
         # 1. encode (+ CTC head + argmax) — one device batch
         t = time.perf_counter()
-        out = eng.encode(None if resident is not None else [s.audio_data for s in streams], resident=resident)
+        clips = None if resident is not None else [s.audio_data for s in streams]
+        out = eng.encode(clips, resident=resident, independent=True) if independent and B > 1 else \
+            eng.encode(clips, resident=resident)
         dt = time.perf_counter() - t
         for tm in timings:
             tm.encode = dt

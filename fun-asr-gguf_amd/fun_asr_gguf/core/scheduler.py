@@ -97,10 +97,11 @@ class ContinuousBatcher:
 
         def encode_ahead(need):
             # clips are encoded ahead of their admission in encoder batches of the engine's full capacity (a padded
-            # batch of 32 runs ~2.5x the per-clip rate of a batch of 8); within the invariant width, one at a time
+            # batch of 32 runs ~2.5x the per-clip rate of a batch of 8); within the invariant width as independent
+            # clips (each its single-clip encode, in concurrent lanes)
             nonlocal n_encode_batches, t_enc
             while len(ready) < need and queue:
-                k = 1 if alone else min(enc_cap, len(queue))
+                k = min(enc_cap, len(queue))
                 idxs = [queue.pop(0) for _ in range(k)]
                 streams = []
                 for i in idxs:
@@ -108,7 +109,7 @@ class ContinuousBatcher:
                     st.accept_waveform(sr, chunks[i])
                     streams.append(st)
                 t = time.perf_counter()
-                fronts = self.decoder.front(streams, language, context)
+                fronts = self.decoder.front(streams, language, context, independent=alone)
                 t_enc += time.perf_counter() - t
                 n_encode_batches += 1
                 ready.extend(_Job(i, st, f) for i, st, f in zip(idxs, streams, fronts))

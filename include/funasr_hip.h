@@ -108,6 +108,11 @@ int fa_encode_fetch(fa_engine* e, float* audio_embd_out, int64_t tgt_stride, int
  * with blanks (= blank_id) and repeats removed; n_out[b] = count. */
 int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* frames_out, int64_t out_stride,
                     int32_t* n_out);
+/* Encode mode: 0 (default) = one padded batch; 1 = independent clips: every clip of a multi-clip call runs the
+ * single-clip encode (exactly the arithmetic of encoding it alone) in a lane of its own -- its own rows of the batch
+ * arenas, its own workspaces and HIP stream -- so up to 8 one-clip encodes run concurrently. Used where a batch must
+ * give each clip its one-at-a-time result (the reference encodes every segment alone, orchestrator.py:139-171). */
+int fa_set_encode_mode(fa_engine* e, int32_t mode);
 /* Debug hooks (tests): flags bit 0 keeps clip 0's embedded LFR features (x*sqrt(512)+PE, [T, d_in]) of
  * the next fa_encode; fa_encode_tap(e, 0, out, n) copies them out. Bit 1 makes one block of the fused decode layer
  * withhold its q|k|v hand-off, forcing the in-launch fan-in timeout (10 ms per wait): fa_llm_generate_end then

@@ -21,7 +21,7 @@ class FakeEngine:
         self.last = []
         self.seqs = {}
 
-    def encode(self, clips, want_enc=False, resident=None):
+    def encode(self, clips, want_enc=False, resident=None, independent=False):
         self._idle("encode")
         self.n_encodes = getattr(self, "n_encodes", 0) + 1
         self.last = [np.asarray(c, np.float32) for c in clips]

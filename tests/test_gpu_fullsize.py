@@ -443,3 +443,13 @@ def test_encoder_batch_vs_alone_f32_order(eng):
         same.append(bool(np.array_equal(out["audio_embd"][b], one["audio_embd"][0])))
         assert _rel(out["enc"][b], one["enc"][0]) < ENC_ATOL
     print(f"encoder batch-6 vs alone: audio_embd max-abs/max {worst:.2e}, bit-identical per segment {same}")
+    # independent-clip mode (fa_set_encode_mode(1): each clip's single-clip encode in a concurrent lane): bit-identical
+    # to encoding each clip alone, CTC collapse included
+    ind = eng.encode(chunks, want_enc=True, independent=True)
+    pairs = eng.ctc_collapse(60514, len(chunks))
+    for b, c in enumerate(chunks):
+        one = eng.encode([c], want_enc=True)
+        p1 = eng.ctc_collapse(60514, 1)[0]
+        assert np.array_equal(ind["audio_embd"][b], one["audio_embd"][0]), f"segment {b}: audio rows"
+        assert np.array_equal(ind["enc"][b], one["enc"][0]) and np.array_equal(ind["ctc_ids"][b], one["ctc_ids"][0])
+        assert np.array_equal(pairs[b][0], p1[0]) and np.array_equal(pairs[b][1], p1[1]), f"segment {b}: collapse"
