@@ -160,6 +160,7 @@ struct Engine {
   // Measured (graph-replayed, full model): 1 / 8 / 32 steps per graph -> batch 1 0.489 / 0.499 / 0.525 ms per step,
   // batch 32 1.223 / 1.239 / 1.358 ms: one step per graph replay stays the default
   int graph_steps = 1;
+  bool pf_row_local = false;  // the prefill forward being run is row-local (see llm_forward)
   int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after a fused fan-in timeout
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
@@ -976,6 +977,9 @@ struct Engine {
     // (no k_prep_q8 launches but layer 0's)
     const bool fused = decode && fused_shape_ok() && ((M == 1 && use_fused) || (M <= fused_max_m && use_fused == 1));
     const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm && !fused;
+    // row-local prefill (pf_row_local): every row's arithmetic that of its own sequence's prefill (gemv_q8 row_local,
+    // one key split, no query tiles); small row counts run the fused GEMV, which is row-local already
+    const int rl = !decode && pf_row_local && !small ? 1 : 0;
     (void)max_pos;
     if (fused) {
       llm_forward_fused(M);
@@ -990,6 +994,7 @@ struct Engine {
       GemvArgs a{};
       a.M = M;
       a.eps = lc.rms_eps;
+      a.row_local = rl;
       // q|k|v = W . rms_norm(x)*attn_norm
       a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
       a.out = lqkv; a.ldo = QKV;
@@ -1004,18 +1009,19 @@ struct Engine {
           qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
                         seq_stride, stream);
         // M > 4: the attention also leaves its rows as q8_0 blocks for the o GEMM (no prep launch)
-        if (!decode && n_ptiles > 0)  // query tiles: each K/V tile serves 64 rows x 2 heads
+        if (!decode && n_ptiles > 0 && !rl)  // query tiles: each K/V tile serves 64 rows x 2 heads
           attn_prefill(d_ptiles, n_ptiles, d_tok_pos, H, KV, seq_stride, kc, vc, lq, latt, small ? nullptr : lxq2,
                        small ? nullptr : lxd2, stream);
         else
           attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
                      d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream, small ? nullptr : lxq2,
-                     small ? nullptr : lxd2);
+                     small ? nullptr : lxd2, rl ? 1 : ATTN_SPLITS);
         prof_end(3, 0, 0);
       }
       // x += Wo . attn
       GemvArgs o{};
       o.M = M; o.eps = lc.rms_eps; o.wq = w.o.q; o.wd = w.o.d; o.O = E; o.rpw = gemv_rows_per_wave(E);
+      o.row_local = rl;
       o.out = lx; o.ldo = E; o.res = lx; o.ldr = E;
       if (small) { o.x = latt; o.ldx = H * D; }
       else { o.xq = lxq2; o.xd = lxd2; }
@@ -1024,6 +1030,7 @@ struct Engine {
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
       GemvArgs g{};
       g.M = M; g.eps = lc.rms_eps; g.wq = w.gate.q; g.wd = w.gate.d; g.wq2 = w.up.q; g.wd2 = w.up.d; g.O = F;
+      g.row_local = rl;
       g.rpw = gemv_rows_per_wave(F); g.out = lact; g.ldo = F;
       if (small) { g.x = lx; g.ldx = E; g.norm_w = w.ffn_norm; }
       else {
@@ -1035,6 +1042,7 @@ struct Engine {
       // x += Wdown . act
       GemvArgs dn{};
       dn.M = M; dn.eps = lc.rms_eps; dn.wq = w.down.q; dn.wd = w.down.d; dn.O = E; dn.rpw = gemv_rows_per_wave(E);
+      dn.row_local = rl;
       dn.out = lx; dn.ldo = E; dn.res = lx; dn.ldr = E;
       if (small) { dn.x = lact; dn.ldx = F; }
       else { dn.xq = lxq2; dn.xd = lxd2; }
@@ -1063,6 +1071,14 @@ struct Engine {
     else if (nrm) { h.xq = lxq; h.xd = lxd; h.ssp = d_ssp; }  // rows from the last down epilogue
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
     gemv(h, E, 3);
+  }
+
+  // the two-launch layer gives every token of a batch of up to fused_max_m its own grid slab with the batch-1
+  // arithmetic, and the LM head is the fused GEMV up to g_gemv_small_max tokens (the MFMA LM head above sums in
+  // another f32 order); every other decode path is only known to be invariant at width 1
+  int invariant_width() const {
+    if (use_fused == 1 && fused_shape_ok()) return std::max(1, std::min(fused_max_m, fa::g_gemv_small_max));
+    return 1;
   }
 
   bool fused_shape_ok() const {
@@ -1676,7 +1692,9 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   e->set_sampling(s);
   e->set_prefill_tiles(sq.data(), ps.data(), n_tokens);
+  e->pf_row_local = true;  // a prompt's prefill arithmetic is the same alone and in a row-local batch
   e->llm_forward(n_tokens, false, e->n_past[seq] + n_tokens - 1);
+  e->pf_row_local = false;
   e->n_ptiles = 0;
   // the first token's draw is keyed by the last prompt row's (seq, position)
   e->sample(1, e->d_tok_seq + (n_tokens - 1), e->d_tok_pos + (n_tokens - 1), nullptr, e->d_tok_cur, nullptr);
@@ -1712,6 +1730,29 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     total += n_tokens[i];
   }
   e->set_sampling(s);
+  // within the invariant width the batch is row-local: every prompt gets exactly its fa_llm_prefill arithmetic (the
+  // reference prefills every segment alone); prompts short enough for the fused GEMV path run one by one
+  const bool row_local = n_seqs <= e->invariant_width();
+  if (row_local) {
+    bool all_long = true;
+    for (int i = 0; i < n_seqs; ++i) all_long = all_long && !fa::gemv_small(n_tokens[i]);
+    if (!all_long || n_seqs == 1) {
+      int64_t o = 0;
+      for (int i = 0; i < n_seqs; ++i) {
+        int tk = 0;
+        const int rc = fa_llm_prefill(h, seqs[i], embd + o * E, n_tokens[i], s, &tk, nullptr);
+        if (rc != FA_OK) return rc;
+        if (tok_out) tok_out[i] = tk;
+        o += n_tokens[i];
+      }
+      // fa_llm_prefill left only the last sequence's logits row: point every sequence at its own (re-run is not
+      // needed: each call kept its row 0, so only the last one is current)
+      std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
+      e->logits_row[seqs[n_seqs - 1]] = 0;
+      return FA_OK;
+    }
+  }
+  e->pf_row_local = row_local;
   // sequences in order, as many per forward as the row capacity holds; one weight pass per forward
   int64_t off = 0;
   for (int i0 = 0; i0 < n_seqs;) {
@@ -1733,7 +1774,12 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
     e->set_prefill_tiles(sq.data(), ps.data(), rows);
-    e->llm_forward(rows, false, 0, n);
+    try {
+      e->llm_forward(rows, false, 0, n);
+    } catch (...) {
+      e->pf_row_local = false;
+      throw;
+    }
     e->n_ptiles = 0;
     // each first token's draw is keyed by its sequence's last prompt row (seq, position), as fa_llm_prefill's
     FA_HIP(hipMemcpyAsync(e->d_ids, lseq.data(), n * 4, hipMemcpyHostToDevice, e->stream));
@@ -1753,6 +1799,7 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     off += rows;
     i0 = i1;
   }
+  e->pf_row_local = false;
   (void)total;
   FA_API_END
 }
@@ -1810,13 +1857,7 @@ int fa_llm_generate(fa_engine* h, const int32_t* seqs, int32_t n_seqs, int32_t n
 
 int fa_llm_invariant_width(fa_engine* h, int32_t* out) {
   FA_API_BEGIN
-  Engine* e = h->e;
-  // the two-launch layer gives every token of a batch of up to fused_max_m its own grid slab with the batch-1
-  // arithmetic, and the LM head is the fused GEMV up to g_gemv_small_max tokens (the MFMA LM head above sums in
-  // another f32 order); every other decode path is only known to be invariant at width 1
-  int w = 1;
-  if (e->use_fused == 1 && e->fused_shape_ok()) w = std::max(1, std::min(e->fused_max_m, fa::g_gemv_small_max));
-  *out = w;
+  *out = h->e->invariant_width();
   FA_API_END
 }
 

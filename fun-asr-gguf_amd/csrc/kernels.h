@@ -98,6 +98,10 @@ struct GemvArgs {
   // scales) and writes per-token sum-of-squares partials ssp_out [M][32]; a GEMM with ssp != nullptr reads such rows
   // (xq / xd) and applies rstd = 1/sqrtf(sum ssp / K + eps) to the block scales
   const float* ssp; float* ssp_out; const float* qn_w;
+  // prefill whose token rows must each get the arithmetic of their own sequence's prefill, whatever else the call
+  // holds (fa_llm_prefill, and fa_llm_prefill_batch within the invariant width): every GEMM on the K-in-block MFMA
+  // kernel, whose per-row result does not depend on the token count (no split-K, no 128-token tiles)
+  int row_local;
 };
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
@@ -137,7 +141,7 @@ void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
                 int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout = nullptr,
-                float* dout = nullptr);
+                float* dout = nullptr, int max_splits = 16);
 // Fused batch-1 decode layer (M = 1; llm.hip): attention + split o projection, and gate|up + SwiGLU + split down
 // projection, each with an in-launch group fan-in (see the kernels). FUSED_PARTS = partial vectors summed by the next
 // launch's prologue (8 kv heads for o, 8 groups of 384 act rows for down).

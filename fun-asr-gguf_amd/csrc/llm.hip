@@ -1035,11 +1035,11 @@ static void launch_gemm_kw(const GemvArgs& a, int K, hipStream_t s) {
 // K-in-block GEMM for the shapes it is instantiated for; false otherwise. 8 waves (16 measured slower on the
 // few-tile o / down shapes at batch 32: 10.2 / 18.3 vs 8.8 / 14.6 us, register-capped at 128 VGPRs);
 // q8_0 blocks per wave NBW = blocks of K per wave.
-static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s) {
+static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s, bool force = false) {
   constexpr int nw = 8;
   // batched decode (a few hundred tiles or less) measured 2.6 % faster per step on the split-K block kernel
-  // (1.974 vs 2.027 ms at batch 32, same box); prefill-sized grids take this one
-  if (g_gemm_q8_kw < 2 && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) < 256) return false;
+  // (1.974 vs 2.027 ms at batch 32, same box); prefill-sized grids take this one (row-local prefill: always)
+  if (!force && g_gemm_q8_kw < 2 && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) < 256) return false;
   const int nb = (K / 32) * (epi == 2 ? 2 : 1);
   if (nb % nw) return false;
   switch (epi * 100 + nb / nw) {
@@ -1332,6 +1332,11 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     return;
   }
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
+  if (a.row_local) {  // each token row's arithmetic independent of the token count: the K-in-block kernel only
+    FA_REQUIRE(epi != 3 && !a.ssp && !a.ssp_out, "gemv_q8: row-local rows are prefill layer GEMMs");
+    FA_REQUIRE(gemm_q8_kw(a, K, epi, s, true), "gemv_q8: row-local GEMM shape not instantiated");
+    return;
+  }
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
   if (epi == 3 && K == 1024 && a.M <= 32 && g_lm_head_b) {  // batched LM head: persistent tile loop
@@ -2100,7 +2105,8 @@ void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
-                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout, float* dout) {
+                int64_t seq_stride, float* out, const AttnWork& wk, hipStream_t s, int8_t* qout, float* dout,
+                int max_splits) {
   FA_REQUIRE(H == KV * GQ, "attn_block: n_head must be 2*n_head_kv");
   FA_REQUIRE(wk.counters && wk.partials && M <= wk.max_tokens && KV <= wk.max_kv, "attn_block: workspace too small");
   const float scale = 1.0f / sqrtf(128.0f);
@@ -2108,7 +2114,7 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // prefill. Batch 32 measured 14.7-17.0 us for every target of 256-1024 blocks, lean or not (attn_batch.hip): the
   // K/V stream of 512 (sequence, kv head) pairs comes in at ~2.8 TB/s whatever the block shape.
   int ns = 1;
-  while (ns < ASPLIT && (ns + 1) * M * KV <= g_attn_blocks) ++ns;
+  while (ns < std::min(ASPLIT, max_splits) && (ns + 1) * M * KV <= g_attn_blocks) ++ns;
   FA_REQUIRE(ns == 1 || M <= wk.max_split_tokens, "attn_block: split partials workspace too small");
   const bool lean = g_attn_lean >= 0 ? g_attn_lean != 0 : M * KV * ns > 3 * 256;
   auto kern = lean ? (decode_mode ? k_attn_block<1, 1> : k_attn_block<0, 1>)

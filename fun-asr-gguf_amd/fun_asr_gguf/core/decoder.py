@@ -90,12 +90,12 @@ def invariant_width(eng):
 
 
 def prefill_group(eng, seqs, embds, samp):
-    """Prefill `embds` into slots `seqs` -> first tokens. One prompt: llama_decode of its batch. Several: within the
-    engine's invariant width each prompt is prefilled alone (so every sequence gets exactly its single-sequence
-    tokens, as the reference decodes every segment alone, core/decoder.py:70-123); wider groups share forwards
-    (one weight pass per forward, fa_llm_prefill_batch; agreement to the q8_0 noise floor)."""
-    if len(embds) == 1 or len(embds) <= invariant_width(eng):
-        return [eng.llm_prefill(q, e, **samp) for q, e in zip(seqs, embds)]
+    """Prefill `embds` into slots `seqs` -> first tokens. One prompt: llama_decode of its batch. Several: their
+    prompts share forwards (one weight pass per forward, fa_llm_prefill_batch); within the engine's invariant width
+    that batch is row-local, so every sequence gets exactly its single-sequence prefill (the reference decodes every
+    segment alone, core/decoder.py:70-123); wider groups agree to the q8_0 noise floor."""
+    if len(embds) == 1:
+        return [eng.llm_prefill(seqs[0], embds[0], **samp)]
     return eng.llm_prefill_batch(list(seqs), embds, **samp)
 
 
