@@ -205,6 +205,7 @@ struct Engine {
       if (l.s) hipStreamDestroy(l.s);
     }
     if (ev_fork) hipEventDestroy(ev_fork);
+    if (hp_meta) hipHostFree(hp_meta);
     for (auto& g : step_graphs) hipGraphExecDestroy(g.second);
     for (auto& e : ev_pool) {
       hipEventDestroy(e.first);
@@ -803,6 +804,8 @@ struct Engine {
   };
   std::vector<EncLane> enc_lanes;
   int encode_mode = 0;  // 0: padded batch; 1: independent clips in concurrent lanes
+  int64_t* hp_meta = nullptr;  // pinned per-clip length records: region 0 = batch encode, 1 + lane = lane encode
+  int meta_slot = 0;
   hipEvent_t ev_fork = nullptr;
 
   EncBind enc_bind() const {
@@ -821,14 +824,17 @@ struct Engine {
     if (!l.s) {
       FA_HIP(hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking));
       FA_HIP(hipEventCreateWithFlags(&l.done, hipEventDisableTiming));
+      // the arrival counters start at zero (zeroed once, re-armed by the combining blocks). The zeroing is enqueued on
+      // the lane's own stream, ahead of its kernels: a plain hipMemset runs on the null stream, which a non-blocking
+      // stream does not wait for, and reused device memory is not zero (a lane created mid-run then raced it)
       l.attn = enc_attn_wk;
       l.attn.part = alloc<float>(l.attn.part_n);
       l.attn.cnt = alloc<int>(l.attn.cnt_n * CNT_LINE);
-      FA_HIP(hipMemset(l.attn.cnt, 0, l.attn.cnt_n * CNT_LINE * sizeof(int)));
+      FA_HIP(hipMemsetAsync(l.attn.cnt, 0, l.attn.cnt_n * CNT_LINE * sizeof(int), l.s));
       l.gemm = enc_gemm_wk;
       l.gemm.part = alloc<float>(l.gemm.part_n);
       l.gemm.cnt = alloc<int>(l.gemm.cnt_n * CNT_LINE);
-      FA_HIP(hipMemset(l.gemm.cnt, 0, l.gemm.cnt_n * CNT_LINE * sizeof(int)));
+      FA_HIP(hipMemsetAsync(l.gemm.cnt, 0, l.gemm.cnt_n * CNT_LINE * sizeof(int), l.s));
     }
     return l;
   }
@@ -846,7 +852,9 @@ struct Engine {
     try {
       for (int b = 0; b < batch; ++b) {
         EncLane& l = enc_lane(b % kEncLanes);
-        if (b >= kEncLanes) FA_HIP(hipStreamWaitEvent(l.s, l.done, 0));  // the lane's previous clip (same workspaces)
+        // the lane's previous clip used the same workspaces and pinned length record: the host waits for it (the
+        // record is rewritten at enqueue time)
+        if (b >= kEncLanes) FA_HIP(hipEventSynchronize(l.done));
         FA_HIP(hipStreamWaitEvent(l.s, ev_fork, 0));
         EncBind lb = base;
         lb.stream = l.s; lb.attn = l.attn; lb.gemm = l.gemm;
@@ -857,7 +865,9 @@ struct Engine {
         lb.cbuf += b * T * d; lb.ctc_pval += b * T * nt; lb.ctc_pidx += b * T * nt; lb.ctc_ids += b * T;
         lb.d_nsamp += b; lb.d_tmel += b; lb.d_tlfr += b; lb.d_tgt += b; lb.d_ctclen += b;
         enc_rebind(lb);
+        meta_slot = 1 + b % kEncLanes;
         encode_device(pcm + (size_t)b * stride, n_samples + b, 1, stride);
+        meta_slot = 0;
         FA_HIP(hipEventRecord(l.done, l.s));
         tl[b] = h_tlfr[0];
         tg[b] = h_tgt[0];
@@ -866,6 +876,7 @@ struct Engine {
       }
     } catch (...) {
       enc_rebind(base);
+      meta_slot = 0;
       throw;
     }
     for (int i = 0; i < std::min(batch, kEncLanes); ++i) FA_HIP(hipStreamWaitEvent(stream, enc_lanes[i].done, 0));
@@ -901,11 +912,25 @@ struct Engine {
     const int rows = batch * ts;
     last_batch = batch;
     last_tstride = ts;
-    FA_HIP(hipMemcpyAsync(d_nsamp, n_samples, batch * sizeof(int64_t), hipMemcpyHostToDevice, stream));
-    FA_HIP(hipMemcpyAsync(d_tmel, tmel.data(), batch * 4, hipMemcpyHostToDevice, stream));
-    FA_HIP(hipMemcpyAsync(d_tlfr, h_tlfr.data(), batch * 4, hipMemcpyHostToDevice, stream));
-    FA_HIP(hipMemcpyAsync(d_tgt, h_tgt.data(), batch * 4, hipMemcpyHostToDevice, stream));
-    FA_HIP(hipMemcpyAsync(d_ctclen, h_ctclen.data(), batch * 4, hipMemcpyHostToDevice, stream));
+    // the per-clip lengths go up from pinned host memory owned by the engine (one region per encode lane), so no
+    // copy depends on when the runtime reads a pageable source (the lane loop reuses the host vectors at once)
+    if (!hp_meta) {
+      FA_HIP(hipHostMalloc(&hp_meta, (size_t)(kEncLanes + 1) * max_batch * 6 * sizeof(int64_t), hipHostMallocDefault));
+    }
+    int64_t* hm = hp_meta + (size_t)meta_slot * max_batch * 6;
+    int32_t* hm32 = reinterpret_cast<int32_t*>(hm + max_batch);
+    for (int b = 0; b < batch; ++b) {
+      hm[b] = n_samples[b];
+      hm32[b] = tmel[b];
+      hm32[max_batch + b] = h_tlfr[b];
+      hm32[2 * max_batch + b] = h_tgt[b];
+      hm32[3 * max_batch + b] = h_ctclen[b];
+    }
+    FA_HIP(hipMemcpyAsync(d_nsamp, hm, batch * sizeof(int64_t), hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tmel, hm32, batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tlfr, hm32 + max_batch, batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tgt, hm32 + 2 * max_batch, batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_ctclen, hm32 + 3 * max_batch, batch * 4, hipMemcpyHostToDevice, stream));
     // F1-F4
     if (enc_fp16) prepare_fp16();
     else if (enc_gemm) prepare_bf3();
@@ -1152,7 +1177,7 @@ struct Engine {
   bool fused_error() {
     int err = 0;
     FA_HIP(hipMemcpy(&err, fdw.err, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) FA_HIP(hipMemset(fdw.err, 0, sizeof(int)));
+    if (err) FA_HIP(hipMemsetAsync(fdw.err, 0, sizeof(int), stream));  // ordered before the next launches
     return err != 0;
   }
 

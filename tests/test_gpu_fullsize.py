@@ -419,11 +419,18 @@ def test_c4_batch_of_6_equals_sequential_segments():
         audio = synth_audio(300 * SR, 4000)
         wins = octc.segments_info(300.0, 60.0, 4.0)
         chunks = [audio[int(s * SR):int(e * SR)] for s, e in wins]
+        w0 = api.models.engine.llm_invariant_width()
         batch = api.transcribe_batch(chunks, temperature=0.0)
-        for c, b in zip(chunks, batch):
-            one = api.transcribe_batch([c], temperature=0.0)[0]
-            assert b.n_gen == one.n_gen == 253
-            assert b.text == one.text and b.aligned == one.aligned
+        ones = [api.transcribe_batch([c], temperature=0.0)[0] for c in chunks]
+        diag = []
+        for k, (b, one) in enumerate(zip(batch, ones)):
+            if b.text != one.text or b.aligned != one.aligned:
+                pre = next((i for i, (x, y) in enumerate(zip(b.text, one.text)) if x != y), min(len(b.text), len(one.text)))
+                diag.append(f"segment {k}: texts agree on {pre} of {len(one.text)} chars; audio rows equal "
+                            f"{np.array_equal(b.audio_embd, one.audio_embd)}; ctc equal {b.ctc_results == one.ctc_results}")
+        w1 = api.models.engine.llm_invariant_width()
+        assert not diag and w0 == w1 == 6, f"invariant width {w0} -> {w1}; " + "; ".join(diag)
+        assert all(b.n_gen == one.n_gen == 253 for b, one in zip(batch, ones))
     finally:
         api.cleanup()
 
