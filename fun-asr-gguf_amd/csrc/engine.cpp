@@ -996,15 +996,16 @@ struct Engine {
     // prefill: rows are consecutive positions of one sequence, logits for the last row only.
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
-    const bool small = gemv_small(M);
+    // row-local prefill (pf_row_local): every row's arithmetic that of its own sequence's prefill (gemv_q8 row_local,
+    // one key split, no query tiles; never the fused-GEMV path, whose use would depend on the call's row count)
+    const int rl = !decode && pf_row_local ? 1 : 0;
+    const bool small = gemv_small(M) && !rl;
     // batched decode: the residual GEMMs (o, down) quantise their new rows times the next RMSNorm weight and leave
     // per-token sum-of-squares partials; q|k|v, gate|up and the LM head apply rstd to those rows' block scales
     // (no k_prep_q8 launches but layer 0's)
     const bool fused = decode && fused_shape_ok() && ((M == 1 && use_fused) || (M <= fused_max_m && use_fused == 1));
     const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm && !fused;
-    // row-local prefill (pf_row_local): every row's arithmetic that of its own sequence's prefill (gemv_q8 row_local,
-    // one key split, no query tiles); small row counts run the fused GEMV, which is row-local already
-    const int rl = !decode && pf_row_local && !small ? 1 : 0;
+
     (void)max_pos;
     if (fused) {
       llm_forward_fused(M);
@@ -1756,28 +1757,8 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
   }
   e->set_sampling(s);
   // within the invariant width the batch is row-local: every prompt gets exactly its fa_llm_prefill arithmetic (the
-  // reference prefills every segment alone); prompts short enough for the fused GEMV path run one by one
-  const bool row_local = n_seqs <= e->invariant_width();
-  if (row_local) {
-    bool all_long = true;
-    for (int i = 0; i < n_seqs; ++i) all_long = all_long && !fa::gemv_small(n_tokens[i]);
-    if (!all_long || n_seqs == 1) {
-      int64_t o = 0;
-      for (int i = 0; i < n_seqs; ++i) {
-        int tk = 0;
-        const int rc = fa_llm_prefill(h, seqs[i], embd + o * E, n_tokens[i], s, &tk, nullptr);
-        if (rc != FA_OK) return rc;
-        if (tok_out) tok_out[i] = tk;
-        o += n_tokens[i];
-      }
-      // fa_llm_prefill left only the last sequence's logits row: point every sequence at its own (re-run is not
-      // needed: each call kept its row 0, so only the last one is current)
-      std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
-      e->logits_row[seqs[n_seqs - 1]] = 0;
-      return FA_OK;
-    }
-  }
-  e->pf_row_local = row_local;
+  // reference prefills every segment alone)
+  e->pf_row_local = n_seqs <= e->invariant_width();
   // sequences in order, as many per forward as the row capacity holds; one weight pass per forward
   int64_t off = 0;
   for (int i0 = 0; i0 < n_seqs;) {

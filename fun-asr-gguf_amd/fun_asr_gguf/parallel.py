@@ -2,10 +2,11 @@
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on ROCm, "gloo" in CPU tests).
 Segments are assigned longest-first to the least-loaded rank (LPT); every rank decodes its share as one
-device batch; the only exchange is the result gather to rank 0 (gather_object of small per-segment
+device batch; the only exchange is the result gather to rank 0 (tensor all_gathers of the JSON-encoded per-segment
 records: text, char timestamps, hotwords, CTC tokens, timings), after which rank 0 merges. No data-path
 collective: the PCM chunks are cut from the same input on every rank.
 """
+import json
 from dataclasses import asdict
 
 from .nano_ctc import Token
@@ -36,17 +37,37 @@ def from_record(r):
                         timings=Timings(**r["timings"]), n_prefix=r["n_prefix"], n_suffix=r["n_suffix"])
 
 
+def _pack(records_by_index):
+    """Records -> UTF-8 JSON bytes (floats in shortest round-trip form: the merge on rank 0 sees the exact values)."""
+    return json.dumps(sorted(records_by_index.items()), ensure_ascii=False).encode("utf-8")
+
+
 def gather_to_root(records_by_index, n_total, dist, group=None):
-    """records_by_index: {segment index: record} of this rank -> full ordered list on rank 0, None elsewhere."""
+    """records_by_index: {segment index: record} of this rank -> full ordered list on rank 0, None elsewhere.
+    Two tensor collectives over the process group (RCCL over xGMI with backend "nccl": device tensors; gloo: host): an
+    all_gather of the payload sizes, then an all_gather of the JSON payloads padded to the largest (KB-scale: latency-
+    bound). No pickling: the records cross as UTF-8 JSON."""
+    import torch
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    bucket = [None] * world if rank == 0 else None
-    dist.gather_object(records_by_index, bucket, dst=0, group=group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    payload = _pack(records_by_index)
+    size = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, size, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    n = max(1, max(sizes))
+    buf = torch.zeros(n, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
     if rank != 0:
         return None
     merged = {}
-    for part in bucket:
-        merged.update(part)
+    for b, k in zip(bufs, sizes):
+        for idx, rec in json.loads(bytes(b[:k].cpu().numpy()).decode("utf-8")):
+            merged[int(idx)] = rec
     assert len(merged) == n_total, f"gather lost segments: {len(merged)} of {n_total}"
     return [merged[i] for i in range(n_total)]
 

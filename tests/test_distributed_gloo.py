@@ -4,6 +4,7 @@ the records of a single-rank run."""
 import os
 import socket
 
+import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -44,12 +45,14 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gather_world2_equals_single():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_world2_equals_single(world):
+    """world 2 and 3 (uneven LPT shares: 6 segments over 3 ranks, one rank with the short one)."""
     from fun_asr_gguf.parallel import to_record, from_record
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

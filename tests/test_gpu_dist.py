@@ -1,6 +1,6 @@
 """The result gather over RCCL (backend "nccl") on the GPU box: one rank per GPU, so a one-GPU box runs world_size 1
 (RCCL refuses two ranks on one device). It exercises the real collective path of `parallel.gather_to_root`
-(gather_object over RCCL on the rank's device) and the real engine through `transcribe(..., ranks=dist)`; the N > 1
+(two tensor all_gathers of the JSON records over RCCL on the rank's device) and the real engine through `transcribe(..., ranks=dist)`; the N > 1
 logic is covered on CPU by tests/test_distributed_gloo.py (world_size 2, gloo)."""
 import os
 import socket

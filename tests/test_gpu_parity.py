@@ -439,6 +439,7 @@ def test_llm_prefill_batch_equals_per_sequence(llm_tiny_oracle, monkeypatch, t_m
     from fun_asr_gguf import _native
     monkeypatch.setenv("FUNASR_GEMM_T_MIN_M", str(t_min_m))
     monkeypatch.setenv("FUNASR_ATTN_PREFILL_MIN_M", str(apf_min_m))
+    monkeypatch.setenv("FUNASR_FUSED_MAX_M", "1")  # invariant width 1: the batch takes the shared-forward kernels
     m = llm_tiny_oracle
     rng = np.random.default_rng(21)
     prompts = [np.concatenate([m.embed_prompt(rng.integers(0, 4096, n)),
@@ -477,6 +478,7 @@ def test_llm_prefill_batch_continuation_query_tiles(llm_tiny_oracle, monkeypatch
     logits."""
     from fun_asr_gguf import _native
     monkeypatch.delenv("FUNASR_ATTN_PREFILL_MIN_M", raising=False)
+    monkeypatch.setenv("FUNASR_FUSED_MAX_M", "1")  # invariant width 1: the batch takes the shared-forward kernels
     m = llm_tiny_oracle
     rng = np.random.default_rng(5)
     prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (90, 20, 70)]
@@ -641,3 +643,35 @@ def test_fused_timeout_recovers_on_five_launch_layer():
     (f1, t1, l1, m1, w1), (f0, t0, l0, m0, w0) = runs
     assert w1 == 1 and f1 == f0 and t1 == t0 and m1 == m0
     assert np.array_equal(l1, l0)
+
+
+def test_llm_prefill_batch_row_local_exact(llm_tiny_oracle):
+    """Within the invariant width fa_llm_prefill_batch is row-local: every prompt gets exactly the arithmetic of its own
+    fa_llm_prefill (K-in-block GEMMs, one key split, no query tiles, never the row-count-dependent fused-GEMV path), so
+    first tokens and logits are bit-identical, for short prompts (<= 6 rows) and for prompts continuing a cached prefix."""
+    from fun_asr_gguf import _native
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(33)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (5, 90, 37, 12)]
+    cut = [2, 41, 20, 6]
+    e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=128, max_seqs=4), max_batch=1, max_samples=16000)
+    try:
+        e.synthetic_weights(0)
+        assert e.llm_invariant_width() >= 4
+        single = []
+        for s, p in enumerate(prompts):  # each alone, in two calls (prefix, then the rest)
+            e.llm_reset(s)
+            e.llm_prefill(s, p[:cut[s]], temperature=0.0)
+            t = e.llm_prefill(s, p[cut[s]:], temperature=0.0)
+            single.append((t, e.llm_logits(s)))
+        for s in range(4):
+            e.llm_reset(s)
+        e.llm_prefill_batch([0, 1, 2, 3], [p[:c] for p, c in zip(prompts, cut)], temperature=0.0)
+        toks = e.llm_prefill_batch([3, 1, 0, 2], [prompts[q][cut[q]:] for q in (3, 1, 0, 2)], temperature=0.0)
+        for k, q in enumerate((3, 1, 0, 2)):
+            assert toks[k] == single[q][0], q
+            assert np.array_equal(e.llm_logits(q), single[q][1]), q
+        m.reset()
+        _check_step(e.llm_logits(1), m.forward(prompts[1], 0))
+    finally:
+        e.close()
