@@ -673,6 +673,9 @@ struct Engine {
       fdw.err = alloc<int>(1);
       fdw.gqkv = reinterpret_cast<unsigned long long*>(alloc<float>(MF * 2 * nq));
       FA_HIP(hipMemset(fdw.gqkv, 0, MF * nq * 8));
+      const size_t ngp = MF * FUSED_PARTS * ATTN_SPLITS * ATTN_PART_FLOATS;
+      fdw.gpart = reinterpret_cast<unsigned long long*>(alloc<float>(2 * ngp));
+      FA_HIP(hipMemset(fdw.gpart, 0, ngp * 8));
       fdw.pzero = alloc<float>(MF * FUSED_PARTS * E);
       FA_HIP(hipMemset(fdw.pzero, 0, MF * FUSED_PARTS * E * sizeof(float)));
     }

@@ -158,6 +158,8 @@ struct FusedDecodeWork {
   int* err = nullptr;       // set to 1 by a timed-out fan-in wait
   float* pzero = nullptr;   // [FUSED_MAX_M][FUSED_PARTS][E] zeros: layer 0's partials in the two-launch layer
   unsigned long long* gqkv = nullptr;  // [FUSED_MAX_M][(H + 2 KV) D] q|k|v granules of the two-launch layer (zeroed once)
+  unsigned long long* gpart = nullptr; // [FUSED_MAX_M][FUSED_PARTS][ATTN_SPLITS][ATTN_PART_FLOATS] attention split
+                                       // partials of the two-launch layer as granules (zeroed once)
 };
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,

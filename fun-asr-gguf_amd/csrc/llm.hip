@@ -1829,20 +1829,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
 // [4 (lane & 31), +4) (other waves: unspecified). Every wave of the block must call it. Shared by k_attn_block and
 // k_attn_o, so the fused and the 5-launch layers combine identically.
 static_assert(ASPLIT == 4 * AWV, "combine_splits: 4 splits per wave");
-__device__ __forceinline__ float4 combine_splits(const __amdgpu_buffer_rsrc_t& rs, int n_active, int wave, int lane) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  constexpr int D = 128, SPW = ASPLIT / AWV;
+typedef float cf4v __attribute__((ext_vector_type(4)));
+// The fold of combine_splits: pml[t] = {m0, l0, m1, l1}, po[t] = o[head lane >> 5][4 (lane & 31), +4) of split
+// 4 wave + t (entries past n_active are ignored). Shared with the granule form of the two-launch layer.
+__device__ __forceinline__ float4 combine_fold(const cf4v* pml, const cf4v* po, int n_active, int wave, int lane) {
+  typedef cf4v f4v;
+  constexpr int SPW = ASPLIT / AWV;
   __shared__ float s_cml[AWV][64][2];
   __shared__ __attribute__((aligned(16))) f4v s_co[AWV][64];
-  const int jj = lane >> 5, dd = (lane & 31) * 4;
+  const int jj = lane >> 5;
   {
-    f4v pml[SPW], po[SPW];
-#pragma unroll
-    for (int t = 0; t < SPW; ++t) {
-      const int tt = min(wave * SPW + t, n_active - 1);  // clamped duplicates past n_active are not folded
-      pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
-      po[t] = ld_sc1_f4(rs, (tt * APART + jj * D + dd) * 4);
-    }
     float MM = -INFINITY;
 #pragma unroll
     for (int t = 0; t < SPW; ++t)
@@ -1876,6 +1872,18 @@ __device__ __forceinline__ float4 combine_splits(const __amdgpu_buffer_rsrc_t& r
     oo += wt * s_co[w][lane];
   }
   return make_float4(oo.x / LL, oo.y / LL, oo.z / LL, oo.w / LL);
+}
+__device__ __forceinline__ float4 combine_splits(const __amdgpu_buffer_rsrc_t& rs, int n_active, int wave, int lane) {
+  constexpr int D = 128, SPW = ASPLIT / AWV;
+  const int jj = lane >> 5, dd = (lane & 31) * 4;
+  cf4v pml[SPW], po[SPW];
+#pragma unroll
+  for (int t = 0; t < SPW; ++t) {
+    const int tt = min(wave * SPW + t, n_active - 1);  // clamped duplicates past n_active are not folded
+    pml[t] = ld_sc1_f4(rs, (tt * APART + GQ * D) * 4);
+    po[t] = ld_sc1_f4(rs, (tt * APART + jj * D + dd) * 4);
+  }
+  return combine_fold(pml, po, n_active, wave, lane);
 }
 
 template <int DM, int LEAN>
@@ -2653,12 +2661,23 @@ struct AttnOArgs {
   unsigned* cnt_qkv;   // [KV][CNT_LINE]
   unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
   int dbg_drop;        // test hook (fa_set_debug bit 1): block (0, 0) publishes no q|k|v granules -> fan-in timeout
+  unsigned long long* gpart;  // FA_PART_GRANULE: [KV][ASPLIT][APART] split partials as granules {value, tag}
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
 // no drain, no ticket, no read-back (the fused FFN's hand-off). 0: sc1 rows + ticket fan-in + sc1 read-back.
 #ifndef FA_QKV_GRANULE
 #define FA_QKV_GRANULE 1
+#endif
+// FA_PART_GRANULE = 1 (two-launch layer, A/B only): the attention split partials of a kv head go to the head's 16
+// blocks as data-tagged granules too (each consumer lane polls the 8 values per split it folds), replacing the drained
+// sc1 stores + ticket fan-in + sc1 read-back; every block still adds one ticket (not waited on) so the counter keeps
+// counting launches (the epoch source). Same fold, same order: bit-identical outputs. Measured (scripts/gpu_r3_pg.sh,
+// graph-replayed step): AB 12.5-12.9 vs 9.4-9.7 us -- every poll re-reads the block's 16 KB of partials, and those
+// reads queue in the consumer CU's memory pipe (MI355X_MICROARCH.md handoff-1to1: granules pay off up to ~4 KB per
+// consumer); the ticket fan-in stays the default.
+#ifndef FA_PART_GRANULE
+#define FA_PART_GRANULE 0
 #endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
@@ -2691,6 +2710,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       if (a.xsum) a.xsum += (int64_t)mt * a.E;
       a.cnt_qkv += mt * a.KV * CNT_LINE;
       a.gqkv += (int64_t)mt * nq;
+      if (a.gpart) a.gpart += (int64_t)mt * a.KV * FS * APART;
     }
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2730,7 +2750,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     qpre.kw1 = a.kn[lane + 64];
     // this launch's epoch: head g's attention fan-in counter (+FS per launch) read before any block of head g can add
     // to it in this launch (an add needs every block's q|k|v granules, each stored after its block read the counter)
-    if (FA_QKV_GRANULE)
+    if (FA_QKV_GRANULE || FA_PART_GRANULE)
       ep_qkv = __hip_atomic_load(a.cnt + g * CNT_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / FS + 1;
   } else {
     // q|k|v row inputs do not depend on the position: issued before the tok_pos / tok_seq read (one round trip less
@@ -2868,24 +2888,77 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   const bool active = attn_split_merge<1, QKV ? 1 : 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
                                              a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
                                              M, L, o, &qpre);
-  float* pbase = a.partials + (int64_t)g * FS * APART;
-  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
-  if (active && wave == 0) {
-    const f4v ov = {o.x, o.y, o.z, o.w};
-    st_sc1_f4(ov, rs, (sp * APART + j * D + d0) * 4);
-    const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
-    if (lane == 0) {
-      const f4v ml = {M, L, M1, L1};
-      st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
+  float4 r;
+  if (QKV && FA_PART_GRANULE) {
+    // publish this split's partial as granules tagged with the launch's epoch; poll the n_active splits' granules
+    // this lane folds (wave w: splits [4 w, 4 w + 4); head lane >> 5, dims [4 (lane & 31), +4) and the 4 (m, l))
+    unsigned long long* gp = a.gpart + (int64_t)g * FS * APART;
+    if (active && wave == 0) {
+      const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
+      const unsigned long long tg = (unsigned long long)ep_qkv << 32;
+      unsigned long long* po = gp + sp * APART + j * D + d0;
+      __hip_atomic_store(po + 0, tg | __float_as_uint(o.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(po + 1, tg | __float_as_uint(o.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(po + 2, tg | __float_as_uint(o.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(po + 3, tg | __float_as_uint(o.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < 4) {
+        const float v = lane == 0 ? M : lane == 1 ? L : lane == 2 ? M1 : L1;
+        __hip_atomic_store(gp + sp * APART + GQ * D + lane, tg | __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    STAMP(9);
+    if (threadIdx.x == 0)  // the launch counter (epoch source): one ticket per block, nobody waits on it
+      __hip_atomic_fetch_add(a.cnt + g * CNT_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int SPW = FS / AWV;
+    const int jj = lane >> 5, dd = (lane & 31) * 4;
+    const __amdgpu_buffer_rsrc_t rg = buf_rsrc(gp, FS * APART * 8);
+    f4v pml[SPW], pov[SPW];
+    SpinDeadline dl;
+    for (;;) {
+      bool ok = true;
+#pragma unroll
+      for (int t = 0; t < SPW; ++t) {
+        const int tt = min(wave * SPW + t, n_active - 1);  // clamped duplicates past n_active are not folded
+        const f4v m0 = ld_sc1_f4(rg, (tt * APART + GQ * D) * 8), m1 = ld_sc1_f4(rg, (tt * APART + GQ * D + 2) * 8);
+        const f4v o0 = ld_sc1_f4(rg, (tt * APART + jj * D + dd) * 8);
+        const f4v o1 = ld_sc1_f4(rg, (tt * APART + jj * D + dd + 2) * 8);
+        pml[t] = f4v{m0.x, m0.z, m1.x, m1.z};
+        pov[t] = f4v{o0.x, o0.z, o1.x, o1.z};
+        const unsigned e = ep_qkv;
+        ok = ok && __float_as_uint(m0.y) == e && __float_as_uint(m0.w) == e && __float_as_uint(m1.y) == e &&
+             __float_as_uint(m1.w) == e && __float_as_uint(o0.y) == e && __float_as_uint(o0.w) == e &&
+             __float_as_uint(o1.y) == e && __float_as_uint(o1.w) == e;
+      }
+      if (ok) break;
+      if (dl.expired()) {
+        __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    STAMP(10);
+    r = combine_fold(pml, pov, n_active, wave, lane);
+  } else {
+    float* pbase = a.partials + (int64_t)g * FS * APART;
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pbase, FS * APART * 4);
+    if (active && wave == 0) {
+      const f4v ov = {o.x, o.y, o.z, o.w};
+      st_sc1_f4(ov, rs, (sp * APART + j * D + d0) * 4);
+      const float M1 = lane_f(M, 32), L1 = lane_f(L, 32);  // head 1's (M, L) live in lanes 32..63
+      if (lane == 0) {
+        const f4v ml = {M, L, M1, L1};
+        st_sc1_f4(ml, rs, (sp * APART + GQ * D) * 4);
+      }
+    }
+    STAMP(9);
+    fanin_wait(a.cnt + g * CNT_LINE, FS, a.err);
+    STAMP(10);
+    // every split combines the n_active partials (combine_splits, as the last arriver of k_attn_block does)
+    r = combine_splits(rs, n_active, wave, lane);
   }
-  STAMP(9);
-  fanin_wait(a.cnt + g * CNT_LINE, FS, a.err);
-  STAMP(10);
-  // every split combines the n_active partials (combine_splits, as the last arriver of k_attn_block does)
   __shared__ __attribute__((aligned(16))) int8_t s_aq[GQ * D];
   __shared__ float s_ad[GQ * D / 32];
-  const float4 r = combine_splits(rs, n_active, wave, lane);
   if (wave == 0) {
     const int jj = lane >> 5, dd = (lane & 31) * 4;
     // q8_0 of the o projection's input (lanes 8b..8b+7 hold one 32-dim block), into LDS
@@ -2938,8 +3011,9 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err,
               x, psum ? psum : fw.pzero, psum ? xsum : nullptr, norm_w, wqkv_q, wqkv_d,
-              fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop};
+              fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop, fw.gpart};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
+  FA_REQUIRE(!FA_PART_GRANULE || fw.gpart, "qkv_attn_o_fused: partial granule workspace");
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, M), dim3(AWV * 64), 0, s, a);
 }
 

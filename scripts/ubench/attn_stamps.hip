@@ -64,6 +64,8 @@ int main(int argc, char** argv) {
   fw.opart = dalloc<float>(8 * 1024); fw.dpart = dalloc<float>(8 * 1024); fw.act = dalloc<float>(2 * 3072); CK(hipMemset(fw.act, 0, 2 * 3072 * 4));
   fw.xmid = dalloc<float>(1024); fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
   fw.gqkv = dalloc<unsigned long long>(4096); CK(hipMemset(fw.gqkv, 0, 4096 * 8));
+  fw.gpart = dalloc<unsigned long long>(8 * ATTN_SPLITS * ATTN_PART_FLOATS);
+  CK(hipMemset(fw.gpart, 0, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 8));
   CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   CK(hipMemset(fw.xmid, 0, 1024 * 4)); CK(hipMemset(fw.dpart, 0, 8 * 1024 * 4));
   const int nblk = fused_c ? 256 : M * KV * ATTN_SPLITS;

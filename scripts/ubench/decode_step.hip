@@ -73,6 +73,8 @@ int main(int argc, char** argv) {
   fw.opart = dalloc<float>(8 * E); fw.dpart = dalloc<float>(8 * E); fw.act = dalloc<float>(2 * F); CK(hipMemset(fw.act, 0, 2 * F * 4)); fw.xmid = dalloc<float>(E);
   fw.cnt = dalloc<unsigned>(FUSED_CNT_LINES * CNT_LINE); fw.err = dalloc<int>(1);
   fw.gqkv = dalloc<unsigned long long>(4096); CK(hipMemset(fw.gqkv, 0, 4096 * 8));
+  fw.gpart = dalloc<unsigned long long>(8 * ATTN_SPLITS * ATTN_PART_FLOATS);
+  CK(hipMemset(fw.gpart, 0, 8 * ATTN_SPLITS * ATTN_PART_FLOATS * 8));
   CK(hipMemset(fw.cnt, 0, FUSED_CNT_LINES * CNT_LINE * 4)); CK(hipMemset(fw.err, 0, 4));
   CK(hipMemset(fw.opart, 0, 8 * E * 4)); CK(hipMemset(fw.dpart, 0, 8 * E * 4)); CK(hipMemset(fw.xmid, 0, E * 4));
   wk.max_tokens = 1;
