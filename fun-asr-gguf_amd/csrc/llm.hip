@@ -1514,15 +1514,28 @@ struct AttnQIn {
 // it is in flight.
 // PIPE: the next pass's K/V loads are issued before this pass's math (2x the K/V registers: non-lean blocks only;
 // batch-1 B of the fused layer 7.44 -> 7.32 us, scripts/ubench/decode_step)
-template <int NI, int AW, bool PIPE>
+// PRE: the first pass's K/V (groups g0 + AW i, i < NI) were loaded by the caller (the first NI of AKV_PRE groups:
+// the same clamped addresses load_kv_groups<NI> would use)
+constexpr int AKV_PRE = 4;
+template <int NI, int AW, bool PIPE, bool PRE = false>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
-                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8]) {
+                                          float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
+                                          const int4* pk = nullptr, const int4* pv = nullptr) {
   int4 kt[NI], vt[NI];
-  load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-  load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+  if constexpr (PRE) {
+    static_assert(NI <= AKV_PRE, "attn_wave: preloaded groups");
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      kt[i] = pk[i];
+      vt[i] = pv[i];
+    }
+  } else {
+    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
+    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+  }
   __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
   if (decode) {
@@ -1680,14 +1693,16 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // split's softmax state in (M, L, o) for lane -> head j = lane >> 5, dims [d0, d0 + 4) (d0 = 4 (lane & 31)).
 // Shared by k_attn_block (partials + last-arriver combine) and k_attn_o (fused decode: every split combines, then
 // multiplies its slice of the o projection).
-template <int DM, int LEAN>
+template <int DM, int LEAN, bool PRE = false>
 __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, int seq, int nsplit, int H, int KV,
                                                  int64_t seq_stride, int64_t head_stride, __half* __restrict__ kc,
                                                  __half* __restrict__ vc, const float* __restrict__ qsrc,
                                                  const float* __restrict__ qn, const float* __restrict__ kn,
                                                  const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
                                                  float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
-                                                 float4& o, const AttnQIn* pre = nullptr) {
+                                                 float4& o, const AttnQIn* pre = nullptr, const int4* pk = nullptr,
+                                                 const int4* pv = nullptr) {
+  static_assert(!PRE || LEAN, "attn_split_merge: preloaded K/V with lean passes only (NI <= 4)");
   constexpr int D = 128;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_keys = pos + 1;
@@ -1722,8 +1737,10 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     AttnQIn qi;
     if (DM && pre) {  // the caller loaded the pos-independent inputs ahead of its pos read
       qi = *pre;
-      qi.c = rcos[(int64_t)pos * 64 + lane];
-      qi.sn = rsin[(int64_t)pos * 64 + lane];
+      if (!PRE) {  // PRE: the caller loaded the rope row with the first pass's K/V
+        qi.c = rcos[(int64_t)pos * 64 + lane];
+        qi.sn = rsin[(int64_t)pos * 64 + lane];
+      }
     } else if (DM) {
       const float* row = qsrc + (int64_t)m * (H + 2 * KV) * D;
 #pragma unroll
@@ -1754,14 +1771,14 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     __half* vd = vb + (int64_t)pos * D;
     const int ni = (ge - g0 + AWV - 1) / AWV;
     if (ni <= 1)
-      attn_wave<1, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<1, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 2)
-      attn_wave<2, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<2, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 4 || LEAN)
-      attn_wave<4, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
-                       s_q[wave], s_kn, s_vn, mx, l, acc);
+      attn_wave<4, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else
       attn_wave<8, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
@@ -2679,8 +2696,35 @@ struct AttnOArgs {
 #ifndef FA_PART_GRANULE
 #define FA_PART_GRANULE 0
 #endif
+// FA_KV_EARLY (two-launch layer): where each wave issues its first attention pass's K/V rows (the cached keys do not
+// depend on this launch's q|k|v) and the rope row: 0 = in the attention (after the q|k|v hand-off), 1 = after the
+// rmsnorm prologue (behind the q|k|v / o weights, ahead of the GEMV dots), 2 = after the q|k|v rows are published
+// (ahead of the hand-off poll). Graph-replayed step (scripts/gpu_r3_kv.sh, n_past 330): 2 = 465.6-466.1 us (AB 9.05-9.13),
+// 0 = 474.4-479.3 us (AB 9.50-9.64), 1 = 479.6-488.0 us (the K/V requests delay the GEMV's weight loads).
+#ifndef FA_KV_EARLY
+#define FA_KV_EARLY 2
+#endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
+
+// FA_KV_EARLY: the wave's first lean pass of attn_split_merge (groups gb + wave + AWV i, i < AKV_PRE, clamped as
+// load_kv_groups clamps them) and the rope row at pos, issued ahead of the attention. Splits past n_active and waves
+// without groups load nothing (their registers are never read).
+__device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int pos, int seq, int wave, int lane,
+                                         AttnQIn& qpre, int4 (&pk)[AKV_PRE], int4 (&pv)[AKV_PRE]) {
+  const int n_keys = pos + 1, n_groups = (n_keys + 3) >> 2;
+  const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)ASPLIT));
+  const int n_active = (int)ceilf((float)n_groups / (float)gps);
+  qpre.c = a.rcos[(int64_t)pos * 64 + lane];
+  qpre.sn = a.rsin[(int64_t)pos * 64 + lane];
+  if (sp >= n_active) return;
+  const int g0 = sp * gps + wave, ge = min(n_groups, sp * gps + gps);
+  if (g0 >= ge) return;
+  const __half* kb = a.kc + (int64_t)seq * a.seq_stride + g * a.head_stride;
+  const __half* vb = a.vc + (int64_t)seq * a.seq_stride + g * a.head_stride;
+  load_kv_groups<AKV_PRE, AWV>(kb, a.KV, g0, n_keys, lane >> 4, lane & 15, pk);
+  load_kv_groups<AKV_PRE, AWV>(vb, a.KV, g0, n_keys, lane >> 4, lane & 15, pv);
+}
 
 // QKV = true: the two-launch batch-1 layer. The 16 split blocks of kv head g first compute the 512 q|k|v rows that
 // head's attention reads (q heads GQ g .. GQ g + 1, k head g, v head g), FQ_ROWS each, with the prologue and the
@@ -2774,6 +2818,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
   STAMP(0);
+  int4 kpre[AKV_PRE], vpre[AKV_PRE];  // FA_KV_EARLY: the wave's first-pass K/V
   // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
   const int KO = a.H * D;
   // coalesced: load k reads rows 16 wave + 4 k + (lane >> 4) of the slice, 256 contiguous bytes each; lane chunk
@@ -2804,6 +2849,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       *reinterpret_cast<float4*>(a.xsum + threadIdx.x * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
     norm_quant_block_regs<4>(xv, xw, true, a.eps, 1024, s_xq, s_xd, s_red);
     __syncthreads();
+    if (FA_KV_EARLY == 1) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
     STAMP(12);
     // ---- the wave's QR rows (compute_group<1, 1, 0>'s arithmetic), published as two 16-B sc1 stores
     const int4 xq = *reinterpret_cast<const int4*>(s_xq + lane * 16);
@@ -2827,6 +2873,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
         __hip_atomic_store(a.gqkv + qrow0 + QR * wave + lane, ((unsigned long long)ep_qkv << 32) | __float_as_uint(yv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (FA_KV_EARLY == 2) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
     STAMP(13);
     // thread t: head g's local rows 2t, 2t + 1 (q head GQ g, q head GQ g + 1, k head g, v head g; 128 each)
     __shared__ float s_qkv[(GQ + 2) * D];
@@ -2885,9 +2932,11 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
   // QKV: lean passes (at most 4 groups per wave pass, no next-pass prefetch): the GEMV and the preloads need the
   // registers; identical arithmetic to k_attn_o<false> up to 4 groups per wave (n_past < 16 x 4 x 4 x 4 = 1024)
-  const bool active = attn_split_merge<1, QKV ? 1 : 0>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride, a.head_stride, a.kc,
-                                             a.vc, a.qkv, a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0,
-                                             M, L, o, &qpre);
+  constexpr bool PRE = QKV && FA_KV_EARLY != 0;
+  const bool active = attn_split_merge<1, QKV ? 1 : 0, PRE>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride,
+                                                            a.head_stride, a.kc, a.vc, a.qkv, a.qn, a.kn, a.rcos,
+                                                            a.rsin, a.eps, a.scale, n_active, j, d0, M, L, o, &qpre,
+                                                            kpre, vpre);
   float4 r;
   if (QKV && FA_PART_GRANULE) {
     // publish this split's partial as granules tagged with the launch's epoch; poll the n_active splits' granules
