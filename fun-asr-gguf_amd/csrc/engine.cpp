@@ -1383,6 +1383,14 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_ffn_pair_min_m = 4;
     fa::g_gemm_bf3_pf = 2;
     if (const char* g = getenv("FUNASR_BF3_PF")) fa::g_gemm_bf3_pf = atoi(g) >= 2 ? 2 : 1;
+    // 256x256 bf16x3 tiles from 192 tiles per launch (batched encoder; bit-identical outputs): scripts/ubench/
+    // gemm_f32_bench at M = 32032: 292-330 vs 243-276 TF/s f32-equivalent for the 128x128 tiles
+    fa::g_gemm_bf3_256 = 192;
+    if (const char* g = getenv("FUNASR_BF3_256")) fa::g_gemm_bf3_256 = std::max(0, atoi(g));
+    // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
+    // scripts/ubench/attn_batch at batch 32, 42.7 MB of K/V: 14.65 vs 15.7-15.9 us for the split blocks
+    fa::g_attn_wide = 256;
+    if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation

@@ -587,7 +587,9 @@ static void run_gemm16(const AL& al, const __half* W, int64_t ldw, int M, int N,
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ahead (1 or 2; FUNASR_BF3_PF)
-int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves
+int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
+                           // 6 = 256x256x32
+int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
 
 template <int WM, int WN, int KB>
 struct TileB3 {
@@ -781,6 +783,155 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
                      reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
+// 256x256x32 bf16x3 tile (batched encoder, C3): 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 accumulators of
+// 32x32, 512 threads, one block per CU. Per 16 of k a wave reads 12 fragments (4 + 2 tiles, two planes) for 24 MFMAs
+// (the 128x128 tile: 8 for 12), and a k-step has 48 MFMAs per wave between barriers. Same stage layout, operand maps,
+// per-element MFMA order (lo.hi, hi.lo, hi.hi per 16 of k, k ascending) and epilogue calls as k_gemm_bf3: every output
+// is bit-identical to the 128x128 and 64x64 tiles. LDS: two stages of 4 planes x 256 rows x 80 B = 160 KiB.
+#ifndef B3B_VARIANT
+// A/B only (scripts/gpu_r3_g256b.sh, M = 32032): 1 = MFMA blocks at raised wave priority (275-325 TF/s), 2 = also the
+// next stage stored between the k halves (193-229 TF/s); 0 (292-330 TF/s) stays
+#define B3B_VARIANT 0
+#endif
+constexpr int B3B_T = 512, B3B_BM = 256, B3B_BN = 256, B3B_KB = 32, B3B_LDK = B3B_KB + 8;
+constexpr int B3B_PA = B3B_BM * B3B_LDK, B3B_PB = B3B_BN * B3B_LDK;  // bf16 per plane
+constexpr int B3B_STAGE = 2 * (B3B_PA + B3B_PB);                     // [Ah][Al][Bh][Bl]
+constexpr int B3B_NA = B3B_BM * B3B_KB / 4 / B3B_T;                  // float4 of A per thread (4)
+constexpr int B3B_NB = B3B_BN * B3B_KB / 8 / B3B_T;                  // 8-bf16 chunks of each W plane per thread (2)
+constexpr size_t B3B_LDS = 2 * B3B_STAGE * 2;                        // bytes
+
+template <class AL>
+__device__ __forceinline__ void load_b3b(const AL& al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
+                                         int64_t ldw, int m0, int n0, int k0, int M, int N, int K,
+                                         float4 (&ra)[B3B_NA], uint4 (&rh)[B3B_NB], uint4 (&rl)[B3B_NB], int t) {
+  constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
+#pragma unroll
+  for (int i = 0; i < B3B_NA; ++i) {
+    const int idx = t + i * B3B_T;
+    ra[i] = al.load4(m0 + idx / R4, k0 + 4 * (idx % R4), M, K);
+  }
+#pragma unroll
+  for (int i = 0; i < B3B_NB; ++i) {
+    const int idx = t + i * B3B_T;  // K % 8 == 0
+    const int n = n0 + idx / R8, k = k0 + 8 * (idx % R8);
+    const bool in = n < N && k < K;
+    const int64_t o = (int64_t)n * ldw + k;
+    rh[i] = in ? *reinterpret_cast<const uint4*>(Wh + o) : make_uint4(0, 0, 0, 0);
+    rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void store_b3b(__bf16* st, const float4 (&ra)[B3B_NA], const uint4 (&rh)[B3B_NB],
+                                          const uint4 (&rl)[B3B_NB], int t) {
+  constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
+#pragma unroll
+  for (int i = 0; i < B3B_NA; ++i) {
+    const int idx = t + i * B3B_T;
+    const float4 v = ra[i];
+    const bf16x4 h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    const bf16x4 l = {(__bf16)(v.x - (float)h[0]), (__bf16)(v.y - (float)h[1]), (__bf16)(v.z - (float)h[2]),
+                      (__bf16)(v.w - (float)h[3])};
+    const int o = (idx / R4) * B3B_LDK + 4 * (idx % R4);
+    *reinterpret_cast<bf16x4*>(st + o) = h;
+    *reinterpret_cast<bf16x4*>(st + B3B_PA + o) = l;
+  }
+#pragma unroll
+  for (int i = 0; i < B3B_NB; ++i) {
+    const int idx = t + i * B3B_T;
+    const int o = (idx / R8) * B3B_LDK + 8 * (idx % R8);
+    *reinterpret_cast<uint4*>(st + 2 * B3B_PA + o) = rh[i];
+    *reinterpret_cast<uint4*>(st + 2 * B3B_PA + B3B_PB + o) = rl[i];
+  }
+}
+
+template <class AL, class EPI>
+__global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* __restrict__ Wh,
+                                                            const __bf16* __restrict__ Wl, int64_t ldw, int M, int N,
+                                                            int K, EPI epi) {
+  constexpr int WM = 4, WN = 2, LDK = B3B_LDK;
+  extern __shared__ float smem[];  // 2 stages; the epilogue reuses it
+  int tm, tn;
+  if (!xcd_tile((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, tm, tn)) return;
+  const int m0 = tm * B3B_BM, n0 = tn * B3B_BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int r = lane & 31, h = lane >> 5;
+  __bf16* sh = reinterpret_cast<__bf16*>(smem);
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  float4 ra[B3B_NA];
+  uint4 rh[B3B_NB], rl[B3B_NB];
+  load_b3b(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl, t);
+  store_b3b(sh, ra, rh, rl, t);
+  __syncthreads();
+  const int nk = (K + B3B_KB - 1) / B3B_KB;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_b3b(al, Wh, Wl, ldw, m0, n0, (kt + 1) * B3B_KB, M, N, K, ra, rh, rl, t);
+    const __bf16* stage = sh + cur * B3B_STAGE;
+    const __bf16* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
+    const __bf16* b = stage + 2 * B3B_PA + (wc * 32 * WN + r) * LDK + 8 * h;
+#pragma unroll
+    for (int kk = 0; kk < B3B_KB / 16; ++kk) {
+#if B3B_VARIANT == 2
+      if (kk == 1 && kt + 1 < nk) store_b3b(sh + (cur ^ 1) * B3B_STAGE, ra, rh, rl, t);
+#endif
+      bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(b + 32 * j * LDK + 16 * kk);
+        blo[j] = *reinterpret_cast<const bf16x8*>(b + B3B_PB + 32 * j * LDK + 16 * kk);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(a + 32 * i * LDK + 16 * kk);
+        alo[i] = *reinterpret_cast<const bf16x8*>(a + B3B_PA + 32 * i * LDK + 16 * kk);
+      }
+#if B3B_VARIANT >= 1
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], blo[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+#if B3B_VARIANT >= 1
+      __builtin_amdgcn_s_setprio(0);
+#endif
+    }
+#if B3B_VARIANT != 2
+    if (kt + 1 < nk) store_b3b(sh + (cur ^ 1) * B3B_STAGE, ra, rh, rl, t);
+#endif
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+  epi.finish(m0, n0, M, N, smem);
+}
+
+template <class AL, class EPI>
+static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                               hipStream_t s) {
+  FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3_256: K and ldw must be multiples of 8");
+  static bool attr = false;
+  if (!attr) {
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)B3B_LDS));
+    attr = true;
+  }
+  const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
+  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI>), grid, dim3(B3B_T), B3B_LDS, s, al,
+                     reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+}
+
 // microbenchmark helper: resident blocks per CU of the 128x128x32 bf16x3 kernel (linear epilogue), its dynamic LDS
 int gemm_bf3_occupancy_128() {
   using T = TileB3<2, 2, 32>;
@@ -798,7 +949,10 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
   const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   const bool pf = g_gemm_bf3_pf > 1;
-  if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
+  // 256x256 tiles while they still give most CUs a block (f == 6 forces them)
+  if (f == 6 || (f == 0 && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256))
+    launch_gemm_b3_256(al, w, ldw, M, N, K, epi, s);
+  else if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
   else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32>(al, w, ldw, M, N, K, epi, s);
   else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
     if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2>(al, w, ldw, M, N, K, epi, s);

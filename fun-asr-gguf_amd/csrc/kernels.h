@@ -111,6 +111,7 @@ int lm_head_parts(int O, int M);
 int gemm_k_splits(int O, int M, int K, int epi);  // K splits of the split-K GEMM form for this shape
 extern int g_attn_lean;    // -1 auto, 0/1 force the 128-VGPR attention variant (A/B)
 extern int g_attn_blocks;  // attention key-split target (blocks per launch), 1024 by default
+extern int g_attn_wide;    // decode launches with >= this many (token, kv head) pairs: 16-wave blocks, no splits
 extern int g_lm_head_mt6;    // LM head of 3-6 token batches in one block row (default 1)
 extern int g_sk_min_blocks;  // split-K shape choice: fewest blocks before fewer splits are preferred (default 256)
 extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 5); MFMA GEMM above
@@ -177,6 +178,7 @@ void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s, int M = 1);
 extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
+extern int g_gemm_bf3_256;    // bf16x3 GEMMs: 256x256 tiles when a launch has at least this many (0 = off)
 extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 4)
 // out[m] = xmid[m] + sum_p dpart[m][p] for m < M (a small batch's residual rows after its last fused layer)
 void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);

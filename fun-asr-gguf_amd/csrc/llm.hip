@@ -1463,6 +1463,7 @@ constexpr int GQ = 2;     // query heads per kv head (Qwen3-0.6B: 16 / 8)
 constexpr int AWV = 4;    // waves per block
 int g_attn_blocks = 1024;  // key splits are added while (token, kv head, split) blocks stay within this many
 int g_attn_lean = -1;      // -1: lean blocks when a launch needs more than 3 per CU; 0 / 1 force (A/B)
+int g_attn_wide = 0;       // decode launches with at least this many (token, kv head) pairs: one 16-wave block each
 constexpr int AGI = 16;   // 4-key groups per wave per pass (registers: 16 int4 of K + 16 of V)
 constexpr int ASPLIT = ATTN_SPLITS;  // key splits (blocks) per (token, kv head)
 constexpr int AMIN_G = 8;            // minimum 4-key groups per split (32 keys = 16 KB of K+V)
@@ -1693,7 +1694,7 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // split's softmax state in (M, L, o) for lane -> head j = lane >> 5, dims [d0, d0 + 4) (d0 = 4 (lane & 31)).
 // Shared by k_attn_block (partials + last-arriver combine) and k_attn_o (fused decode: every split combines, then
 // multiplies its slice of the o projection).
-template <int DM, int LEAN, bool PRE = false>
+template <int DM, int LEAN, bool PRE = false, int NW = AWV>
 __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, int seq, int nsplit, int H, int KV,
                                                  int64_t seq_stride, int64_t head_stride, __half* __restrict__ kc,
                                                  __half* __restrict__ vc, const float* __restrict__ qsrc,
@@ -1717,10 +1718,10 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   STAMP(1);
   __half* kb = kc + (int64_t)seq * seq_stride + g * head_stride;
   __half* vb = vc + (int64_t)seq * seq_stride + g * head_stride;
-  __shared__ float s_q[AWV][GQ][D];          // per-wave q (scaled, roped) in natural dim order
+  __shared__ float s_q[NW][GQ][D];          // per-wave q (scaled, roped) in natural dim order
   __shared__ float s_kn[D], s_vn[D];        // fresh K/V row (decode)
-  __shared__ float s_ml[AWV][GQ][2];
-  __shared__ float s_o[AWV][GQ][D];          // [wave][head][dim], summed over the wave's 4 key rows
+  __shared__ float s_ml[NW][GQ][2];
+  __shared__ float s_o[NW][GQ][D];          // [wave][head][dim], summed over the wave's 4 key rows
   const int kq = lane >> 4, dq = lane & 15;
   float mx[GQ], l[GQ], acc[GQ][8];
 #pragma unroll
@@ -1731,7 +1732,7 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     for (int e = 0; e < 8; ++e) acc[j][e] = 0.f;
   }
   const int fresh_group = DM ? (pos >> 2) : -1;
-  const bool fresh_here = fresh_group >= gb && fresh_group < ge && (fresh_group - gb) % AWV == wave;
+  const bool fresh_here = fresh_group >= gb && fresh_group < ge && (fresh_group - gb) % NW == wave;
   const int g0 = gb + wave;
   if (g0 < ge) {
     AttnQIn qi;
@@ -1769,18 +1770,18 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     }
     __half* kd = kb + (int64_t)pos * D;
     __half* vd = vb + (int64_t)pos * D;
-    const int ni = (ge - g0 + AWV - 1) / AWV;
+    const int ni = (ge - g0 + NW - 1) / NW;
     if (ni <= 1)
-      attn_wave<1, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+      attn_wave<1, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 2)
-      attn_wave<2, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+      attn_wave<2, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 4 || LEAN)
-      attn_wave<4, AWV, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
+      attn_wave<4, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else
-      attn_wave<8, AWV, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
+      attn_wave<8, NW, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
   }
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
@@ -1823,11 +1824,11 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   d0 = (lane & 31) * 4;
   M = -INFINITY;
 #pragma unroll
-  for (int w = 0; w < AWV; ++w) M = fmaxf(M, s_ml[w][j][0]);
+  for (int w = 0; w < NW; ++w) M = fmaxf(M, s_ml[w][j][0]);
   L = 0.f;
   o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int w = 0; w < AWV; ++w) {
+  for (int w = 0; w < NW; ++w) {
     const float mw = s_ml[w][j][0];
     const float wt = mw == -INFINITY ? 0.f : __expf(mw - M);
     L += wt * s_ml[w][j][1];
@@ -1903,8 +1904,10 @@ __device__ __forceinline__ float4 combine_splits(const __amdgpu_buffer_rsrc_t& r
   return combine_fold(pml, po, n_active, wave, lane);
 }
 
-template <int DM, int LEAN>
-__global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
+// NW = 16 (batched decode, one block per (token, kv head), n_active == 1 only): the 16 waves of one CU share the key
+// range, merged in LDS; no split partials, no combine hop
+template <int DM, int LEAN, int NW = AWV>
+__global__ __launch_bounds__(NW * 64, NW > AWV ? 1 : LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
                                                          int nsplit, int decode_mode, int H, int KV,
                                                          int64_t seq_stride, int64_t head_stride,
                                                          __half* __restrict__ kc,
@@ -1927,11 +1930,11 @@ __global__ __launch_bounds__(AWV * 64, LEAN ? 4 : 1) void k_attn_block(const int
   int n_active, j, d0;
   float M, L;
   float4 o;
-  if (!attn_split_merge<DM, LEAN>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc, qn, kn, rcos,
-                                  rsin, eps, scale, n_active, j, d0, M, L, o))
+  if (!attn_split_merge<DM, LEAN, false, NW>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc,
+                                              qn, kn, rcos, rsin, eps, scale, n_active, j, d0, M, L, o))
     return;
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;  // j, d0: wave 0's lane map
-  if (n_active == 1) {
+  if (NW != AWV || n_active == 1) {  // NW != AWV: the host launches one split
     if (wave != 0) return;
     const float4 r = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
     *reinterpret_cast<float4*>(op) = r;
@@ -2138,6 +2141,12 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // key splits only while (token, kv head) blocks alone leave the chip idle: 16 at batch 1-4, 4 at batch 32, 1 for
   // prefill. Batch 32 measured 14.7-17.0 us for every target of 256-1024 blocks, lean or not (attn_batch.hip): the
   // K/V stream of 512 (sequence, kv head) pairs comes in at ~2.8 TB/s whatever the block shape.
+  if (decode_mode && g_attn_wide > 0 && M * KV >= g_attn_wide) {  // one 16-wave block per (token, kv head)
+    hipLaunchKernelGGL((k_attn_block<1, 1, 16>), dim3(KV, 1, M), dim3(16 * 64), 0, s, tok_seq, tok_pos, 1, decode_mode,
+                       H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters,
+                       wk.partials, qout, dout);
+    return;
+  }
   int ns = 1;
   while (ns < std::min(ASPLIT, max_splits) && (ns + 1) * M * KV <= g_attn_blocks) ++ns;
   FA_REQUIRE(ns == 1 || M <= wk.max_split_tokens, "attn_block: split partials workspace too small");

@@ -1,6 +1,7 @@
 // Batched decode attention (C3 shape): 32 tokens, each its own sequence at n_past in [200, 460], 28 layers of
 // distinct fp16 K/V caches (cold, like the engine), graph-replayed. Prints us per launch and the K/V bytes
 // rate for each (split target, lean) setting.
+#include <cmath>
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -38,9 +39,24 @@ int main(int argc, char** argv) {
   const double bytes = keys * KV * D * 2 * 2;  // K and V rows read per layer
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   printf("n_ctx per sequence slot %d\n", NCTX);
-  for (int target : {256, 512, 768, 1024}) {
+  {  // 16-wave blocks (one per (token, kv head)) vs the default split blocks: outputs agree to f32 rounding
+    std::vector<float> ref((size_t)M * H * D), wide((size_t)M * H * D);
+    for (int w : {0, 1}) {
+      g_attn_wide = w; g_attn_blocks = 1024; g_attn_lean = -1;
+      attn_block(qkv, 1, qn, qn, 1e-6f, rc, rs, kc, vc, M, H, KV, seq, pos, seq_stride, att, wk, s);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy((w ? wide : ref).data(), att, ref.size() * 4, hipMemcpyDeviceToHost));
+    }
+    double e = 0, mx = 0;
+    for (size_t i = 0; i < ref.size(); ++i) { e = std::max(e, (double)std::fabs(ref[i] - wide[i])); mx = std::max(mx, (double)std::fabs(ref[i])); }
+    printf("wide vs split blocks: max|diff| %.3g of max %.3g %s\n", e, mx, e <= 1e-5 * mx ? "ok" : "FAIL");
+    g_attn_wide = 0;
+  }
+  for (int target : {-1, 256, 512, 768, 1024}) {
     for (int lean : {0, 1}) {
-      g_attn_blocks = target; g_attn_lean = lean;
+      if (target < 0 && lean == 0) continue;
+      g_attn_wide = target < 0 ? 1 : 0;
+      g_attn_blocks = target < 0 ? 1024 : target; g_attn_lean = lean;
       hipGraph_t g; hipGraphExec_t ex;
       CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       for (int l = 0; l < L; ++l)
@@ -52,7 +68,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
       CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
       const double us = ms * 1e3 / R / L;
-      printf("blocks target %4d lean %d: %6.2f us per launch, K/V %.1f MB -> %.2f TB/s\n", target, lean, us, bytes / 1e6,
+      printf("%s target %4d lean %d: %6.2f us per launch, K/V %.1f MB -> %.2f TB/s\n", target < 0 ? "wide  " : "blocks", target, lean, us, bytes / 1e6,
              bytes / (us * 1e-6) / 1e12);
       CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
     }
