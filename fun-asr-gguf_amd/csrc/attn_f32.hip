@@ -301,12 +301,22 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// FA_ATTN_TRV = 1: V is split into bf16 planes while staged too ([key][D + 32] rows) and the V^T fragments are read with
+// ds_read_b64_tr_b16 (4 keys x 16 dims per 16-lane group, two reads per plane per fragment), instead of 8 f32 LDS
+// reads + 8 in-register splits per fragment. Row stride D + 32 bf16 (16 or 48 mod 64 dwords): the two 16-lane groups
+// of a 32-lane half read 4 rows x 8 dwords each on 64 distinct banks. Same split values, same MFMA order: outputs
+// bit-identical to FA_ATTN_TRV = 0.
+#ifndef FA_ATTN_TRV
+#define FA_ATTN_TRV 1
+#endif
 template <int D>
 struct AttnLds3 {
   static constexpr int SK = D + 8;                   // K plane row (bf16): 16-B reads of 16 rows, distinct bank groups
   static constexpr int KP = AK * SK;                 // bf16 per K plane
   static constexpr int VOFF = 2 * KP / 2;            // V tile offset (floats) after the Kh, Kl planes
-  static constexpr int STAGE = VOFF + AttnLds<D>::TILE;  // floats per stage
+  static constexpr int SV = D + 32;                  // V plane row (bf16, FA_ATTN_TRV)
+  static constexpr int VP = AK * SV;                 // bf16 per V plane
+  static constexpr int STAGE = VOFF + (FA_ATTN_TRV ? VP : AttnLds<D>::TILE);  // floats per stage
   static constexpr int BYTES_PIPE = 2 * STAGE * 4;
   static constexpr int BYTES_OUT = AttnLds<D>::BYTES_OUT;
   static constexpr int BYTES = (BYTES_PIPE > BYTES_OUT ? BYTES_PIPE : BYTES_OUT) + 2 * AQ * 4 + 16;
@@ -327,8 +337,26 @@ __device__ __forceinline__ void attn3_store_tile(float* st, const f4v (&pk)[AK *
                        (__bf16)(v.w - (float)hi[3])};
     *reinterpret_cast<bf16x4*>(kb + key * L::SK + 4 * d4) = hi;
     *reinterpret_cast<bf16x4*>(kb + L::KP + key * L::SK + 4 * d4) = lo;
-    *reinterpret_cast<f4v*>(vs_ + key * AttnLds<D>::S + 4 * d4) = pv[c];
+    if constexpr (FA_ATTN_TRV) {
+      __bf16* vb = reinterpret_cast<__bf16*>(vs_);
+      const f4v w = pv[c];
+      const bf16x4 vh = {(__bf16)w.x, (__bf16)w.y, (__bf16)w.z, (__bf16)w.w};
+      const bf16x4 vl = {(__bf16)(w.x - (float)vh[0]), (__bf16)(w.y - (float)vh[1]), (__bf16)(w.z - (float)vh[2]),
+                         (__bf16)(w.w - (float)vh[3])};
+      *reinterpret_cast<bf16x4*>(vb + key * L::SV + 4 * d4) = vh;
+      *reinterpret_cast<bf16x4*>(vb + L::VP + key * L::SV + 4 * d4) = vl;
+    } else {
+      *reinterpret_cast<f4v*>(vs_ + key * AttnLds<D>::S + 4 * d4) = pv[c];
+    }
   }
+}
+
+// 4 keys x 1 dim per lane from a row-major bf16 [key][SV] plane: lane 4q + p of its 16-lane group supplies row q,
+// columns 4p .. 4p + 3 of the group's 4 x 16 block and receives column (lane & 15) of the 4 rows (T10)
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x4 ld_tr4(const __bf16* p) {
+  const v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
+  return __builtin_bit_cast(bf16x4, v);
 }
 
 template <int D>
@@ -434,12 +462,24 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
 #pragma unroll
       for (int i = 0; i < NDT; ++i) {
         bf16x8 vh, vl;
+        if constexpr (FA_ATTN_TRV) {
+          // lane group gq = lane >> 4: keys 16 s2 + 4 (gq >> 1) (+ 8), dims 32 i + 16 (gq & 1) + 0..15; this lane's
+          // address: row (lane >> 2) & 3 of the block, columns 4 (lane & 3) .. +3
+          const __bf16* vb = reinterpret_cast<const __bf16*>(vs_);
+          const int gq = lane >> 4, key = 16 * s2 + 4 * (gq >> 1) + ((lane >> 2) & 3);
+          const int off = key * L::SV + 32 * i + 16 * (gq & 1) + 4 * (lane & 3);
+          const bf16x4 h0 = ld_tr4(vb + off), h1 = ld_tr4(vb + off + 8 * L::SV);
+          const bf16x4 l0 = ld_tr4(vb + L::VP + off), l1 = ld_tr4(vb + L::VP + off + 8 * L::SV);
+          vh = bf16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+          vl = bf16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int key = 16 * s2 + 8 * (j >> 2) + 4 * h + (j & 3);
-          const float x = vs_[key * AttnLds<D>::S + i * 32 + r];
-          vh[j] = (__bf16)x;
-          vl[j] = (__bf16)(x - (float)vh[j]);
+          for (int j = 0; j < 8; ++j) {
+            const int key = 16 * s2 + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float x = vs_[key * AttnLds<D>::S + i * 32 + r];
+            vh[j] = (__bf16)x;
+            vl[j] = (__bf16)(x - (float)vh[j]);
+          }
         }
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o[i], 0, 0, 0);
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o[i], 0, 0, 0);

@@ -292,6 +292,61 @@ struct EpiArgmax128 {
   }
 };
 
+// The same for the 256x256 tile (8 waves as 2 x 4, each 4 x 2 sub-tiles): [256 rows][8 slices] winners, per-wave
+// scratch, partial (value, index) per (row, 256-column tile). argmax_combine is associative with the lower index
+// winning ties, so the winners equal the 128-column tiling's.
+struct EpiArgmax256 {
+  const float* bias;
+  float* pval;   // [M][n_tiles]
+  int* pidx;
+  int n_tiles;
+  __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
+    const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 7;
+    const int col = col0 + (lane & 31);
+    const float b = col < N ? bias[col] : 0.f;
+    float* sv = lds;                               // [256 rows][8 slices]
+    int* si = reinterpret_cast<int*>(lds + 2048);  // [256][8]
+    float* scr = lds + 4096 + wave * (32 * 33);    // [32 rows][33]
+    const int slice = (col0 & 255) >> 5, rb = row0 & 255;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      scr[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = col < N ? acc[r] + b : -INFINITY;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int lr = lane >> 1, c0 = 16 * (lane & 1);  // lane pair -> row lr, columns [c0, c0 + 16)
+    float v = scr[lr * 33 + c0];
+    int i = col0 + c0 < N ? col0 + c0 : 0x7fffffff;
+#pragma unroll
+    for (int c = 1; c < 16; ++c) {
+      const int cc = col0 + c0 + c;
+      argmax_combine(v, i, scr[lr * 33 + c0 + c], cc < N ? cc : 0x7fffffff);
+    }
+    argmax_combine(v, i, __shfl_xor(v, 1, 64), __shfl_xor(i, 1, 64));
+    if ((lane & 1) == 0) {
+      sv[(rb + lr) * 8 + slice] = v;
+      si[(rb + lr) * 8 + slice] = i;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the scratch is rewritten by the next sub-tile
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __device__ __forceinline__ void finish(int m0, int n0, int M, int N, float* lds) const {
+    const float* sv = lds;
+    const int* si = reinterpret_cast<const int*>(lds + 2048);
+    __syncthreads();
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < M) {
+      const int lr = threadIdx.x;
+      float v = sv[lr * 8];
+      int i = si[lr * 8];
+#pragma unroll
+      for (int c = 1; c < 8; ++c) argmax_combine(v, i, sv[lr * 8 + c], si[lr * 8 + c]);
+      pval[(int64_t)(m0 + lr) * n_tiles + n0 / 256] = v;
+      pidx[(int64_t)(m0 + lr) * n_tiles + n0 / 256] = i;
+    }
+  }
+};
+
 // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one L2,
 // MI355X_MICROARCH.md "Workgroup dispatch"), so block b takes tile id (b % 8) * per + b / 8: each XCD owns one
 // contiguous run of tile ids, and ids run through bands of 4 M-tiles (all N-tiles of a band, M fastest), so an XCD's
@@ -1023,7 +1078,11 @@ void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* b
                      int* pidx, int* out, hipStream_t s, const __half* W16, WSplit wb) {
   ALoadPlain al{A, lda};
   int n_tiles = cdiv(N, 64);
-  if (wb.hi) {  // bf16x3: 128x128 blocks (one clip: 1001 x 60515 = 3784 tiles; 64x64 measured 606 us)
+  if (wb.hi && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256) {  // batched: 256x256
+    n_tiles = cdiv(N, 256);
+    EpiArgmax256 epi{bias, pval, pidx, n_tiles};
+    launch_gemm_b3_256(al, wb, K, M, N, K, epi, s);
+  } else if (wb.hi) {  // bf16x3: 128x128 blocks (one clip: 1001 x 60515 = 3784 tiles; 64x64 measured 606 us)
     n_tiles = cdiv(N, 128);
     EpiArgmax128 epi{bias, pval, pidx, n_tiles};
     launch_gemm_b3<ALoadPlain, EpiArgmax128, 2, 2, 32>(al, wb, K, M, N, K, epi, s);

@@ -25,23 +25,25 @@ int main() {
     std::vector<int> hl(B, T); int* lens; CK(hipMalloc(&lens, B * 4));
     CK(hipMemcpy(lens, hl.data(), B * 4, hipMemcpyHostToDevice));
     const double flops = 4.0 * B * T * (double)T * d;
+   for (int bf3 : {0, 1}) {
     for (int ks : {0, 1, 2, 4, 8}) {
       if (B > 1 && ks > 1) continue;
       g_attn_f32_force_splits = ks;
       hipGraph_t g; hipGraphExec_t ex;
       const int n = B > 1 ? 4 : L;
       CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      for (int i = 0; i < n; ++i) attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, out, d, B, T, H, Dh, lens, wk, s);
+      for (int i = 0; i < n; ++i) attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, out, d, B, T, H, Dh, lens, wk, s, 0, bf3);
       CK(hipStreamEndCapture(s, &g)); CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       CK(hipGraphLaunch(ex, s)); CK(hipStreamSynchronize(s));
       hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
       CK(hipEventRecord(a, s)); for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
       CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
       const double us = ms * 1e3 / (3.0 * n);
-      printf("batch %2d splits %d%s: %8.1f us per launch  %6.1f TF/s\n", B, ks ? ks : attn_f32_splits(B, T, H),
-             ks ? "" : " (default)", us, flops / us / 1e6);
+      printf("%s batch %2d splits %d%s: %8.1f us per launch  %6.1f TF/s\n", bf3 ? "bf16x3" : "f32   ", B,
+             ks ? ks : attn_f32_splits(B, T, H), ks ? "" : " (default)", us, flops / us / 1e6);
       CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
     }
+   }
     CK(hipFree(qkv)); CK(hipFree(out)); CK(hipFree(lens));
   }
   return 0;

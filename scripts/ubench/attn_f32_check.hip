@@ -1,4 +1,5 @@
 // attn_f32 (encoder attention) vs a CPU double reference over split / partial-tile / masked cases.
+#include <cstring>
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -101,10 +102,13 @@ int main() {
     CK(hipMalloc(&dq, qkv.size() * 4)); CK(hipMalloc(&dout, out.size() * 4)); CK(hipMalloc(&dl, c.B * 4));
     CK(hipMemcpy(dq, qkv.data(), qkv.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dl, lens.data(), c.B * 4, hipMemcpyHostToDevice));
+   for (int bf3 : {0, 1}) {
     for (int rep = 0; rep < 2; ++rep)
-      attn_f32(dq, dq + d, dq + 2 * d, 3 * d, 3 * d, 3 * d, dout, d, c.B, c.T, c.H, c.Dh, dl, wk, st);
+      attn_f32(dq, dq + d, dq + 2 * d, 3 * d, 3 * d, 3 * d, dout, d, c.B, c.T, c.H, c.Dh, dl, wk, st, 0, bf3);
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t hsh = 1469598103934665603ull;  // FNV-1a of the output bits (build-to-build bit identity)
+    for (float v : out) { uint32_t u; memcpy(&u, &v, 4); hsh = (hsh ^ u) * 1099511628211ull; }
     double maxerr = 0, maxref = 0;
     const double scale = std::pow((double)c.Dh, -0.5);
     std::vector<double> sc(c.T);
@@ -134,8 +138,10 @@ int main() {
         }
     const bool ok = maxerr < 1e-4 * std::max(1.0, maxref);
     bad += !ok;
-    printf("B=%d T=%4d H=%d D=%3d len0=%4d splits=%d  max|err|=%.3g (max|ref| %.3g) %s\n", c.B, c.T, c.H, c.Dh, c.len0,
-           attn_f32_splits(c.B, c.T, c.H), maxerr, maxref, ok ? "ok" : "FAIL");
+    printf("%s B=%d T=%4d H=%d D=%3d len0=%4d splits=%d  max|err|=%.3g (max|ref| %.3g) hash %016llx %s\n",
+           bf3 ? "bf16x3" : "f32   ", c.B, c.T, c.H, c.Dh, c.len0, attn_f32_splits(c.B, c.T, c.H), maxerr, maxref,
+           (unsigned long long)hsh, ok ? "ok" : "FAIL");
+   }
     CK(hipFree(dq)); CK(hipFree(dout)); CK(hipFree(dl));
   }
   return bad != 0;
