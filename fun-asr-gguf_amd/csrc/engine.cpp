@@ -975,6 +975,29 @@ struct Engine {
     }
   }
 
+  // CTC head alone over a caller's encoder output (the CTC graph's own session, decoder.py:27: ctc_decoder with
+  // mask=None, then ctc_lo and argmax, model_definition.py:335-337): T rows, every key unmasked. Uses the encode
+  // buffers, so the previous encode's outputs are gone afterwards (fa_encode_fetch then fails).
+  void ctc_head(const float* enc_host, int T, int32_t* ids_out) {
+    FA_REQUIRE(T >= 1 && T <= tl_max, "fa_ctc_head: T out of range (1 .. the T_lfr of max_samples)");
+    const int d = ec.d_model;
+    last_batch = 0;
+    if (enc_fp16) prepare_fp16();
+    else if (enc_gemm) prepare_bf3();
+    if (!hp_meta) {
+      FA_HIP(hipHostMalloc(&hp_meta, (size_t)(kEncLanes + 1) * max_batch * 6 * sizeof(int64_t), hipHostMallocDefault));
+    }
+    int32_t* hm32 = reinterpret_cast<int32_t*>(hp_meta + (size_t)meta_slot * max_batch * 6 + max_batch);
+    hm32[3 * max_batch] = T;
+    FA_HIP(hipMemcpyAsync(d_ctclen, hm32 + 3 * max_batch, 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(enc, enc_host, (size_t)T * d * 4, hipMemcpyHostToDevice, stream));
+    run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, T, T, d_ctclen);
+    gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, T, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w),
+                    WB(ctc_w));
+    FA_HIP(hipMemcpyAsync(ids_out, ctc_ids, (size_t)T * 4, hipMemcpyDeviceToHost, stream));
+    FA_HIP(hipStreamSynchronize(stream));
+  }
+
   // ---------------------------------------------------------------------------------------------
   // prefill rows -> query tiles of <= 64 consecutive positions of one sequence (uploaded on the stream; host copy
   // kept in h_ptiles until the next call). Below attn_pf_min_m rows (or head dim != 128) the per-row path runs.
@@ -1609,6 +1632,13 @@ int fa_encode(fa_engine* h, const float* pcm, const int64_t* n_samples, int32_t 
   else e->encode_device(e->d_pcm, n_samples, batch, stride);
   int r = fa_encode_fetch(h, audio_embd_out, tgt_stride, ctc_ids_out, ids_stride, t_lfr_out, target_len_out, enc_out);
   if (r != FA_OK) return r;
+  FA_API_END
+}
+
+int fa_ctc_head(fa_engine* h, const float* enc, int32_t T, int32_t* ids_out) {
+  FA_API_BEGIN
+  FA_REQUIRE(enc && ids_out, "fa_ctc_head args");
+  h->e->ctc_head(enc, T, ids_out);
   FA_API_END
 }
 

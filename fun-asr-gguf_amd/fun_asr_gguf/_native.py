@@ -21,7 +21,7 @@ EXPORTS = [
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
-    "fa_llm_invariant_width", "fa_set_encode_mode",
+    "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head",
 ]
 
 
@@ -75,6 +75,7 @@ def load():
     lib.fa_encode_device.argtypes = [P, P, P, I32, I64]
     lib.fa_encode_fetch.argtypes = [P, P, I64, P, I64, P, P, P]
     lib.fa_ctc_collapse.argtypes = [P, I32, P, P, I64, P]
+    lib.fa_ctc_head.argtypes = [P, P, I32, P]
     lib.fa_set_debug.argtypes = [P, I32]
     lib.fa_set_encoder_fp16.argtypes = [P, I32]
     lib.fa_set_decode_fused.argtypes = [P, I32]
@@ -283,6 +284,13 @@ class Engine:
             out["lfr_embedded"] = lfr[:t0]
             _check(self.lib.fa_set_debug(self.h, 0), "fa_set_debug")
         return out
+
+    def ctc_head(self, enc):
+        """The CTC graph alone over encoder rows enc [T, d_model] -> argmax ids [T] int32 (fa_ctc_head)."""
+        enc = np.ascontiguousarray(enc, np.float32)
+        ids = np.zeros(enc.shape[0], np.int32)
+        _check(self.lib.fa_ctc_head(self.h, _ptr(enc), enc.shape[0], _ptr(ids)), "fa_ctc_head")
+        return ids
 
     def ctc_collapse(self, blank_id, n_clips):
         stride = self.frame_counts(self.max_samples)[2] + 1

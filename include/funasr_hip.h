@@ -104,6 +104,10 @@ int fa_encode_device(fa_engine* e, const float* d_pcm, const int64_t* n_samples,
 int fa_pcm_upload(fa_engine* e, const float* pcm, int64_t n_floats);
 int fa_encode_fetch(fa_engine* e, float* audio_embd_out, int64_t tgt_stride, int32_t* ctc_ids_out,
                     int64_t ids_stride, int32_t* t_lfr_out, int32_t* target_len_out, float* enc_out);
+/* The CTC graph alone (ctc_sess.run({"enc_output": ...}), decoder.py:27): ctc_decoder with no mask, ctc_lo and
+ * argmax (model_definition.py:335-337) over T caller-given encoder rows enc [T, d_model] f32 (fp16 graph: fp16
+ * values) -> ids_out [T]. Reuses the encode buffers: the outputs of the previous fa_encode cannot be fetched after. */
+int fa_ctc_head(fa_engine* e, const float* enc, int32_t T, int32_t* ids_out);
 /* Greedy CTC collapse on device (nano_ctc.py:65-104): for clip b, compacted (id, first_frame) pairs
  * with blanks (= blank_id) and repeats removed; n_out[b] = count. */
 int fa_ctc_collapse(fa_engine* e, int32_t blank_id, int32_t* ids_out, int32_t* frames_out, int64_t out_stride,
