@@ -45,9 +45,10 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gather_world2_equals_single(world):
-    """world 2 and 3 (uneven LPT shares: 6 segments over 3 ranks, one rank with the short one)."""
+    """world 2 and 3 (uneven LPT shares: 6 segments over 3 ranks, one rank with the short one) and 8 (the driver's
+    8-GPU C4 shape: 6 segments over 8 ranks, two ranks with no segment)."""
     from fun_asr_gguf.parallel import to_record, from_record
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
