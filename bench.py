@@ -69,6 +69,21 @@ def cpu_baseline():
                       f"(README.md:292-306 laptop CPU anchor: 7.19 s)"}
 
 
+def pmc_mfma_busy(mode):
+    """MFMA-pipe busy fraction per encoder kernel class from the committed counter pass of `mode` (scripts/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES over the CUs' cycles while the class runs, rocprofv3 --pmc on bench.py itself), or {}."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_mfma_{mode}*.json")))
+    if not files:
+        return {}
+    try:
+        d = json.load(open(files[-1]))
+        return {k: round(v["mfma_busy"], 4) for k, v in d.items() if isinstance(v, dict) and "mfma_busy" in v}, \
+            os.path.basename(files[-1])
+    except Exception:
+        return {}
+
+
 def pmc_traffic():
     """Per-launch HBM bytes of the decode GEMV class from the committed PMC pass (scripts/pmc_traffic.py,
     rocprofv3 --pmc FETCH_SIZE with the gfx950 x2 correction), or None when no summary is present."""
@@ -476,6 +491,13 @@ def headline(args, world, dt, dt_prof, prof, stage):
             tfs = e["flops"] / (e["ms"] / 1e3) / 1e12
             roof[key] = {"achieved_TFs": round(tfs, 2), "peak_TFs": round(enc_peak, 1), "arith": "bf16x3" if bf3 else "f32",
                          "frac": round(tfs / enc_peak, 4), "avg_launch_us": round(e["ms"] * 1e3 / e["launches"], 2)}
+            busy = pmc_mfma_busy("bf16x3" if bf3 else "f32")
+            if busy:
+                cls = {"encoder_gemm": "encoder GEMM (bf16x3)" if bf3 else "encoder GEMM (exact f32 / STFT / mel)",
+                       "encoder_attention": "encoder attention (bf16x3)" if bf3 else "encoder attention (exact f32)"}[key]
+                if cls in busy[0]:  # counter-derived MFMA utilisation (the batch-32 encode of the PMC pass)
+                    roof[key]["mfma_busy"] = busy[0][cls]
+                    roof[key]["mfma_busy_source"] = "profiles/" + busy[1]
     lm = prof[4]
     if lm["launches"]:
         lm_s = lm["ms"] / lm["launches"] / 1e3
