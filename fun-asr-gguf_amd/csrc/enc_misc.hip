@@ -202,9 +202,61 @@ __global__ __launch_bounds__(256) void k_fsmn(const float* __restrict__ v, int64
   }
 }
 
+// Batched encodes, 16-B lanes: a lane owns 4 consecutive channels (one float4 per row; a wave reads 1 KB rows as 16 B
+// per lane instead of 4), FR rows. The per-channel arithmetic is k_fsmn's (same taps, same fmaf order): bit-identical.
+template <int FR>
+__global__ __launch_bounds__(256) void k_fsmn4(const float* __restrict__ v, int64_t ldv, const float* __restrict__ w,
+                                               float* __restrict__ out, int64_t ldo, int rows, int C,
+                                               const int* __restrict__ lens, int t_stride, int r16) {
+  constexpr int LP = (FSMN_K - 1) / 2, NW = FR + FSMN_K - 1;
+  const int c = 4 * (blockIdx.x * 64 + (threadIdx.x & 63));
+  const int r0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * FR;
+  if (c >= C || r0 >= rows) return;
+  float4 wk[FSMN_K], win[NW];
+#pragma unroll
+  for (int j = 0; j < FSMN_K; ++j)
+    wk[j] = make_float4(r16e(w[c * FSMN_K + j], r16), r16e(w[(c + 1) * FSMN_K + j], r16),
+                        r16e(w[(c + 2) * FSMN_K + j], r16), r16e(w[(c + 3) * FSMN_K + j], r16));
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int q = min(max(r0 - LP + i, 0), rows - 1);  // clamped address; out-of-clip taps are skipped below
+    win[i] = *reinterpret_cast<const float4*>(v + (int64_t)q * ldv + c);
+  }
+#pragma unroll
+  for (int i = 0; i < FR; ++i) {
+    const int r = r0 + i;
+    if (r >= rows) break;
+    const int b = r / t_stride, lo = b * t_stride, hi = lo + (lens ? lens[b] : t_stride);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < FSMN_K; ++j) {
+      const int q = r - LP + j;
+      const bool in = q >= lo && q < hi;
+      acc.x = fmaf(wk[j].x, in ? win[i + j].x : 0.f, acc.x);
+      acc.y = fmaf(wk[j].y, in ? win[i + j].y : 0.f, acc.y);
+      acc.z = fmaf(wk[j].z, in ? win[i + j].z : 0.f, acc.z);
+      acc.w = fmaf(wk[j].w, in ? win[i + j].w : 0.f, acc.w);
+    }
+    const bool sv = r < hi;
+    const float4 self = win[i + LP];
+    *reinterpret_cast<float4*>(out + (int64_t)r * ldo + c) =
+        make_float4(r16e(r16e(acc.x, r16) + (sv ? self.x : 0.f), r16), r16e(r16e(acc.y, r16) + (sv ? self.y : 0.f), r16),
+                    r16e(r16e(acc.z, r16) + (sv ? self.z : 0.f), r16), r16e(r16e(acc.w, r16) + (sv ? self.w : 0.f), r16));
+  }
+}
+
+int g_fsmn_vec = 1;  // FUNASR_FSMN_VEC=0: the 4-B-lane kernel for batched encodes too (A/B)
+
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
           const int* lens, int t_stride, hipStream_t s, int r16) {
   FA_REQUIRE(ksize == FSMN_K, "fsmn: kernel size 11 (SenseVoiceSmall sanm_shfit 0, kernel_size 11)");
+  const bool vec = g_fsmn_vec && C % 256 == 0 && ldv % 4 == 0 && ldo % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(v) | reinterpret_cast<uintptr_t>(out)) % 16 == 0;
+  if (vec && (int64_t)cdiv(C, 256) * cdiv(rows, 4 * 16) >= 512) {
+    hipLaunchKernelGGL(k_fsmn4<16>, dim3(cdiv(C, 256), cdiv(rows, 4 * 16)), dim3(256), 0, s, v, ldv, w, out, ldo, rows,
+                       C, lens, t_stride, r16);
+    return;
+  }
   if ((int64_t)cdiv(C, 64) * cdiv(rows, 4 * 32) >= 512)
     hipLaunchKernelGGL(k_fsmn<32>, dim3(cdiv(C, 64), cdiv(rows, 4 * 32)), dim3(256), 0, s, v, ldv, w, out, ldo, rows, C,
                        lens, t_stride, r16);

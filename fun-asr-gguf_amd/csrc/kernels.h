@@ -114,6 +114,7 @@ extern int g_attn_blocks;  // attention key-split target (blocks per launch), 10
 extern int g_attn_wide;    // decode launches with >= this many (token, kv head) pairs: 16-wave blocks, no splits
 extern int g_lm_head_mt6;    // LM head of 3-6 token batches in one block row (default 1)
 extern int g_sk_min_blocks;  // split-K shape choice: fewest blocks before fewer splits are preferred (default 256)
+extern int g_fsmn_vec;       // 1 (default): 16-B-lane FSMN kernel for batched encodes; 0: 4-B lanes (A/B)
 extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 5); MFMA GEMM above
 extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)
 bool gemv_small(int M);
