@@ -5,14 +5,19 @@ q8_0 Qwen3 prefill of 73 + 126 + 5 tokens, 253 greedy decode steps with EOS igno
 Synthetic seeded audio and synthetic weights of the full architecture (no checkpoints ship).
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  N>1, either form:
+    python bench.py --gpus N ...          (this script spawns N rank processes itself, before any GPU call)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0. value = total audio seconds of all ranks / max-over-ranks wall time of the
-K timed steps (inputs resident in HBM: fa_pcm_upload before the timed region).
+K timed steps (inputs resident in HBM: fa_pcm_upload before the timed region). n_gpus = the RCCL world size.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,6 +36,54 @@ BF16X3_PEAK_TFS = 2500.0 / 3.0           # bf16 dense 2.5 PF/s, three bf16 produ
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv, script=None, grace_s=30.0):
+    """`python bench.py --gpus N` without a launcher: start N fresh rank processes of `script` (default this file)
+    with torchrun's environment (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
+    MASTER_PORT), one GPU each (the rank binds device LOCAL_RANK). The parent imports no torch and makes no GPU call
+    (a process that has initialised HIP must not start GPU children by exec, and needs no device here). Rank 0's
+    stdout (the JSON line) is returned; the other ranks' stdout and every rank's stderr pass through to stderr. When a
+    rank fails, the others get `grace_s` to exit (a peer blocked in a collective never will) and are then killed by
+    PID. -> (worst exit code, rank 0's stdout)."""
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BENCH_LAUNCHER="spawn")
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, stderr=None))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed_at = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            break
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.monotonic()
+            log(f"bench launcher: rank(s) {[r for r, rc in enumerate(rcs) if rc not in (None, 0)]} failed")
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p, rc in zip(procs, rcs):
+                if rc is None:
+                    p.send_signal(signal.SIGKILL)
+        time.sleep(0.2)
+    reader.join(timeout=10)
+    rcs = [p.returncode for p in procs]
+    worst = max(rcs, key=lambda rc: (rc != 0, abs(rc)))
+    text = out0[0].decode("utf-8", "replace") if out0 and out0[0] else ""
+    return worst, text
 
 
 def cpu_baseline():
@@ -284,7 +337,8 @@ def c4_leg(steps, warmup, device, model, barrier, dist):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of the job; without WORLD_SIZE in the environment, N > 1 spawns N ranks")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -296,9 +350,20 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (300 s long-audio) leg")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # no launcher: become one: N fresh rank processes, started before this process touches a GPU
+        rc, text = spawn_ranks(args.gpus, sys.argv[1:])
+        if text:
+            sys.stdout.write(text)
+            sys.stdout.flush()
+        sys.exit(rc if 0 <= rc < 256 else 128 + (-rc if rc < 0 else 1))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    args.launcher = os.environ.get("BENCH_LAUNCHER", "torchrun" if world > 1 else "single")
     dist = None
     if world > 1:
         import torch
@@ -306,6 +371,7 @@ def main():
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
     def barrier():
         if dist is not None:
@@ -511,13 +577,15 @@ def headline(args, world, dt, dt_prof, prof, stage):
            "config": {"workload": "configs[1]: single 60 s clip per GPU per step, fp32 encoder + CTC + q8_0 LLM "
                                   "(73+126+5 prefill, 253 greedy steps, EOS ignored)",
                       "model": "Fun-ASR-Nano (SenseVoiceSmall enc 70 SANM blocks + Qwen3-0.6B q8_0)",
-                      "global_batch": world, "seq_len": int(CLIP_S * SR), "parallelism": f"dp{world}"},
+                      "global_batch": world, "seq_len": int(CLIP_S * SR), "parallelism": f"dp{world}",
+                      "ranks": world, "launcher": args.launcher,
+                      "gpus_flag": args.gpus if args.gpus is not None else world},
            "stage_ms": {k: round(v / args.steps * 1e3, 3) for k, v in zip(
                ["encode", "ctc", "prompt", "prefill", "generate", "align"], stage)},
            "profiled_pass_ms_per_step": round(dt_prof / args.steps * 1e3, 3),
            "kernel_class_avg_us": {names[c]: round(prof[c]["ms"] * 1e3 / max(1, prof[c]["launches"]), 2) for c in prof},
            "roofline": roof}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:  # on rank 0 at N = 1 only
         try:
             out["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # reported, never fatal for the GPU number

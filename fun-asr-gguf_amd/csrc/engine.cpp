@@ -206,6 +206,8 @@ struct Engine {
     }
     if (ev_fork) hipEventDestroy(ev_fork);
     if (hp_meta) hipHostFree(hp_meta);
+    for (hipEvent_t ev : ev_meta)
+      if (ev) hipEventDestroy(ev);
     for (auto& g : step_graphs) hipGraphExecDestroy(g.second);
     for (auto& e : ev_pool) {
       hipEventDestroy(e.first);
@@ -809,6 +811,17 @@ struct Engine {
   int encode_mode = 0;  // 0: padded batch; 1: independent clips in concurrent lanes
   int64_t* hp_meta = nullptr;  // pinned per-clip length records: region 0 = batch encode, 1 + lane = lane encode
   int meta_slot = 0;
+  hipEvent_t ev_meta[kEncLanes + 1] = {};  // recorded after a region's copies; the host waits on it before rewriting
+  // the pinned record of meta_slot, once the copies that last read it (an earlier call, still queued) have run
+  int64_t* meta_region() {
+    if (!hp_meta) {
+      FA_HIP(hipHostMalloc(&hp_meta, (size_t)(kEncLanes + 1) * max_batch * 6 * sizeof(int64_t), hipHostMallocDefault));
+    }
+    hipEvent_t& ev = ev_meta[meta_slot];
+    if (ev) FA_HIP(hipEventSynchronize(ev));
+    else FA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return hp_meta + (size_t)meta_slot * max_batch * 6;
+  }
   hipEvent_t ev_fork = nullptr;
 
   EncBind enc_bind() const {
@@ -917,10 +930,7 @@ struct Engine {
     last_tstride = ts;
     // the per-clip lengths go up from pinned host memory owned by the engine (one region per encode lane), so no
     // copy depends on when the runtime reads a pageable source (the lane loop reuses the host vectors at once)
-    if (!hp_meta) {
-      FA_HIP(hipHostMalloc(&hp_meta, (size_t)(kEncLanes + 1) * max_batch * 6 * sizeof(int64_t), hipHostMallocDefault));
-    }
-    int64_t* hm = hp_meta + (size_t)meta_slot * max_batch * 6;
+    int64_t* hm = meta_region();
     int32_t* hm32 = reinterpret_cast<int32_t*>(hm + max_batch);
     for (int b = 0; b < batch; ++b) {
       hm[b] = n_samples[b];
@@ -934,6 +944,7 @@ struct Engine {
     FA_HIP(hipMemcpyAsync(d_tlfr, hm32 + max_batch, batch * 4, hipMemcpyHostToDevice, stream));
     FA_HIP(hipMemcpyAsync(d_tgt, hm32 + 2 * max_batch, batch * 4, hipMemcpyHostToDevice, stream));
     FA_HIP(hipMemcpyAsync(d_ctclen, hm32 + 3 * max_batch, batch * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipEventRecord(ev_meta[meta_slot], stream));
     // F1-F4
     if (enc_fp16) prepare_fp16();
     else if (enc_gemm) prepare_bf3();
@@ -984,12 +995,10 @@ struct Engine {
     last_batch = 0;
     if (enc_fp16) prepare_fp16();
     else if (enc_gemm) prepare_bf3();
-    if (!hp_meta) {
-      FA_HIP(hipHostMalloc(&hp_meta, (size_t)(kEncLanes + 1) * max_batch * 6 * sizeof(int64_t), hipHostMallocDefault));
-    }
-    int32_t* hm32 = reinterpret_cast<int32_t*>(hp_meta + (size_t)meta_slot * max_batch * 6 + max_batch);
+    int32_t* hm32 = reinterpret_cast<int32_t*>(meta_region() + max_batch);
     hm32[3 * max_batch] = T;
     FA_HIP(hipMemcpyAsync(d_ctclen, hm32 + 3 * max_batch, 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipEventRecord(ev_meta[meta_slot], stream));
     FA_HIP(hipMemcpyAsync(enc, enc_host, (size_t)T * d * 4, hipMemcpyHostToDevice, stream));
     run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, T, T, d_ctclen);
     gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, T, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w),

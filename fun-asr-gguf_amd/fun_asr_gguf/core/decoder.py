@@ -107,8 +107,25 @@ class LLMDecoder:
         seed = int(np.random.randint(0, 2 ** 31 - 1))  # decoder.py:89: fresh seed per call
         return dict(temperature=temperature, top_p=top_p, top_k=top_k, seed=seed)
 
+    def slot_capacity(self):
+        """Sequence slots of the engine (its KV cache holds max_seqs sequences; a host stand-in: config.max_batch)."""
+        eng = self.models.engine
+        cap = getattr(eng, "llm_cfg", None)
+        cap = cap.get("max_seqs") if isinstance(cap, dict) else getattr(eng, "max_seqs", None)
+        if not cap:
+            cap = getattr(getattr(self.models, "config", None), "max_batch", None)
+        return max(1, int(cap or 1 << 30))  # no stated capacity (a bare stand-in): one group
+
     def decode_many(self, embds, n_predict, temperature=0.3, top_p=1.0, top_k=50, reporter=None, stream_output=False):
-        """Prefill every sequence, then decode them as one continuous batch. -> [LLMDecodeResult]"""
+        """Prefill every sequence, then decode them as one continuous batch. -> [LLMDecodeResult]
+        More sequences than the engine has slots run as consecutive groups of slot_capacity()."""
+        cap = self.slot_capacity()
+        if len(embds) > cap:
+            out = []
+            for i in range(0, len(embds), cap):
+                n_p = n_predict[i:i + cap] if isinstance(n_predict, (list, tuple)) else n_predict
+                out += self.decode_many(embds[i:i + cap], n_p, temperature, top_p, top_k, reporter, stream_output)
+            return out
         eng = self.models.engine
         cfg = self.models.config
         samp = self._sampling(temperature, top_p, top_k)

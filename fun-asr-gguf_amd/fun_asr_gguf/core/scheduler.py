@@ -17,6 +17,7 @@ sharded over N GPUs gives exactly the 1-GPU results. Wider batches (padded encod
 the M > 6 decode kernels) agree to the fp32 / q8_0 noise floors.
 """
 import time
+import warnings
 from typing import List, Optional
 
 import numpy as np
@@ -87,6 +88,7 @@ class ContinuousBatcher:
         # within the engine's invariant width every clip is encoded and prefilled alone and decodes with its
         # single-sequence arithmetic: results are exactly the one-clip-at-a-time results, whatever the grouping
         alone = S <= invariant_width(eng)
+        invariance_lost = False
         n_admit = n_encode_batches = 0
         t_enc = t_pre = t_wait = 0.0
         self.n_chunks = 0
@@ -94,6 +96,17 @@ class ContinuousBatcher:
 
         ready = []  # encoded clips (front done) waiting for a slot
         enc_cap = eng.max_batch if hasattr(eng, "max_batch") else S
+
+        def check_width():
+            # the engine's invariant width can drop during the run (a fused fan-in timeout moves it to the 5-launch
+            # layer for good, fa_llm_invariant_width 6 -> 1): later batches are then no longer bit-identical to
+            # one-clip decoding. Re-read before every admission and decode chunk; say so once, in stats and a warning
+            nonlocal alone, invariance_lost
+            if alone and S > invariant_width(eng):
+                alone, invariance_lost = False, True
+                warnings.warn(f"decode batches of {S} now exceed the engine's invariant width "
+                              f"({invariant_width(eng)}): results from here on agree with one-clip decoding to the "
+                              "q8_0 noise floor, not bit for bit", RuntimeWarning)
 
         def encode_ahead(need):
             # clips are encoded ahead of their admission in encoder batches of the engine's full capacity (a padded
@@ -116,6 +129,7 @@ class ContinuousBatcher:
 
         def admit(k):
             nonlocal n_admit, t_pre
+            check_width()
             encode_ahead(k)
             jobs = [ready.pop(0) for _ in range(min(k, len(ready)))]
             slots = [free.pop(0) for _ in jobs]
@@ -170,12 +184,14 @@ class ContinuousBatcher:
                         continue
                     if not active:
                         break
+                    check_width()
                     pending = self._begin(eng, active, waiting(), len(free), admit_min, samp)
                 jobs, chunk = pending
                 t = time.perf_counter()
                 toks = eng.llm_generate_end()
                 t_wait += time.perf_counter() - t
                 pending = None
+                check_width()
                 # sequences this chunk leaves unfinished, decided from the token ids alone (stop ids, n_predict), get
                 # the next chunk enqueued BEFORE the host detokenises this one (host work overlaps the GPU's) -- unless
                 # the slots it frees are due for an admission (a prefill cannot run while a chunk is in flight). A
@@ -206,6 +222,7 @@ class ContinuousBatcher:
             for j, r in zip(retry, rs):
                 done[j.idx] = (j, r)
         self.stats = dict(admissions=n_admit, encode_batches=n_encode_batches, retried=len(retry), chunks=self.n_chunks,
+                          slots=S, batch_invariant=not invariance_lost and S <= invariant_width(eng),
                           encode_s=round(t_enc, 4), prefill_s=round(t_pre, 4), generate_wait_s=round(t_wait, 4),
                           total_s=round(time.perf_counter() - t_run, 4))
         out = []

@@ -17,9 +17,18 @@ def _frames(n):
 
 
 class FakeEngine:
-    def __init__(self):
+    """max_seqs: slot range like the native engine's KV cache ('seq out of range' beyond it). loop_below: sampling
+    temperatures below it emit one repeated token (the repetition breaker cuts such a decode), like a looping model."""
+
+    def __init__(self, max_seqs=None, loop_below=None):
         self.last = []
         self.seqs = {}
+        self.max_seqs = max_seqs
+        self.loop_below = loop_below
+
+    def _slot(self, s):
+        if self.max_seqs is not None and not 0 <= s < self.max_seqs:
+            raise RuntimeError(f"fa_llm_reset: seq out of range ({s} of {self.max_seqs})")
 
     def encode(self, clips, want_enc=False, resident=None, independent=False):
         self._idle("encode")
@@ -55,10 +64,12 @@ class FakeEngine:
 
     def llm_reset(self, s):
         self._idle("llm_reset")
+        self._slot(s)
         self.seqs.pop(s, None)
 
     def llm_prefill(self, s, embd, **samp):
         self._idle("llm_prefill")
+        self._slot(s)
         h = int(np.abs(embd).sum() * 1000) % 100003
         self.seqs[s] = h
         return 1000 + h % 20
@@ -69,6 +80,10 @@ class FakeEngine:
     def llm_generate(self, seqs, n, **samp):
         out = np.zeros((len(seqs), n), np.int32)
         for r, s in enumerate(seqs):
+            self._slot(s)
+            if self.loop_below is not None and samp.get("temperature", 0.0) < self.loop_below:
+                out[r, :] = 1000
+                continue
             for k in range(n):
                 self.seqs[s] = (self.seqs[s] * 1103515245 + 12345) % 2147483647
                 out[r, k] = 1000 + self.seqs[s] % 40
@@ -91,11 +106,11 @@ class FakeEngine:
             raise RuntimeError(f"{what}: a generate call is in flight")
 
 
-def fake_models(max_batch=4, n_predict=24):
+def fake_models(max_batch=4, n_predict=24, ignore_eos=True, loop_below=None):
     cfg = ASREngineConfig(encoder_onnx_path="synthetic", ctc_onnx_path="synthetic", decoder_gguf_path="synthetic",
-                          tokens_path="synthetic", n_predict=n_predict, max_batch=max_batch, ignore_eos=True)
+                          tokens_path="synthetic", n_predict=n_predict, max_batch=max_batch, ignore_eos=ignore_eos)
     m = ModelManager(cfg)
-    m.engine = FakeEngine()
+    m.engine = FakeEngine(max_seqs=max_batch, loop_below=loop_below)
     m.vocab = SyntheticVocab(N_VOCAB)
     m.eos_token = m.vocab.eos
     m.ctc_id2token = CTCSyntheticTokens(CTC_VOCAB)
@@ -104,11 +119,11 @@ def fake_models(max_batch=4, n_predict=24):
     return m
 
 
-def fake_api(max_batch=4, n_predict=24):
+def fake_api(max_batch=4, n_predict=24, ignore_eos=True, loop_below=None):
     from fun_asr_gguf import FunASREngine
     api = FunASREngine("synthetic", "synthetic", "synthetic", "synthetic", n_predict=n_predict, max_batch=max_batch,
-                       ignore_eos=True)
-    m = fake_models(max_batch, n_predict)
+                       ignore_eos=ignore_eos)
+    m = fake_models(max_batch, n_predict, ignore_eos, loop_below)
     api.models = m
     api.orchestrator.models = m
     api.orchestrator.decoder.models = m

@@ -460,3 +460,90 @@ def test_encoder_batch_vs_alone_f32_order(eng):
         assert np.array_equal(ind["audio_embd"][b], one["audio_embd"][0]), f"segment {b}: audio rows"
         assert np.array_equal(ind["enc"][b], one["enc"][0]) and np.array_equal(ind["ctc_ids"][b], one["ctc_ids"][0])
         assert np.array_equal(pairs[b][0], p1[0]) and np.array_equal(pairs[b][1], p1[1]), f"segment {b}: collapse"
+
+
+def test_continuous_batching_slot_reuse_equals_per_clip():
+    """configs[2]'s continuous batch with slot reuse, within the invariant width (N2): 10 ragged clips (3-20 s) with
+    mixed decode lengths (5-40 tokens) on 4 sequence slots through decode_segments (core/scheduler.py: a finished
+    clip's slot is refilled with the next clip, prefilled between decode chunks, while the other slots are mid-decode).
+    Every clip's text, n_gen, CTC tokens and char timestamps equal decoding that clip alone bit for bit (the reference
+    decodes every segment alone: orchestrator.py:139-171 -> core/decoder.py:132-246)."""
+    from fun_asr_gguf import create_asr_engine
+    from fun_asr_gguf.synthetic import synth_audio
+    api = create_asr_engine("synthetic", "synthetic", "synthetic", "synthetic", verbose=False, model="full",
+                            max_batch=4, n_ctx=512, n_predict=40, ignore_eos=True)
+    try:
+        secs = [3.0, 17.5, 8.2, 20.0, 5.1, 12.7, 3.9, 15.3, 9.6, 6.4]
+        n_pred = [5, 40, 12, 33, 7, 38, 21, 9, 26, 17]
+        clips = [synth_audio(int(s * SR), 900 + i) for i, s in enumerate(secs)]
+        orch = api.orchestrator
+        got = orch.decode_segments(clips, None, None, False, 0.0, 1.0, 50, n_predicts=n_pred)
+        st = dict(orch.batcher.stats)
+        assert st["admissions"] == 10 > st["slots"] == 4 and st["batch_invariant"], st
+        for i, (c, n, g) in enumerate(zip(clips, n_pred, got)):
+            one = orch.decode_segments([c], None, None, False, 0.0, 1.0, 50, n_predicts=[n])[0]
+            assert g.n_gen == one.n_gen == n, (i, g.n_gen, one.n_gen)
+            assert g.ctc_results == one.ctc_results, f"clip {i}: CTC tokens"
+            assert g.text == one.text, f"clip {i}: text"
+            assert g.aligned == one.aligned, f"clip {i}: char timestamps"
+        assert api.models.engine.llm_invariant_width() == 6
+    finally:
+        api.cleanup()
+
+
+def test_llm_full_slot_reuse_above_width_bound(eng, g60):
+    """Slot reuse above the invariant width (configs[2] shape): 40 ragged prompts on 32 slots. Slots 0-31 are prefilled
+    as one batch; the first 8 clips stop after 8 steps, and their slots take clips 32-39 (one 8-prompt admission
+    prefill while 24 sequences are mid-decode, slots reset and reused with their stale K/V rows still in the cache);
+    then every slot decodes together, in admission order. 16 steps per clip, teacher-forced on each clip's single-stream
+    tokens: the batch-32 bound of test_llm_full_batch32_vs_single_streams_bound (cosine >= 0.9995, equal argmax where
+    the single-stream top-2 margin exceeds 0.15)."""
+    adaptor = g60["adaptor"].astype(np.float32)
+    base = _bench_prompts(eng, adaptor, 40)
+    prompts = [p[:204 - 3 * (i % 7)] if i % 7 else p for i, p in enumerate(base)]  # ragged: 186-204 rows
+    K = 16
+    single = _single_runs(eng, prompts, K)
+    n_steps = [8] * 8 + [K] * 32
+    slot_of, k_of, order = {}, {}, []
+    for s in range(32):
+        eng.llm_reset(s)
+    eng.llm_prefill_batch(list(range(32)), prompts[:32])
+    for c in range(32):
+        slot_of[c], k_of[c] = c, 0
+        order.append(c)
+    worst = 1.0
+
+    def check(c):
+        nonlocal worst
+        lg, ref = eng.llm_logits(slot_of[c]), single[c][1][k_of[c]]
+        cs = _cos(lg, ref)
+        worst = min(worst, cs)
+        assert cs >= 0.9995, f"clip {c} step {k_of[c]}: cosine {cs}"
+        top2 = np.sort(ref)[-2:]
+        if top2[1] - top2[0] > 0.15:
+            assert int(np.argmax(lg)) == int(np.argmax(ref)), f"clip {c} step {k_of[c]}: argmax"
+
+    for c in order:
+        check(c)
+    admitted = False
+    while order:
+        for c in order:
+            eng.llm_set_token(slot_of[c], single[c][0][k_of[c]])
+        eng.llm_generate([slot_of[c] for c in order], 1)
+        for c in order:
+            k_of[c] += 1
+            check(c)
+        order = [c for c in order if k_of[c] < n_steps[c]]
+        if not admitted and len(order) == 24:  # clips 0-7 finished: their slots take clips 32-39
+            freed = sorted(set(range(32)) - {slot_of[c] for c in order})
+            assert freed == list(range(8))
+            for s in freed:
+                eng.llm_reset(s)
+            eng.llm_prefill_batch(freed, prompts[32:40])
+            for c, s in zip(range(32, 40), freed):
+                slot_of[c], k_of[c] = s, 0
+                check(c)
+                order.append(c)
+            admitted = True
+    assert admitted and all(k_of[c] == n_steps[c] for c in range(40))
+    print(f"slot reuse above the width: worst cosine {worst:.6f}")
