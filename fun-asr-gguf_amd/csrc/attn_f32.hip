@@ -300,6 +300,8 @@ __global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, c
 //   Softmax, masking, key splits and the epilogue are the exact-f32 kernel's.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8a __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4a __attribute__((ext_vector_type(4)));
 
 // FA_ATTN_TRV = 1: V is split into bf16 planes while staged too ([key][D + 32] rows) and the V^T fragments are read with
 // ds_read_b64_tr_b16 (4 keys x 16 dims per 16-lane group, two reads per plane per fragment), instead of 8 f32 LDS
@@ -322,7 +324,7 @@ struct AttnLds3 {
   static constexpr int BYTES = (BYTES_PIPE > BYTES_OUT ? BYTES_PIPE : BYTES_OUT) + 2 * AQ * 4 + 16;
 };
 
-template <int D>
+template <int D, int P = 3>
 __device__ __forceinline__ void attn3_store_tile(float* st, const f4v (&pk)[AK * D / 1024], const f4v (&pv)[AK * D / 1024]) {
   using L = AttnLds3<D>;
   __bf16* kb = reinterpret_cast<__bf16*>(st);
@@ -331,6 +333,14 @@ __device__ __forceinline__ void attn3_store_tile(float* st, const f4v (&pk)[AK *
   for (int c = 0; c < AK * D / 1024; ++c) {
     const int f = threadIdx.x + 256 * c;
     const int key = f / (D / 4), d4 = f % (D / 4);
+    if constexpr (P == 1) {  // fp16 graph: K and V are fp16 values, one exact f16 plane each
+      const f4v v = pk[c], w = pv[c];
+      _Float16* kh = reinterpret_cast<_Float16*>(st);
+      _Float16* vh = reinterpret_cast<_Float16*>(vs_);
+      *reinterpret_cast<f16x4a*>(kh + key * L::SK + 4 * d4) = f16x4a{(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+      *reinterpret_cast<f16x4a*>(vh + key * L::SV + 4 * d4) = f16x4a{(_Float16)w.x, (_Float16)w.y, (_Float16)w.z, (_Float16)w.w};
+      continue;
+    }
     const f4v v = pk[c];
     const bf16x4 hi = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
     const bf16x4 lo = {(__bf16)(v.x - (float)hi[0]), (__bf16)(v.y - (float)hi[1]), (__bf16)(v.z - (float)hi[2]),
@@ -358,8 +368,17 @@ __device__ __forceinline__ bf16x4 ld_tr4(const __bf16* p) {
   const v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
   return __builtin_bit_cast(bf16x4, v);
 }
+__device__ __forceinline__ f16x4a ld_tr4h(const _Float16* p) {
+  const v4i16 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(p));
+  return __builtin_bit_cast(f16x4a, v);
+}
 
-template <int D>
+// P = 1: the fp16 graph's attention (C5) on v_mfma_f32_32x32x16_f16: q, k and v are fp16 values (outputs of the fp16
+// q|k|v projection), so S^T = K . Q^T is one f16 MFMA per 16 of k with exact products (d^-0.5 applied to the f32
+// scores after the dot), and O^T += V^T . P^T is two (P^T split into f16 hi + lo in registers, V^T exact): the
+// attention stays f32 arithmetic on fp16 inputs with its output rounded to fp16, the oracle's contract
+// (oracle/encoder_fp16.py); 3 MFMAs per 16 keys x 16 dims instead of the exact-f32 form's 8 x 64 cycles
+template <int D, int P = 3>
 __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
@@ -381,8 +400,10 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
   const int n_kt = (t_stride + AK - 1) / AK;
   const int tpk = (n_kt + KS - 1) / KS;
   const int kt0 = ks * tpk, kt1 = min(n_kt, kt0 + tpk);
-  // this wave's 32 queries, pre-scaled (python: q * d_k**-0.5 before the dot), split into bf16 fragments
+  // this wave's 32 queries, pre-scaled (python: q * d_k**-0.5 before the dot), split into bf16 fragments (P = 1: the
+  // fp16 q values as they are, scaled after the dot)
   bf16x8 qh[NKS], ql[NKS];
+  f16x8a qf[NKS];
   {
     const int q = min(q0 + wave * 32 + r, t_stride - 1);
     const float* p = Q + (row_base + q) * ldq + head * D + 8 * h;
@@ -390,6 +411,11 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     for (int st = 0; st < NKS; ++st) {
       const float4 a = *reinterpret_cast<const float4*>(p + 16 * st);
       const float4 b = *reinterpret_cast<const float4*>(p + 16 * st + 4);
+      if constexpr (P == 1) {
+        qf[st] = f16x8a{(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w, (_Float16)b.x, (_Float16)b.y,
+                        (_Float16)b.z, (_Float16)b.w};
+        continue;
+      }
       const float x[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale, b.x * scale, b.y * scale, b.z * scale,
                           b.w * scale};
 #pragma unroll
@@ -406,7 +432,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
   f4v pk[AK * D / 1024], pv[AK * D / 1024];
   if (kt0 < kt1) {
     attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt0, pk, pv);
-    attn3_store_tile<D>(lds, pk, pv);
+    attn3_store_tile<D, P>(lds, pk, pv);
   }
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
@@ -416,13 +442,23 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     const float* vs_ = lds + stage * L::STAGE + L::VOFF;
     const int k0 = kt * AK;
     f32x16 s = {};
+    if constexpr (P == 1) {
+      const _Float16* kf_ = reinterpret_cast<const _Float16*>(kh_);
 #pragma unroll
-    for (int st = 0; st < NKS; ++st) {
-      const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kh_ + r * L::SK + 16 * st + 8 * h);
-      const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kh_ + L::KP + r * L::SK + 16 * st + 8 * h);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], s, 0, 0, 0);
+      for (int st = 0; st < NKS; ++st) {
+        const f16x8a kf = *reinterpret_cast<const f16x8a*>(kf_ + r * L::SK + 16 * st + 8 * h);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[st], s, 0, 0, 0);
+      }
+      s *= scale;
+    } else {
+#pragma unroll
+      for (int st = 0; st < NKS; ++st) {
+        const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kh_ + r * L::SK + 16 * st + 8 * h);
+        const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kh_ + L::KP + r * L::SK + 16 * st + 8 * h);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], s, 0, 0, 0);
+      }
     }
     // mask + online softmax (as k_attn_f32)
     float mt = -INFINITY;
@@ -453,6 +489,25 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     // O^T[d][q] += V^T[d][key] P^T[key][q]: P^T k-step s2 = registers 8 s2 .. 8 s2 + 7 (keys 16 s2 + kl(j))
 #pragma unroll
     for (int s2 = 0; s2 < AK / 16; ++s2) {
+      if constexpr (P == 1) {
+        f16x8a ph, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ph[j] = (_Float16)s[8 * s2 + j];
+          pl[j] = (_Float16)(s[8 * s2 + j] - (float)ph[j]);
+        }
+        const _Float16* vb = reinterpret_cast<const _Float16*>(vs_);
+        const int gq = lane >> 4, key = 16 * s2 + 4 * (gq >> 1) + ((lane >> 2) & 3);
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) {
+          const int off = key * L::SV + 32 * i + 16 * (gq & 1) + 4 * (lane & 3);
+          const f16x4a h0 = ld_tr4h(vb + off), h1 = ld_tr4h(vb + off + 8 * L::SV);
+          const f16x8a vh = f16x8a{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+          o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[i], 0, 0, 0);
+          o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[i], 0, 0, 0);
+        }
+        continue;
+      }
       bf16x8 ph, pl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -486,14 +541,15 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o[i], 0, 0, 0);
       }
     }
-    if (kt + 1 < kt1) attn3_store_tile<D>(lds + (stage ^ 1) * L::STAGE, pk, pv);
+    if (kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
     __syncthreads();
   }
-  attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, 0, part, cnt,
-                   L::BYTES);
+  attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, P == 1 ? 1 : 0,
+                   part, cnt, L::BYTES);
 }
 
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
+int g_attn_f16_mfma = 1;          // fp16 graph attention on f16 MFMAs (k_attn_bf3<D, 1>); 0: exact f32 + rounding (A/B)
 
 int attn_f32_splits(int batch, int t_stride, int n_heads) {
   if (g_attn_f32_force_splits > 0) return g_attn_f32_force_splits;
@@ -522,7 +578,19 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
     (void)hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<64>::BYTES);
     (void)hipFuncSetAttribute((const void*)k_attn_bf3<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<128>::BYTES);
     (void)hipFuncSetAttribute((const void*)k_attn_bf3<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<64>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<128>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<64, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<64>::BYTES);
     attr_set = true;
+  }
+  if (r16 && g_attn_f16_mfma) {
+    FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
+    if (head_dim == 128)
+      hipLaunchKernelGGL((k_attn_bf3<128, 1>), grid, dim3(256), AttnLds3<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    else
+      hipLaunchKernelGGL((k_attn_bf3<64, 1>), grid, dim3(256), AttnLds3<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    return;
   }
   if (bf3 && !r16) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");

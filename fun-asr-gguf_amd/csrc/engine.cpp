@@ -364,6 +364,93 @@ struct Engine {
     return it->second;
   }
   void weights_changed() { w16_stale = wb_stale = true; }
+
+  // ---- int8-dynamic CTC graph (Fun-ASR-Nano-CTC.int8.onnx, the reference README's default CTC model: 02-Quantize-ONNX.py
+  // :38-46): every CTC-graph linear with an ORT dynamic-quant weight (fa_set_tensor_u8dq) runs DynamicQuantizeLinear +
+  // MatMulInteger + f32 rescale (gemm_f32.hip) instead of the f32 GEMM, once all of them have one (and fa_set_ctc_int8
+  // has not turned it off). Regions are the CTC graph's f32 GEMM weight regions (q|k|v concatenated as in f32).
+  struct U8Region {
+    int N = 0, K = 0;
+    int8_t* q = nullptr;
+    int *cs = nullptr, *bz = nullptr;
+    float* ws = nullptr;
+    std::vector<char> row_set;
+    int n_set = 0;
+  };
+  std::vector<const float*> ctc_regions;          // registration order
+  std::unordered_map<const float*, U8Region> u8w;  // f32 region base -> its int8 form
+  int ctc_i8 = 1;
+  fa::U8Work u8wk;                                 // activation workspace of the batch encode (lanes own theirs)
+  void ctc_region(const float* w, int N, int K) {
+    ctc_regions.push_back(w);
+    U8Region& r = u8w[w];
+    r.N = N;
+    r.K = K;
+    r.row_set.assign(N, 0);
+  }
+  bool ctc_int8_active() const {
+    if (!ctc_i8 || ctc_regions.empty()) return false;
+    for (const float* w : ctc_regions)
+      if (u8w.at(w).n_set < u8w.at(w).N) return false;
+    return true;
+  }
+  U8W U8(const float* W) const {
+    const U8Region& r = u8w.at(W);
+    U8W o;
+    o.q = r.q; o.cs = r.cs; o.bz = r.bz; o.ws = r.ws;
+    return o;
+  }
+  fa::U8Work make_u8work(int rows, int clips) {
+    int kmax = 0;
+    for (const float* w : ctc_regions) kmax = std::max(kmax, u8w.at(w).K);
+    fa::U8Work w;
+    w.xq_n = (int64_t)rows * kmax;
+    w.xq = alloc<int8_t>((size_t)w.xq_n);
+    w.rs = alloc<int>(rows);
+    w.part = alloc<float2>((size_t)clips * 64);
+    w.qp = alloc<float2>(clips);
+    w.max_clips = clips;
+    return w;
+  }
+  // one int8 linear of the CTC graph: DynamicQuantizeLinear of x (per clip over its lens[b] rows), MatMulInteger, rescale
+  void u8_lin(fa::U8Work& w, const float* x, int64_t ldx, const float* W, const float* b, float* C, int64_t ldc, int rows,
+              int ts, const int* lens, int N, int K, int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0) {
+    hipEvent_t ev;
+    prof_begin(1, &ev);
+    fa::dq_quantize(x, ldx, K, lens, ts, rows / ts, w, stream);
+    fa::gemm_u8_linear(w, U8(W), b, C, ldc, rows, N, K, ts, relu, add1, ld1, stream);
+    prof_end(1, 0, 2.0 * rows * N * K);
+  }
+  // CorrectTransformerAdaptor of the CTC graph with its linears in int8-dynamic form (the attention and LayerNorms stay
+  // f32, as in the quantized ONNX graph), then ctc_lo + row argmax -> ctc_ids
+  void run_ctc_int8(const float* in, int rows, int ts, const int* lens) {
+    const AdaptorW& a = ctc_dec;
+    const int d = ec.d_model, f = ec.ctc_ffn, d4 = d / 4;
+    if (!u8wk.xq) u8wk = make_u8work(R, max_batch);
+    fa::U8Work& w = u8wk;
+    u8_lin(w, in, d, a.l1_w, a.l1_b, ffn, f, rows, ts, lens, f, d, 1);
+    u8_lin(w, ffn, f, a.l2_w, a.l2_b, cbuf, d, rows, ts, lens, d, f);
+    for (const AdBlockW& b : a.blocks) {
+      layernorm(cbuf, d, hbuf, d, b.ln1_w, b.ln1_b, rows, d, 1e-12f, nullptr, ts, stream, 0);
+      u8_lin(w, hbuf, d, b.qkv_w, b.qkv_b, qkv, 3 * d, rows, ts, lens, 3 * d, d);
+      {
+        hipEvent_t ev;
+        prof_begin(2, &ev);
+        attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.ctc_heads, d / ec.ctc_heads,
+                 lens, enc_attn_wk, stream, 0, enc_gemm ? 1 : 0);
+        prof_end(2, 0, 4.0 * rows * (double)ts * d);
+      }
+      u8_lin(w, att, d, b.o_w, b.o_b, cbuf, d, rows, ts, lens, d, d, 0, cbuf, d);
+      layernorm(cbuf, d, hbuf, d, b.ln2_w, b.ln2_b, rows, d, 1e-12f, nullptr, ts, stream, 0);
+      u8_lin(w, hbuf, d, b.w1, b.b1, ffn, d4, rows, ts, lens, d4, d, 1);
+      u8_lin(w, ffn, d4, b.w2, b.b2, cbuf, d, rows, ts, lens, d, d4, 0, cbuf, d);
+    }
+    hipEvent_t ev;
+    prof_begin(1, &ev);
+    fa::dq_quantize(cbuf, d, d, lens, ts, rows / ts, w, stream);
+    fa::gemm_u8_ctc_argmax(w, U8(ctc_w), ctc_b, rows, ec.ctc_vocab, d, ts, ctc_pval, ctc_pidx, ctc_ids, stream);
+    prof_end(1, 0, 2.0 * rows * (double)ec.ctc_vocab * d);
+  }
   int bf3_attn() const { return !enc_fp16 && enc_gemm ? 1 : 0; }  // encoder attention products in the same mode
 
   EncBlockW sanm_block(const std::string& p, int d_in) {
@@ -462,6 +549,15 @@ struct Engine {
     lin("ctc_proj.ctc_lo", d, ec.ctc_vocab, cw, cb);
     ctc_w = cw;
     ctc_b = cb;
+    ctc_region(ctc_dec.l1_w, ec.ctc_ffn, d);
+    ctc_region(ctc_dec.l2_w, d, ec.ctc_ffn);
+    for (const AdBlockW& b : ctc_dec.blocks) {
+      ctc_region(b.qkv_w, 3 * d, d);
+      ctc_region(b.o_w, d, d);
+      ctc_region(b.w1, d / 4, d);
+      ctc_region(b.w2, d, d / 4);
+    }
+    ctc_region(ctc_w, ec.ctc_vocab, d);
   }
 
   Q8Mat q8mat(int64_t rows, int64_t cols) {
@@ -800,12 +896,14 @@ struct Engine {
     int *ctc_pidx, *ctc_ids;
     int64_t* d_nsamp;
     int *d_tmel, *d_tlfr, *d_tgt, *d_ctclen;
+    fa::U8Work u8;
   };
   struct EncLane {
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
     AttnF32Work attn;
     GemmF32Work gemm;
+    fa::U8Work u8;  // int8-dynamic CTC activations (allocated once the int8 graph is active)
   };
   std::vector<EncLane> enc_lanes;
   int encode_mode = 0;  // 0: padded batch; 1: independent clips in concurrent lanes
@@ -826,13 +924,13 @@ struct Engine {
 
   EncBind enc_bind() const {
     return EncBind{stream, enc_attn_wk, enc_gemm_wk, xp, mean_part, power, mel, xa, hbuf, qkv, att, mem, ffn, enc, ad, cbuf,
-                   ctc_pval, ctc_pidx, ctc_ids, d_nsamp, d_tmel, d_tlfr, d_tgt, d_ctclen};
+                   ctc_pval, ctc_pidx, ctc_ids, d_nsamp, d_tmel, d_tlfr, d_tgt, d_ctclen, u8wk};
   }
   void enc_rebind(const EncBind& b) {
     stream = b.stream; enc_attn_wk = b.attn; enc_gemm_wk = b.gemm; xp = b.xp; mean_part = b.mean_part; power = b.power;
     mel = b.mel; xa = b.xa; hbuf = b.hbuf; qkv = b.qkv; att = b.att; mem = b.mem; ffn = b.ffn; enc = b.enc; ad = b.ad;
     cbuf = b.cbuf; ctc_pval = b.ctc_pval; ctc_pidx = b.ctc_pidx; ctc_ids = b.ctc_ids; d_nsamp = b.d_nsamp;
-    d_tmel = b.d_tmel; d_tlfr = b.d_tlfr; d_tgt = b.d_tgt; d_ctclen = b.d_ctclen;
+    d_tmel = b.d_tmel; d_tlfr = b.d_tlfr; d_tgt = b.d_tgt; d_ctclen = b.d_ctclen; u8wk = b.u8;
   }
   EncLane& enc_lane(int i) {
     if ((int)enc_lanes.size() <= i) enc_lanes.resize(i + 1);
@@ -872,8 +970,9 @@ struct Engine {
         // record is rewritten at enqueue time)
         if (b >= kEncLanes) FA_HIP(hipEventSynchronize(l.done));
         FA_HIP(hipStreamWaitEvent(l.s, ev_fork, 0));
+        if (ctc_int8_active() && !l.u8.xq) l.u8 = make_u8work(tl_max, 1);
         EncBind lb = base;
-        lb.stream = l.s; lb.attn = l.attn; lb.gemm = l.gemm;
+        lb.stream = l.s; lb.attn = l.attn; lb.gemm = l.gemm; lb.u8 = l.u8;
         lb.xp += b * xp_stride_max; lb.mean_part += b * 64; lb.power += b * (size_t)tm_max * 204;
         lb.mel += b * (size_t)tm_max * ec.n_mels; lb.xa += b * T * wmax; lb.hbuf += b * T * wmax;
         lb.qkv += b * T * 3 * std::max(d, ec.d_llm); lb.att += b * T * std::max(d, ec.d_llm); lb.mem += b * T * d;
@@ -976,6 +1075,10 @@ struct Engine {
     // adaptor (key mask = valid frames) -> ad [rows][d_llm]
     run_adaptor(adaptor, enc, d, ec.d_llm, ec.adaptor_ffn, ec.adaptor_heads, ad, rows, ts, d_tlfr);
     // CTC head (reference: unmasked over the clip's own frames -> key length = ctc_len)
+    if (ctc_int8_active()) {
+      run_ctc_int8(enc, rows, ts, d_ctclen);
+      return;
+    }
     run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, rows, ts, d_ctclen);
     {
       hipEvent_t ev;
@@ -1000,9 +1103,13 @@ struct Engine {
     FA_HIP(hipMemcpyAsync(d_ctclen, hm32 + 3 * max_batch, 4, hipMemcpyHostToDevice, stream));
     FA_HIP(hipEventRecord(ev_meta[meta_slot], stream));
     FA_HIP(hipMemcpyAsync(enc, enc_host, (size_t)T * d * 4, hipMemcpyHostToDevice, stream));
-    run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, T, T, d_ctclen);
-    gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, T, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w),
-                    WB(ctc_w));
+    if (ctc_int8_active()) {
+      run_ctc_int8(enc, T, T, d_ctclen);
+    } else {
+      run_adaptor(ctc_dec, enc, d, d, ec.ctc_ffn, ec.ctc_heads, cbuf, T, T, d_ctclen);
+      gemm_ctc_argmax(cbuf, d, ctc_w, ctc_b, T, ec.ctc_vocab, d, ctc_pval, ctc_pidx, ctc_ids, stream, W16(ctc_w),
+                      WB(ctc_w));
+    }
     FA_HIP(hipMemcpyAsync(ids_out, ctc_ids, (size_t)T * 4, hipMemcpyDeviceToHost, stream));
     FA_HIP(hipStreamSynchronize(stream));
   }
@@ -1419,6 +1526,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     // gemm_f32_bench at M = 32032: 292-330 vs 243-276 TF/s f32-equivalent for the 128x128 tiles
     fa::g_gemm_bf3_256 = 192;
     if (const char* g = getenv("FUNASR_BF3_256")) fa::g_gemm_bf3_256 = std::max(0, atoi(g));
+    if (const char* g = getenv("FUNASR_F16_GEMM")) fa::g_gemm_f16_b3 = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
     // scripts/ubench/attn_batch at batch 32, 42.7 MB of K/V: 14.65 vs 15.7-15.9 us for the split blocks
     fa::g_attn_wide = 256;
@@ -1680,6 +1789,63 @@ int fa_set_encode_mode(fa_engine* h, int32_t mode) {
   FA_API_BEGIN
   FA_REQUIRE(mode == 0 || mode == 1, "encode mode must be 0 (padded batch) or 1 (independent clips)");
   h->e->encode_mode = mode;
+  FA_API_END
+}
+
+int fa_set_tensor_u8dq(fa_engine* h, const char* name, const uint8_t* q, const float* scale, const uint8_t* zero_point,
+                       int64_t rows, int64_t cols) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(q && scale && zero_point && rows > 0 && cols > 0, "fa_set_tensor_u8dq args");
+  fa::Slot& s = e->slot(name);
+  FA_REQUIRE(s.kind == 0 && rows * cols == s.n, std::string("fa_set_tensor_u8dq: not an f32 matrix of that size: ") + name);
+  const float* base = nullptr;
+  for (const float* w : e->ctc_regions) {
+    const Engine::U8Region& r = e->u8w.at(w);
+    if (s.f >= w && s.f < w + (int64_t)r.N * r.K) base = w;
+  }
+  FA_REQUIRE(base, std::string("fa_set_tensor_u8dq: not a CTC-graph linear weight: ") + name);
+  Engine::U8Region& r = e->u8w.at(base);
+  FA_REQUIRE(cols == r.K && (s.f - base) % r.K == 0, std::string("fa_set_tensor_u8dq: shape mismatch for ") + name);
+  const int64_t row0 = (s.f - base) / r.K;
+  if (!r.q) {
+    r.q = e->alloc<int8_t>((size_t)r.N * r.K);
+    r.cs = e->alloc<int>(r.N);
+    r.bz = e->alloc<int>(r.N);
+    r.ws = e->alloc<float>(r.N);
+  }
+  uint8_t* tq = nullptr;
+  float* ts = nullptr;
+  uint8_t* tz = nullptr;
+  FA_HIP(hipMalloc(&tq, rows * cols));
+  FA_HIP(hipMalloc(&ts, rows * 4));
+  FA_HIP(hipMalloc(&tz, rows));
+  FA_HIP(hipMemcpyAsync(tq, q, rows * cols, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(ts, scale, rows * 4, hipMemcpyHostToDevice, e->stream));
+  FA_HIP(hipMemcpyAsync(tz, zero_point, rows, hipMemcpyHostToDevice, e->stream));
+  fa::u8_weight_prep(tq, ts, tz, (int)rows, (int)cols, r.q + row0 * r.K, r.cs + row0, r.bz + row0, r.ws + row0, e->stream);
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_HIP(hipFree(tq));
+  FA_HIP(hipFree(ts));
+  FA_HIP(hipFree(tz));
+  for (int64_t i = row0; i < row0 + rows; ++i)
+    if (!r.row_set[i]) {
+      r.row_set[i] = 1;
+      ++r.n_set;
+    }
+  FA_API_END
+}
+
+int fa_set_ctc_int8(fa_engine* h, int32_t on) {
+  FA_API_BEGIN
+  h->e->ctc_i8 = on != 0;
+  FA_API_END
+}
+
+int fa_ctc_int8_active(fa_engine* h, int32_t* out) {
+  FA_API_BEGIN
+  FA_REQUIRE(out, "fa_ctc_int8_active: out");
+  *out = h->e->ctc_int8_active() ? 1 : 0;
   FA_API_END
 }
 

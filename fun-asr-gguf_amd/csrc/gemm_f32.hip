@@ -241,6 +241,7 @@ struct EpiArgmax128 {
   float* pval;   // [M][n_tiles]
   int* pidx;
   int n_tiles;
+  int r16 = 0;  // fp16 mode: argmax over fp16 logits (Gemm + bias output rounded to fp16)
   // the wave's 32x32 sub-tile goes through LDS (a per-wave [32][33] scratch after the [128][4] winners) so each row's
   // 32 columns are scanned in registers by a lane pair (16 each) instead of a 5-step shuffle butterfly per row:
   // the epilogue was as long as the K = 512 main loop (CTC GEMM 12.3 ms per 32 clips vs 7.3 ms for a linear
@@ -248,14 +249,14 @@ struct EpiArgmax128 {
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
     const int col = col0 + (lane & 31);
-    const float b = col < N ? bias[col] : 0.f;
+    const float b = col < N ? r16v(bias[col], r16) : 0.f;
     float* sv = lds;                              // [128 rows][4 slices]
     int* si = reinterpret_cast<int*>(lds + 512);  // [128][4]
     float* scr = lds + 1024 + wave * (32 * 33);   // [32 rows][33]
     const int slice = (col0 & 127) >> 5, rb = row0 & 127;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      scr[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = col < N ? acc[r] + b : -INFINITY;
+      scr[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = col < N ? r16v(acc[r] + b, r16) : -INFINITY;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -300,17 +301,18 @@ struct EpiArgmax256 {
   float* pval;   // [M][n_tiles]
   int* pidx;
   int n_tiles;
+  int r16 = 0;  // fp16 mode: argmax over fp16 logits (Gemm + bias output rounded to fp16)
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 7;
     const int col = col0 + (lane & 31);
-    const float b = col < N ? bias[col] : 0.f;
+    const float b = col < N ? r16v(bias[col], r16) : 0.f;
     float* sv = lds;                               // [256 rows][8 slices]
     int* si = reinterpret_cast<int*>(lds + 2048);  // [256][8]
     float* scr = lds + 4096 + wave * (32 * 33);    // [32 rows][33]
     const int slice = (col0 & 255) >> 5, rb = row0 & 255;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-      scr[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = col < N ? acc[r] + b : -INFINITY;
+      scr[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 33 + (lane & 31)] = col < N ? r16v(acc[r] + b, r16) : -INFINITY;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -645,24 +647,63 @@ int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ah
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
                            // 6 = 256x256x32
 int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
+int g_gemm_f16_b3 = 1;     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
 
-template <int WM, int WN, int KB>
+// P = 3: bf16x3 split operands (two bf16 planes per operand, three MFMAs per 16 of k); P = 1: the fp16 graph (C5):
+// one fp16 plane per operand (the activations are fp16 values, converted exactly while staged; W is the fp16 weight
+// copy), one v_mfma_f32_32x32x16_f16 per 16 of k, f16 x f16 products exact in the f32 accumulator.
+template <int P>
+struct PrecB;
+template <>
+struct PrecB<3> {
+  typedef __bf16 E;
+  typedef bf16x8 V8;
+  typedef bf16x4 V4;
+  static constexpr int NPL = 2;
+};
+template <>
+struct PrecB<1> {
+  typedef _Float16 E;
+  typedef f16x8 V8;
+  typedef f16x4 V4;
+  static constexpr int NPL = 1;
+};
+template <int P>
+__device__ __forceinline__ f32x16 mfma_pb(const typename PrecB<P>::V8& a, const typename PrecB<P>::V8& b, const f32x16& c) {
+  if constexpr (P == 3) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// one 16-deep k-step of a 32x32 accumulator: bf16x3 lo.hi, hi.lo, hi.hi (this order everywhere); fp16 the one product
+template <int P>
+__device__ __forceinline__ void mma_step(f32x16& acc, const typename PrecB<P>::V8& ah, const typename PrecB<P>::V8& al,
+                                         const typename PrecB<P>::V8& bh, const typename PrecB<P>::V8& bl) {
+  if constexpr (P == 3) {
+    acc = mfma_pb<3>(al, bh, acc);
+    acc = mfma_pb<3>(ah, bl, acc);
+  }
+  acc = mfma_pb<P>(ah, bh, acc);
+}
+
+template <int WM, int WN, int KB, int P = 3>
 struct TileB3 {
   static constexpr int BM = 64 * WM, BN = 64 * WN;
-  static constexpr int LDK = KB + 8;                    // bf16 per LDS row
-  static constexpr int R4 = KB / 4, R8 = KB / 8;        // float4 of A / 8-bf16 chunks of W per tile row
+  static constexpr int LDK = KB + 8;                    // bf16 / f16 per LDS row
+  static constexpr int R4 = KB / 4, R8 = KB / 8;        // float4 of A / 8-element chunks of W per tile row
   static constexpr int NA = BM * KB / 4 / 256;          // float4 of A per thread
-  static constexpr int NB = BN * KB / 8 / 256;          // 8-bf16 chunks of each W plane per thread
-  static constexpr int PA = BM * LDK, PB = BN * LDK;    // bf16 per plane
-  static constexpr int STAGE = 2 * (PA + PB);           // [Ah][Al][Bh][Bl]
+  static constexpr int NB = BN * KB / 8 / 256;          // 8-element chunks of each W plane per thread
+  static constexpr int PA = BM * LDK, PB = BN * LDK;    // elements per plane
+  static constexpr int NPL = PrecB<P>::NPL;
+  static constexpr int OB = NPL * PA;                   // W planes after the A planes
+  static constexpr int STAGE = NPL * (PA + PB);         // [Ah][Al][Bh][Bl] (P = 1: [Ah][Bh])
 };
 
-template <class AL, int WM, int WN, int KB>
-__device__ __forceinline__ void load_b3(const AL& al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                        int64_t ldw, int m0, int n0, int k0, int M, int N, int K,
-                                        float4 (&ra)[TileB3<WM, WN, KB>::NA], uint4 (&rh)[TileB3<WM, WN, KB>::NB],
-                                        uint4 (&rl)[TileB3<WM, WN, KB>::NB], int t) {
-  using T = TileB3<WM, WN, KB>;
+template <class AL, int WM, int WN, int KB, int P>
+__device__ __forceinline__ void load_b3(const AL& al, const typename PrecB<P>::E* __restrict__ Wh,
+                                        const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw, int m0, int n0, int k0,
+                                        int M, int N, int K, float4 (&ra)[TileB3<WM, WN, KB, P>::NA],
+                                        uint4 (&rh)[TileB3<WM, WN, KB, P>::NB], uint4 (&rl)[TileB3<WM, WN, KB, P>::NB],
+                                        int t) {
+  using T = TileB3<WM, WN, KB, P>;
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
@@ -675,32 +716,35 @@ __device__ __forceinline__ void load_b3(const AL& al, const __bf16* __restrict__
     const bool in = n < N && k < K;
     const int64_t o = (int64_t)n * ldw + k;
     rh[i] = in ? *reinterpret_cast<const uint4*>(Wh + o) : make_uint4(0, 0, 0, 0);
-    rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
+    if constexpr (P == 3) rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
   }
 }
 
-template <int WM, int WN, int KB>
-__device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<WM, WN, KB>::NA],
-                                         const uint4 (&rh)[TileB3<WM, WN, KB>::NB],
-                                         const uint4 (&rl)[TileB3<WM, WN, KB>::NB], int t) {
-  using T = TileB3<WM, WN, KB>;
+template <int WM, int WN, int KB, int P>
+__device__ __forceinline__ void store_b3(typename PrecB<P>::E* st, const float4 (&ra)[TileB3<WM, WN, KB, P>::NA],
+                                         const uint4 (&rh)[TileB3<WM, WN, KB, P>::NB],
+                                         const uint4 (&rl)[TileB3<WM, WN, KB, P>::NB], int t) {
+  using T = TileB3<WM, WN, KB, P>;
+  typedef typename PrecB<P>::E E;
+  typedef typename PrecB<P>::V4 V4;
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
     const float4 v = ra[i];
-    const bf16x4 h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    const bf16x4 l = {(__bf16)(v.x - (float)h[0]), (__bf16)(v.y - (float)h[1]), (__bf16)(v.z - (float)h[2]),
-                      (__bf16)(v.w - (float)h[3])};
+    const V4 h = {(E)v.x, (E)v.y, (E)v.z, (E)v.w};
     const int o = (idx / T::R4) * T::LDK + 4 * (idx % T::R4);
-    *reinterpret_cast<bf16x4*>(st + o) = h;
-    *reinterpret_cast<bf16x4*>(st + T::PA + o) = l;
+    *reinterpret_cast<V4*>(st + o) = h;
+    if constexpr (P == 3) {
+      const V4 l = {(E)(v.x - (float)h[0]), (E)(v.y - (float)h[1]), (E)(v.z - (float)h[2]), (E)(v.w - (float)h[3])};
+      *reinterpret_cast<V4*>(st + T::PA + o) = l;
+    }
   }
 #pragma unroll
   for (int i = 0; i < T::NB; ++i) {
     const int idx = t + i * 256;
     const int o = (idx / T::R8) * T::LDK + 8 * (idx % T::R8);
-    *reinterpret_cast<uint4*>(st + 2 * T::PA + o) = rh[i];
-    *reinterpret_cast<uint4*>(st + 2 * T::PA + T::PB + o) = rl[i];
+    *reinterpret_cast<uint4*>(st + T::OB + o) = rh[i];
+    if constexpr (P == 3) *reinterpret_cast<uint4*>(st + T::OB + T::PB + o) = rl[i];
   }
 }
 
@@ -710,17 +754,20 @@ __device__ __forceinline__ void store_b3(__bf16* st, const float4 (&ra)[TileB3<W
 // PF = 2: the global loads run two k-steps ahead (two register sets, the k loop unrolled by two), so a k-step's
 // tile has two steps of compute to land instead of one: few-tile shapes (one clip) have too little work per step to
 // cover the load latency.
-template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1>
-__global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                                       int64_t ldw, int M, int N, int K, EPI epi) {
-  using T = TileB3<WM, WN, KB>;
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1, int P = 3>
+__global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename PrecB<P>::E* __restrict__ Wh,
+                                                       const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw, int M,
+                                                       int N, int K, EPI epi) {
+  using T = TileB3<WM, WN, KB, P>;
+  typedef typename PrecB<P>::E E;
+  typedef typename PrecB<P>::V8 V8;
   constexpr int LDK = T::LDK;
   extern __shared__ float smem[];  // KW x 2 stages; the epilogue reuses it
   int tm, tn;
   if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
   const int m0 = tm * T::BM, n0 = tn * T::BN;
   const int grp = KW > 1 ? (int)(threadIdx.x >> 8) : 0, t = threadIdx.x & 255;
-  __bf16* sh = reinterpret_cast<__bf16*>(smem) + grp * 2 * T::STAGE;
+  E* sh = reinterpret_cast<E*>(smem) + grp * 2 * T::STAGE;
   const int wave = t >> 6, lane = t & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int r = lane & 31, h = lane >> 5;
@@ -732,42 +779,39 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
   float4 ra[T::NA];
   uint4 rh[T::NB], rl[T::NB];
   const int kq = K / KW, kb0 = grp * kq, ke = kb0 + kq;  // host: K % (KW * KB) == 0 when KW > 1
-  load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0, M, N, ke, ra, rh, rl, t);
-  store_b3<WM, WN, KB>(sh, ra, rh, rl, t);
+  load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0, M, N, ke, ra, rh, rl, t);
+  store_b3<WM, WN, KB, P>(sh, ra, rh, rl, t);
   __syncthreads();
   const int nk = (kq + KB - 1) / KB;
-  auto compute = [&](const __bf16* stage) {
-    const __bf16* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
-    const __bf16* b = stage + 2 * T::PA + (wc * 32 * WN + r) * LDK + 8 * h;
+  auto compute = [&](const E* stage) {
+    const E* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
+    const E* b = stage + T::OB + (wc * 32 * WN + r) * LDK + 8 * h;
 #pragma unroll
     for (int kk = 0; kk < KB / 16; ++kk) {
-      bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+      V8 ah[WM], alo[WM], bh[WN], blo[WN];
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
-        ah[i] = *reinterpret_cast<const bf16x8*>(a + 32 * i * LDK + 16 * kk);
-        alo[i] = *reinterpret_cast<const bf16x8*>(a + T::PA + 32 * i * LDK + 16 * kk);
+        ah[i] = *reinterpret_cast<const V8*>(a + 32 * i * LDK + 16 * kk);
+        if constexpr (P == 3) alo[i] = *reinterpret_cast<const V8*>(a + T::PA + 32 * i * LDK + 16 * kk);
       }
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(b + 32 * j * LDK + 16 * kk);
-        blo[j] = *reinterpret_cast<const bf16x8*>(b + T::PB + 32 * j * LDK + 16 * kk);
+        bh[j] = *reinterpret_cast<const V8*>(b + 32 * j * LDK + 16 * kk);
+        if constexpr (P == 3) blo[j] = *reinterpret_cast<const V8*>(b + T::PB + 32 * j * LDK + 16 * kk);
       }
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int j = 0; j < WN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], blo[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < WN; ++j) mma_step<P>(acc[i][j], ah[i], alo[i], bh[j], blo[j]);
     }
   };
   if constexpr (PF == 1) {
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
+      if (kt + 1 < nk)
+        load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
       compute(sh + cur * T::STAGE);
-      if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
       __syncthreads();
     }
   } else {
@@ -775,17 +819,19 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
     // step j - 2's set was stored, i.e. two compute steps before it is stored itself
     float4 rb[T::NA];
     uint4 rhb[T::NB], rlb[T::NB];
-    if (nk > 1) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rh, rl, t);
-    if (nk > 2) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + 2 * KB, M, N, ke, rb, rhb, rlb, t);
+    if (nk > 1) load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rh, rl, t);
+    if (nk > 2) load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + 2 * KB, M, N, ke, rb, rhb, rlb, t);
     for (int kt = 0; kt < nk; kt += 2) {
       compute(sh);  // step kt (stage 0)
-      if (kt + 1 < nk) store_b3<WM, WN, KB>(sh + T::STAGE, ra, rh, rl, t);
-      if (kt + 3 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 3) * KB, M, N, ke, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + T::STAGE, ra, rh, rl, t);
+      if (kt + 3 < nk)
+        load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 3) * KB, M, N, ke, ra, rh, rl, t);
       __syncthreads();
       if (kt + 1 >= nk) break;
       compute(sh + T::STAGE);  // step kt + 1 (stage 1)
-      if (kt + 2 < nk) store_b3<WM, WN, KB>(sh, rb, rhb, rlb, t);
-      if (kt + 4 < nk) load_b3<AL, WM, WN, KB>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 4) * KB, M, N, ke, rb, rhb, rlb, t);
+      if (kt + 2 < nk) store_b3<WM, WN, KB, P>(sh, rb, rhb, rlb, t);
+      if (kt + 4 < nk)
+        load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 4) * KB, M, N, ke, rb, rhb, rlb, t);
       __syncthreads();
     }
   }
@@ -820,45 +866,55 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const __bf16* __re
 // No K splits: the bf16x3 body is fast enough that the split-K seam (publish + ticket + combine, 5-13 us:
 // MI355X_MICROARCH.md splitk-seam) costs more than it saves (one clip, measured: out N 512 K 512 10.8 -> 19.8 us,
 // ffn2 N 512 K 2048 32.6 -> 57 us with 2-4 splits).
-template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1>
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1, int P = 3>
 static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                            hipStream_t s) {
-  using T = TileB3<WM, WN, KB>;
+  using T = TileB3<WM, WN, KB, P>;
+  typedef typename PrecB<P>::E E;
   FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3: K and ldw must be multiples of 8");
   FA_REQUIRE(KW == 1 || K % (KW * KB) == 0, "gemm_bf3: K groups need K % (KW * KB) == 0");
   const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM));
-  const size_t lds = std::max<size_t>(KW * 2 * T::STAGE * 2, 1024);  // >= EpiArgmax scratch
+  // >= EpiArgmax / EpiArgmax128 scratch, >= the KW = 2 accumulator hand-off
+  const size_t lds = std::max<size_t>({(size_t)KW * 2 * T::STAGE * 2, (size_t)(1024 + 4 * 32 * 33) * 4,
+                                       KW > 1 ? (size_t)4 * WM * WN * 16 * 64 * 4 : 0});
   static bool attr = false;
   if (!attr && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF, P>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF>), grid, dim3(256 * KW), lds, s, al,
-                     reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF, P>), grid, dim3(256 * KW), lds, s, al,
+                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
 }
 
-// 256x256x32 bf16x3 tile (batched encoder, C3): 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 accumulators of
-// 32x32, 512 threads, one block per CU. Per 16 of k a wave reads 12 fragments (4 + 2 tiles, two planes) for 24 MFMAs
-// (the 128x128 tile: 8 for 12), and a k-step has 48 MFMAs per wave between barriers. Same stage layout, operand maps,
-// per-element MFMA order (lo.hi, hi.lo, hi.hi per 16 of k, k ascending) and epilogue calls as k_gemm_bf3: every output
-// is bit-identical to the 128x128 and 64x64 tiles. LDS: two stages of 4 planes x 256 rows x 80 B = 160 KiB.
+// 256x256x32 tile (batched encoder, C3; P = 3 bf16x3, P = 1 the fp16 graph): 8 waves as 2 (M) x 4 (N), each wave
+// 128 x 64 = 4 x 2 accumulators of 32x32, 512 threads, one block per CU. Per 16 of k a bf16x3 wave reads 12 fragments
+// (4 + 2 tiles, two planes) for 24 MFMAs (the 128x128 tile: 8 for 12), and a k-step has 48 MFMAs per wave between
+// barriers. Same stage layout, operand maps, per-element MFMA order (lo.hi, hi.lo, hi.hi per 16 of k, k ascending) and
+// epilogue calls as k_gemm_bf3: every output is bit-identical to the 128x128 and 64x64 tiles. LDS: two stages of 4
+// planes x 256 rows x 80 B = 160 KiB (fp16: 2 planes, 80 KiB).
 #ifndef B3B_VARIANT
 // A/B only (scripts/gpu_r3_g256b.sh, M = 32032): 1 = MFMA blocks at raised wave priority (275-325 TF/s), 2 = also the
 // next stage stored between the k halves (193-229 TF/s); 0 (292-330 TF/s) stays
 #define B3B_VARIANT 0
 #endif
 constexpr int B3B_T = 512, B3B_BM = 256, B3B_BN = 256, B3B_KB = 32, B3B_LDK = B3B_KB + 8;
-constexpr int B3B_PA = B3B_BM * B3B_LDK, B3B_PB = B3B_BN * B3B_LDK;  // bf16 per plane
-constexpr int B3B_STAGE = 2 * (B3B_PA + B3B_PB);                     // [Ah][Al][Bh][Bl]
+constexpr int B3B_PA = B3B_BM * B3B_LDK, B3B_PB = B3B_BN * B3B_LDK;  // elements per plane
 constexpr int B3B_NA = B3B_BM * B3B_KB / 4 / B3B_T;                  // float4 of A per thread (4)
-constexpr int B3B_NB = B3B_BN * B3B_KB / 8 / B3B_T;                  // 8-bf16 chunks of each W plane per thread (2)
-constexpr size_t B3B_LDS = 2 * B3B_STAGE * 2;                        // bytes
+constexpr int B3B_NB = B3B_BN * B3B_KB / 8 / B3B_T;                  // 8-element chunks of each W plane per thread (2)
+template <int P>
+struct B3BT {
+  static constexpr int NPL = PrecB<P>::NPL;
+  static constexpr int OB = NPL * B3B_PA;                            // W planes after the A planes
+  static constexpr int STAGE = NPL * (B3B_PA + B3B_PB);              // [Ah][Al][Bh][Bl] (P = 1: [Ah][Bh])
+  static constexpr size_t LDS = std::max<size_t>(2 * STAGE * 2, (4096 + 8 * 32 * 33) * 4);  // >= EpiArgmax256
+};
 
-template <class AL>
-__device__ __forceinline__ void load_b3b(const AL& al, const __bf16* __restrict__ Wh, const __bf16* __restrict__ Wl,
-                                         int64_t ldw, int m0, int n0, int k0, int M, int N, int K,
-                                         float4 (&ra)[B3B_NA], uint4 (&rh)[B3B_NB], uint4 (&rl)[B3B_NB], int t) {
+template <class AL, int P>
+__device__ __forceinline__ void load_b3b(const AL& al, const typename PrecB<P>::E* __restrict__ Wh,
+                                         const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw, int m0, int n0, int k0,
+                                         int M, int N, int K, float4 (&ra)[B3B_NA], uint4 (&rh)[B3B_NB],
+                                         uint4 (&rl)[B3B_NB], int t) {
   constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
 #pragma unroll
   for (int i = 0; i < B3B_NA; ++i) {
@@ -872,38 +928,45 @@ __device__ __forceinline__ void load_b3b(const AL& al, const __bf16* __restrict_
     const bool in = n < N && k < K;
     const int64_t o = (int64_t)n * ldw + k;
     rh[i] = in ? *reinterpret_cast<const uint4*>(Wh + o) : make_uint4(0, 0, 0, 0);
-    rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
+    if constexpr (P == 3) rl[i] = in ? *reinterpret_cast<const uint4*>(Wl + o) : make_uint4(0, 0, 0, 0);
   }
 }
 
-__device__ __forceinline__ void store_b3b(__bf16* st, const float4 (&ra)[B3B_NA], const uint4 (&rh)[B3B_NB],
+template <int P>
+__device__ __forceinline__ void store_b3b(typename PrecB<P>::E* st, const float4 (&ra)[B3B_NA], const uint4 (&rh)[B3B_NB],
                                           const uint4 (&rl)[B3B_NB], int t) {
   constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
+  typedef typename PrecB<P>::E E;
+  typedef typename PrecB<P>::V4 V4;
 #pragma unroll
   for (int i = 0; i < B3B_NA; ++i) {
     const int idx = t + i * B3B_T;
     const float4 v = ra[i];
-    const bf16x4 h = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    const bf16x4 l = {(__bf16)(v.x - (float)h[0]), (__bf16)(v.y - (float)h[1]), (__bf16)(v.z - (float)h[2]),
-                      (__bf16)(v.w - (float)h[3])};
+    const V4 h = {(E)v.x, (E)v.y, (E)v.z, (E)v.w};
     const int o = (idx / R4) * B3B_LDK + 4 * (idx % R4);
-    *reinterpret_cast<bf16x4*>(st + o) = h;
-    *reinterpret_cast<bf16x4*>(st + B3B_PA + o) = l;
+    *reinterpret_cast<V4*>(st + o) = h;
+    if constexpr (P == 3) {
+      const V4 l = {(E)(v.x - (float)h[0]), (E)(v.y - (float)h[1]), (E)(v.z - (float)h[2]), (E)(v.w - (float)h[3])};
+      *reinterpret_cast<V4*>(st + B3B_PA + o) = l;
+    }
   }
 #pragma unroll
   for (int i = 0; i < B3B_NB; ++i) {
     const int idx = t + i * B3B_T;
     const int o = (idx / R8) * B3B_LDK + 8 * (idx % R8);
-    *reinterpret_cast<uint4*>(st + 2 * B3B_PA + o) = rh[i];
-    *reinterpret_cast<uint4*>(st + 2 * B3B_PA + B3B_PB + o) = rl[i];
+    *reinterpret_cast<uint4*>(st + B3BT<P>::OB + o) = rh[i];
+    if constexpr (P == 3) *reinterpret_cast<uint4*>(st + B3BT<P>::OB + B3B_PB + o) = rl[i];
   }
 }
 
-template <class AL, class EPI>
-__global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* __restrict__ Wh,
-                                                            const __bf16* __restrict__ Wl, int64_t ldw, int M, int N,
-                                                            int K, EPI epi) {
+template <class AL, class EPI, int P = 3>
+__global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename PrecB<P>::E* __restrict__ Wh,
+                                                            const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw,
+                                                            int M, int N, int K, EPI epi) {
   constexpr int WM = 4, WN = 2, LDK = B3B_LDK;
+  constexpr int STAGE = B3BT<P>::STAGE, OB = B3BT<P>::OB;
+  typedef typename PrecB<P>::E E;
+  typedef typename PrecB<P>::V8 V8;
   extern __shared__ float smem[];  // 2 stages; the epilogue reuses it
   int tm, tn;
   if (!xcd_tile((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, tm, tn)) return;
@@ -911,7 +974,7 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* 
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int wr = wave >> 2, wc = wave & 3;
   const int r = lane & 31, h = lane >> 5;
-  __bf16* sh = reinterpret_cast<__bf16*>(smem);
+  E* sh = reinterpret_cast<E*>(smem);
   f32x16 acc[WM][WN];
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -919,31 +982,31 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* 
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
   float4 ra[B3B_NA];
   uint4 rh[B3B_NB], rl[B3B_NB];
-  load_b3b(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl, t);
-  store_b3b(sh, ra, rh, rl, t);
+  load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl, t);
+  store_b3b<P>(sh, ra, rh, rl, t);
   __syncthreads();
   const int nk = (K + B3B_KB - 1) / B3B_KB;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_b3b(al, Wh, Wl, ldw, m0, n0, (kt + 1) * B3B_KB, M, N, K, ra, rh, rl, t);
-    const __bf16* stage = sh + cur * B3B_STAGE;
-    const __bf16* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
-    const __bf16* b = stage + 2 * B3B_PA + (wc * 32 * WN + r) * LDK + 8 * h;
+    if (kt + 1 < nk) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, (kt + 1) * B3B_KB, M, N, K, ra, rh, rl, t);
+    const E* stage = sh + cur * STAGE;
+    const E* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
+    const E* b = stage + OB + (wc * 32 * WN + r) * LDK + 8 * h;
 #pragma unroll
     for (int kk = 0; kk < B3B_KB / 16; ++kk) {
 #if B3B_VARIANT == 2
-      if (kk == 1 && kt + 1 < nk) store_b3b(sh + (cur ^ 1) * B3B_STAGE, ra, rh, rl, t);
+      if (kk == 1 && kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
 #endif
-      bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+      V8 ah[WM], alo[WM], bh[WN], blo[WN];
 #pragma unroll
       for (int j = 0; j < WN; ++j) {
-        bh[j] = *reinterpret_cast<const bf16x8*>(b + 32 * j * LDK + 16 * kk);
-        blo[j] = *reinterpret_cast<const bf16x8*>(b + B3B_PB + 32 * j * LDK + 16 * kk);
+        bh[j] = *reinterpret_cast<const V8*>(b + 32 * j * LDK + 16 * kk);
+        if constexpr (P == 3) blo[j] = *reinterpret_cast<const V8*>(b + B3B_PB + 32 * j * LDK + 16 * kk);
       }
 #pragma unroll
       for (int i = 0; i < WM; ++i) {
-        ah[i] = *reinterpret_cast<const bf16x8*>(a + 32 * i * LDK + 16 * kk);
-        alo[i] = *reinterpret_cast<const bf16x8*>(a + B3B_PA + 32 * i * LDK + 16 * kk);
+        ah[i] = *reinterpret_cast<const V8*>(a + 32 * i * LDK + 16 * kk);
+        if constexpr (P == 3) alo[i] = *reinterpret_cast<const V8*>(a + B3B_PA + 32 * i * LDK + 16 * kk);
       }
 #if B3B_VARIANT >= 1
       __builtin_amdgcn_s_setprio(1);
@@ -951,17 +1014,13 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* 
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int j = 0; j < WN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], blo[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < WN; ++j) mma_step<P>(acc[i][j], ah[i], alo[i], bh[j], blo[j]);
 #if B3B_VARIANT >= 1
       __builtin_amdgcn_s_setprio(0);
 #endif
     }
 #if B3B_VARIANT != 2
-    if (kt + 1 < nk) store_b3b(sh + (cur ^ 1) * B3B_STAGE, ra, rh, rl, t);
+    if (kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
 #endif
     __syncthreads();
   }
@@ -972,19 +1031,20 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const __bf16* 
   epi.finish(m0, n0, M, N, smem);
 }
 
-template <class AL, class EPI>
+template <class AL, class EPI, int P = 3>
 static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                                hipStream_t s) {
+  typedef typename PrecB<P>::E E;
   FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3_256: K and ldw must be multiples of 8");
   static bool attr = false;
   if (!attr) {
-    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)B3B_LDS));
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI, P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)B3BT<P>::LDS));
     attr = true;
   }
   const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
-  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI>), grid, dim3(B3B_T), B3B_LDS, s, al,
-                     reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P>), grid, dim3(B3B_T), B3BT<P>::LDS, s, al,
+                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
 }
 
 // microbenchmark helper: resident blocks per CU of the 128x128x32 bf16x3 kernel (linear epilogue), its dynamic LDS
@@ -998,7 +1058,8 @@ int gemm_bf3_occupancy_128() {
   return n;
 }
 
-template <class AL, class EPI>
+// P = 3: bf16x3 planes (w.hi, w.lo); P = 1: the fp16 graph (w.hi = the fp16 weight copy)
+template <class AL, class EPI, int P = 3>
 static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
   const int f = g_gemm_bf3_force;
   const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
@@ -1006,15 +1067,15 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   const bool pf = g_gemm_bf3_pf > 1;
   // 256x256 tiles while they still give most CUs a block (f == 6 forces them)
   if (f == 6 || (f == 0 && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256))
-    launch_gemm_b3_256(al, w, ldw, M, N, K, epi, s);
-  else if (big) launch_gemm_b3<AL, EPI, 2, 2, 32>(al, w, ldw, M, N, K, epi, s);
-  else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32>(al, w, ldw, M, N, K, epi, s);
+    launch_gemm_b3_256<AL, EPI, P>(al, w, ldw, M, N, K, epi, s);
+  else if (big) launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
   else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
-    if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2>(al, w, ldw, M, N, K, epi, s);
-    else launch_gemm_b3<AL, EPI, 1, 1, 64, 2>(al, w, ldw, M, N, K, epi, s);
-  } else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2>(al, w, ldw, M, N, K, epi, s);
-  else if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 2>(al, w, ldw, M, N, K, epi, s);
-  else launch_gemm_b3<AL, EPI, 1, 1, 64>(al, w, ldw, M, N, K, epi, s);
+    if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
+    else launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 1, P>(al, w, ldw, M, N, K, epi, s);
+  } else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2, 1, P>(al, w, ldw, M, N, K, epi, s);
+  else if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
+  else launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
 }
 
 __global__ void k_split_bf16(const float* __restrict__ w, __bf16* __restrict__ hi, __bf16* __restrict__ lo, int64_t n) {
@@ -1038,7 +1099,8 @@ void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const
                  hipStream_t s, const __half* W16, const GemmF32Work* wk, WSplit wb) {
   ALoadPlain al{A, lda};
   EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
-  if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
+  if (W16 && g_gemm_f16_b3) run_gemm_b3<ALoadPlain, EpiLinear, 1>(al, WSplit{reinterpret_cast<const uint16_t*>(W16)}, ldw, M, N, K, epi, s);
+  else if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
   else if (wb.hi) run_gemm_b3(al, wb, ldw, M, N, K, epi, s);
   else run_gemm(al, W, ldw, M, N, K, epi, s, true, wk);
 }
@@ -1074,11 +1136,277 @@ __global__ void k_argmax_final(const float* __restrict__ pval, const int* __rest
   if (lane == 0) out[row] = i;
 }
 
+// ---------------------------------------------------------------------------------------------
+// int8-dynamic CTC graph (the reference's default Fun-ASR-Nano-CTC.int8.onnx: 02-Quantize-ONNX.py:38-46, onnxruntime
+// quantize_dynamic over every MatMul with a constant weight, per-channel QUInt8 weights, reduce_range off). At run time
+// each such MatMul is DynamicQuantizeLinear(x) -> MatMulInteger -> Cast -> Mul(x_scale * w_scale) (ONNX operator
+// semantics; the attention's activation x activation MatMuls stay f32):
+//   x_min = min(0, min x), x_max = max(0, max x) over the whole [1, T, K] input tensor (one clip's unpadded rows),
+//   xs = (x_max - x_min) / 255, xzp = round_half_even(clamp(-x_min / xs, 0, 255)), xq = sat(round_half_even(x / xs) + xzp)
+//   y[i][j] = f32(sum_k (xq[i][k] - xzp) (wq[j][k] - wzp[j])) * f32(xs * ws[j]) (+ bias, the Add that follows)
+// The integer dot runs on v_mfma_i32_32x32x32_i8 with both operands shifted into int8 (x' = xq - 128, w' = wq - 128):
+//   sum (xq - xzp)(wq - wzp) = S' + bz_j rs_i + a cs_j + K a bz_j,  S' = sum x' w', rs_i = sum_k x'[i][k],
+//   cs_j = sum_k w'[j][k], a = 128 - xzp, bz_j = 128 - wzp[j]   (exact in int32 for K <= 2^15)
+// -> the same integers as MatMulInteger, then the f32 rescale, bias and the existing epilogues (ReLU / residual /
+// fused CTC row-argmax).
+typedef int i32x4_u __attribute__((ext_vector_type(4)));
+typedef int i32x16_u __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float rne_f(float v) { return __builtin_rintf(v); }  // round half to even
+
+// weight prep: ORT uint8 [N][K] + scale / zero point per output channel -> w' = wq - 128 (int8), cs_j, bz_j
+__global__ void k_u8w_prep(const uint8_t* __restrict__ q, const float* __restrict__ sc, const uint8_t* __restrict__ zp,
+                           int N, int K, int8_t* __restrict__ wq, int* __restrict__ cs, int* __restrict__ bz,
+                           float* __restrict__ ws) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  if (j >= N) return;
+  int sum = 0;
+  for (int k = lane; k < K; k += 64) {
+    const int v = (int)q[(int64_t)j * K + k] - 128;
+    wq[(int64_t)j * K + k] = (int8_t)v;
+    sum += v;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) {
+    cs[j] = sum;
+    bz[j] = 128 - (int)zp[j];
+    ws[j] = sc[j];
+  }
+}
+
+void u8_weight_prep(const uint8_t* q, const float* scale, const uint8_t* zp, int N, int K, int8_t* wq, int* cs, int* bz,
+                    float* ws, hipStream_t s) {
+  hipLaunchKernelGGL(k_u8w_prep, dim3(N), dim3(64), 0, s, q, scale, zp, N, K, wq, cs, bz, ws);
+}
+
+// per-clip min / max partials of x over the clip's valid rows [0, lens[b]) (row base b * ts): grid (DQ_NB, B)
+constexpr int DQ_NB = 64;
+__global__ __launch_bounds__(256) void k_dq_minmax(const float* __restrict__ x, int64_t ldx, int K,
+                                                   const int* __restrict__ lens, int ts, float2* __restrict__ part) {
+  const int b = blockIdx.y, len = lens ? lens[b] : ts;
+  const int64_t n = (int64_t)len * K;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)DQ_NB * 256) {
+    const int64_t r = i / K, c = i - r * K;
+    const float v = x[((int64_t)b * ts + r) * ldx + c];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  __shared__ float smn[4], smx[4];
+  mn = -wave_max(-mn);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) {
+    smn[threadIdx.x >> 6] = mn;
+    smx[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[b * DQ_NB + blockIdx.x] = make_float2(fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3])),
+                                               fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3])));
+}
+
+// DynamicQuantizeLinear of the clip's rows: one wave per row (grid (cdiv(ts, 4), B)); rows past lens[b] -> zeros.
+// xq [rows][K] int8 (xq - 128), rs [rows] = row sums of the int8 values, qp[b] = {xs, a = 128 - xzp}
+__global__ __launch_bounds__(256) void k_dq_quant(const float* __restrict__ x, int64_t ldx, int K,
+                                                  const int* __restrict__ lens, int ts, const float2* __restrict__ part,
+                                                  int8_t* __restrict__ xq, int* __restrict__ rs, float2* __restrict__ qp) {
+  const int b = blockIdx.y, len = lens ? lens[b] : ts;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wave;
+  float mn = part[b * DQ_NB + lane].x, mx = part[b * DQ_NB + lane].y;  // DQ_NB == 64: one partial per lane
+  mn = -wave_max(-mn);
+  mx = wave_max(mx);
+  mn = fminf(mn, 0.f);
+  mx = fmaxf(mx, 0.f);
+  const float xs = mx == mn ? 1.0f : (mx - mn) / 255.0f;
+  const float zpf = rne_f(fminf(fmaxf(0.0f - mn / xs, 0.0f), 255.0f));
+  if (blockIdx.x == 0 && threadIdx.x == 0) qp[b] = make_float2(xs, 128.0f - zpf);
+  if (r >= ts) return;
+  const int64_t row = (int64_t)b * ts + r;
+  int sum = 0;
+  for (int k = 4 * lane; k < K; k += 256) {
+    char4 o = make_char4(0, 0, 0, 0);
+    if (r < len) {
+      const float4 v = *reinterpret_cast<const float4*>(x + row * ldx + k);
+      const int q0 = (int)fminf(fmaxf(rne_f(v.x / xs) + zpf, 0.f), 255.f) - 128;
+      const int q1 = (int)fminf(fmaxf(rne_f(v.y / xs) + zpf, 0.f), 255.f) - 128;
+      const int q2 = (int)fminf(fmaxf(rne_f(v.z / xs) + zpf, 0.f), 255.f) - 128;
+      const int q3 = (int)fminf(fmaxf(rne_f(v.w / xs) + zpf, 0.f), 255.f) - 128;
+      o = make_char4((char)q0, (char)q1, (char)q2, (char)q3);
+      sum += q0 + q1 + q2 + q3;
+    }
+    *reinterpret_cast<char4*>(xq + row * K + k) = o;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) rs[row] = sum;
+}
+
+// integer GEMM tile: 64 WM x 64 WN x 64 (k), 2x2 waves each WM x WN accumulators of 32x32 (v_mfma_i32_32x32x32_i8:
+// lane (r, h) holds row r, k 16 h .. 16 h + 15 of A and of B; accumulator reg -> row (reg & 3) + 8 (reg >> 2) + 4 h,
+// col r: the f32 kernels' layout, so their epilogues apply). LDS rows of 64 + 16 B: the 16 rows a 16-lane group
+// reads start in distinct 4-bank groups. xcd_tile order, no K splits.
+constexpr int U8_LD = 80;
+template <int WM, int WN>
+struct TileU8 {
+  static constexpr int BM = 64 * WM, BN = 64 * WN;
+  static constexpr int NA = BM * 4 / 256, NB = BN * 4 / 256;  // 16-B chunks per thread
+  static constexpr int STAGE = (BM + BN) * U8_LD;              // bytes
+};
+struct U8Args {
+  const int8_t* xq;
+  const int* rs;
+  const float2* qp;
+  const int8_t* wq;
+  const int* cs;
+  const int* bz;
+  const float* ws;
+  int ts;  // rows per clip (row -> clip = row / ts)
+};
+
+template <class EPI, int WM, int WN>
+__global__ __launch_bounds__(256) void k_gemm_u8(U8Args u, int M, int N, int K, EPI epi) {
+  using T = TileU8<WM, WN>;
+  extern __shared__ float smem[];
+  uint8_t* sm = reinterpret_cast<uint8_t*>(smem);
+  int tm, tn;
+  if (!xcd_tile((N + T::BN - 1) / T::BN, (M + T::BM - 1) / T::BM, tm, tn)) return;
+  const int m0 = tm * T::BM, n0 = tn * T::BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  i32x16_u acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = i32x16_u{};
+  i32x4_u ra[T::NA], rb[T::NB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < T::NA; ++i) {
+      const int idx = t + 256 * i, row = idx >> 2, c = idx & 3;
+      ra[i] = *reinterpret_cast<const i32x4_u*>(u.xq + (int64_t)min(m0 + row, M - 1) * K + k0 + 16 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < T::NB; ++i) {
+      const int idx = t + 256 * i, row = idx >> 2, c = idx & 3;
+      rb[i] = *reinterpret_cast<const i32x4_u*>(u.wq + (int64_t)min(n0 + row, N - 1) * K + k0 + 16 * c);
+    }
+  };
+  auto store = [&](uint8_t* st) {
+#pragma unroll
+    for (int i = 0; i < T::NA; ++i) {
+      const int idx = t + 256 * i;
+      *reinterpret_cast<i32x4_u*>(st + (idx >> 2) * U8_LD + 16 * (idx & 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < T::NB; ++i) {
+      const int idx = t + 256 * i;
+      *reinterpret_cast<i32x4_u*>(st + (T::BM + (idx >> 2)) * U8_LD + 16 * (idx & 3)) = rb[i];
+    }
+  };
+  const int nk = K / 64;  // host: K % 64 == 0
+  load(0);
+  store(sm);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load((kt + 1) * 64);
+    const uint8_t* st = sm + cur * T::STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      i32x4_u av[WM], bv[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+        av[i] = *reinterpret_cast<const i32x4_u*>(st + (wr * 32 * WM + 32 * i + r) * U8_LD + 32 * kk + 16 * h);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        bv[j] = *reinterpret_cast<const i32x4_u*>(st + (T::BM + wc * 32 * WN + 32 * j + r) * U8_LD + 32 * kk + 16 * h);
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(sm + (cur ^ 1) * T::STAGE);
+    __syncthreads();
+  }
+  // MatMulInteger's integers -> f32 rescale (Cast, Mul by f32(xs * ws_j)), then the epilogue (bias, ReLU, residual,
+  // argmax) on the f32 accumulator layout
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int row0 = m0 + (wr * WM + i) * 32, col0 = n0 + (wc * WN + j) * 32;
+      const int col = min(col0 + r, N - 1);
+      const int cs = u.cs[col], bzj = u.bz[col];
+      const float wsj = u.ws[col];
+      f32x16 y;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = min(row0 + (q & 3) + 8 * (q >> 2) + 4 * h, M - 1);
+        const float2 p = u.qp[row / u.ts];
+        const int a = (int)p.y;
+        const int tot = acc[i][j][q] + bzj * u.rs[row] + a * cs + K * a * bzj;
+        y[q] = __fmul_rn((float)tot, __fmul_rn(p.x, wsj));
+      }
+      epi.apply(y, row0, col0, M, N, smem);
+    }
+  epi.finish(m0, n0, M, N, smem);
+}
+
+template <class EPI, int WM, int WN>
+static void launch_gemm_u8(const U8Args& u, int M, int N, int K, const EPI& epi, hipStream_t s) {
+  using T = TileU8<WM, WN>;
+  FA_REQUIRE(K % 64 == 0, "gemm_u8: K must be a multiple of 64");
+  const size_t lds = std::max<size_t>({(size_t)2 * T::STAGE, (size_t)(1024 + 4 * 32 * 33) * 4});
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_u8<EPI, WM, WN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_u8<EPI, WM, WN>), xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM)), dim3(256), lds, s, u, M, N, K,
+                     epi);
+}
+
+// DynamicQuantizeLinear of x (B clips of ts rows, lens[b] valid) into the workspace
+void dq_quantize(const float* x, int64_t ldx, int K, const int* lens, int ts, int B, U8Work& w, hipStream_t s) {
+  FA_REQUIRE(K % 4 == 0 && (int64_t)B * ts * K <= w.xq_n && B <= w.max_clips, "dq_quantize: workspace");
+  hipLaunchKernelGGL(k_dq_minmax, dim3(DQ_NB, B), dim3(256), 0, s, x, ldx, K, lens, ts, w.part);
+  hipLaunchKernelGGL(k_dq_quant, dim3(cdiv(ts, 4), B), dim3(256), 0, s, x, ldx, K, lens, ts, w.part, w.xq, w.rs, w.qp);
+}
+
+void gemm_u8_linear(const U8Work& w, const U8W& wt, const float* bias, float* C, int64_t ldc, int M, int N, int K,
+                    int ts, int relu, const float* add1, int64_t ld1, hipStream_t s) {
+  const U8Args u{w.xq, w.rs, w.qp, wt.q, wt.cs, wt.bz, wt.ws, ts};
+  EpiLinear epi{C, ldc, bias, add1, ld1, nullptr, 0, relu, 0};
+  if ((int64_t)cdiv(M, 128) * cdiv(N, 128) >= 256) launch_gemm_u8<EpiLinear, 2, 2>(u, M, N, K, epi, s);
+  else launch_gemm_u8<EpiLinear, 1, 1>(u, M, N, K, epi, s);
+}
+
+void gemm_u8_ctc_argmax(const U8Work& w, const U8W& wt, const float* bias, int M, int N, int K, int ts, float* pval,
+                        int* pidx, int* out, hipStream_t s) {
+  const U8Args u{w.xq, w.rs, w.qp, wt.q, wt.cs, wt.bz, wt.ws, ts};
+  const int n_tiles = cdiv(N, 128);
+  EpiArgmax128 epi{bias, pval, pidx, n_tiles};
+  launch_gemm_u8<EpiArgmax128, 2, 2>(u, M, N, K, epi, s);
+  hipLaunchKernelGGL(k_argmax_final, dim3(cdiv(M, 4)), dim3(256), 0, s, pval, pidx, M, n_tiles, out);
+}
+
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
                      int* pidx, int* out, hipStream_t s, const __half* W16, WSplit wb) {
   ALoadPlain al{A, lda};
   int n_tiles = cdiv(N, 64);
-  if (wb.hi && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256) {  // batched: 256x256
+  const WSplit w16{reinterpret_cast<const uint16_t*>(W16)};
+  if (W16 && g_gemm_f16_b3 && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256) {
+    n_tiles = cdiv(N, 256);
+    EpiArgmax256 epi{bias, pval, pidx, n_tiles, 1};
+    launch_gemm_b3_256<ALoadPlain, EpiArgmax256, 1>(al, w16, K, M, N, K, epi, s);
+  } else if (W16 && g_gemm_f16_b3) {
+    n_tiles = cdiv(N, 128);
+    EpiArgmax128 epi{bias, pval, pidx, n_tiles, 1};
+    launch_gemm_b3<ALoadPlain, EpiArgmax128, 2, 2, 32, 1, 1, 1>(al, w16, K, M, N, K, epi, s);
+  } else if (wb.hi && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256) {  // batched: 256x256
     n_tiles = cdiv(N, 256);
     EpiArgmax256 epi{bias, pval, pidx, n_tiles};
     launch_gemm_b3_256(al, wb, K, M, N, K, epi, s);

@@ -31,7 +31,9 @@ struct GemmF32Work {
   int* cnt = nullptr;  // [cnt_n][CNT_LINE]
   int64_t cnt_n = 0;
 };
-extern int g_gemm_f32_split;  // 1 (default): K splits where the tiles leave the chip idle; 0: none
+extern int g_gemm_f32_split;
+extern int g_attn_f16_mfma;  // 1 (default): fp16-graph attention on f16 MFMAs; 0: exact f32 + fp16 rounding
+extern int g_gemm_f16_b3;  // 1 (default): fp16-graph GEMMs on the bf16x3 kernel family with one f16 plane; 0: k_gemm_f16  // 1 (default): K splits where the tiles leave the chip idle; 0: none
 // bf16x3 split of an f32 weight (raw bf16 bits): hi = bf16_rn(w), lo = bf16_rn(w - hi), planes laid out as w
 struct WSplit {
   const uint16_t* hi = nullptr;
@@ -49,6 +51,30 @@ void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t l
                   int n_freq, hipStream_t s, int r16 = 0);
 void gemm_ctc_argmax(const float* A, int64_t lda, const float* W, const float* bias, int M, int N, int K, float* pval,
                      int* pidx, int* out, hipStream_t s, const __half* W16 = nullptr, WSplit wb = {});
+
+// int8-dynamic CTC graph (gemm_f32.hip): ORT quantize_dynamic weights (per output channel uint8) held as int8 w' = wq - 128
+// with per-row sums cs, bz = 128 - zero point and the f32 scale; activations DynamicQuantizeLinear'd per clip into U8Work
+struct U8W {
+  const int8_t* q = nullptr;  // [N][K]
+  const int* cs = nullptr;
+  const int* bz = nullptr;
+  const float* ws = nullptr;
+};
+struct U8Work {
+  int8_t* xq = nullptr;    // [rows][K]
+  int64_t xq_n = 0;
+  int* rs = nullptr;       // [rows]
+  float2* part = nullptr;  // [max_clips][64] min / max partials
+  float2* qp = nullptr;    // [max_clips] {x scale, 128 - x zero point}
+  int max_clips = 0;
+};
+void u8_weight_prep(const uint8_t* q, const float* scale, const uint8_t* zp, int N, int K, int8_t* wq, int* cs, int* bz,
+                    float* ws, hipStream_t s);
+void dq_quantize(const float* x, int64_t ldx, int K, const int* lens, int ts, int B, U8Work& w, hipStream_t s);
+void gemm_u8_linear(const U8Work& w, const U8W& wt, const float* bias, float* C, int64_t ldc, int M, int N, int K,
+                    int ts, int relu, const float* add1, int64_t ld1, hipStream_t s);
+void gemm_u8_ctc_argmax(const U8Work& w, const U8W& wt, const float* bias, int M, int N, int K, int ts, float* pval,
+                        int* pidx, int* out, hipStream_t s);
 
 // attn_f32.hip
 // Key-split workspace of the encoder attention (used only while (query tile, head, clip) blocks leave the

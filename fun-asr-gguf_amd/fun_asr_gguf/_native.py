@@ -21,7 +21,8 @@ EXPORTS = [
     "fa_get_tensor_f32", "fa_fuzzy_substring_distance", "fa_set_decode_fused", "fa_set_encoder_gemm",
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
-    "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head",
+    "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head", "fa_set_tensor_u8dq", "fa_set_ctc_int8",
+    "fa_ctc_int8_active",
 ]
 
 
@@ -66,6 +67,9 @@ def load():
     lib.fa_weights_synthetic.argtypes = [P, ctypes.c_uint32]
     lib.fa_set_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_set_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
+    lib.fa_set_tensor_u8dq.argtypes = [P, ctypes.c_char_p, P, P, P, I64, I64]
+    lib.fa_set_ctc_int8.argtypes = [P, I32]
+    lib.fa_ctc_int8_active.argtypes = [P, P]
     lib.fa_get_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_get_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_weights_mark_unset.argtypes = [P, ctypes.c_char_p]
@@ -182,6 +186,27 @@ class Engine:
         b = np.ascontiguousarray(blocks, dtype=np.uint8)
         _check(self.lib.fa_set_tensor_q8_0(self.h, name.encode(), _ptr(b), b.size), f"fa_set_tensor_q8_0({name})")
         self.weights_gen += 1
+
+    def set_tensor_u8dq(self, name, q, scale, zero_point):
+        """One CTC-graph linear in onnxruntime dynamic-quant form (Fun-ASR-Nano-CTC.int8.onnx): q [out][in] uint8,
+        scale [out] f32, zero_point [out] uint8 (fa_set_tensor_u8dq). With every CTC linear set, the CTC head runs the
+        int8-dynamic graph."""
+        q = np.ascontiguousarray(q, dtype=np.uint8)
+        sc = np.ascontiguousarray(scale, dtype=np.float32).ravel()
+        zp = np.ascontiguousarray(zero_point, dtype=np.uint8).ravel()
+        assert q.ndim == 2 and sc.size == zp.size == q.shape[0]
+        _check(self.lib.fa_set_tensor_u8dq(self.h, name.encode(), _ptr(q), _ptr(sc), _ptr(zp), q.shape[0], q.shape[1]),
+               f"fa_set_tensor_u8dq({name})")
+        self.weights_gen += 1
+
+    def set_ctc_int8(self, on=True):
+        """Run the int8-dynamic CTC graph once its weights are set (default), or the f32 / fp16 graph."""
+        _check(self.lib.fa_set_ctc_int8(self.h, 1 if on else 0), "fa_set_ctc_int8")
+
+    def ctc_int8_active(self):
+        v = ctypes.c_int32()
+        _check(self.lib.fa_ctc_int8_active(self.h, ctypes.byref(v)), "fa_ctc_int8_active")
+        return bool(v.value)
 
     def get_tensor_q8_0(self, name, n_elements):
         out = np.empty(n_elements // 32 * 34, np.uint8)

@@ -130,6 +130,13 @@ class ModelManager:
                     self.engine.mark_unset(g)
                 for k, v in sd.items():
                     self.engine.set_tensor(k, v)
+                if role == "ctc" and str(p).endswith(".onnx"):
+                    # Fun-ASR-Nano-CTC.int8.onnx (the README's default CTC model): its weights as stored, so the CTC
+                    # head runs the int8-dynamic graph's arithmetic rather than an f32 graph of dequantised weights
+                    from ..onnx_weights import u8dq_from_onnx
+                    for k, (q, sc, zp) in u8dq_from_onnx(p).items():
+                        if k.startswith(CTC_GROUPS):
+                            self.engine.set_tensor_u8dq(k, q, sc, zp)
                 expect += [(g, p) for g in groups]
             for g, p in expect:
                 require_loaded(self.engine, g, p)

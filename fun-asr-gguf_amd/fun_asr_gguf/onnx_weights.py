@@ -11,7 +11,8 @@ the dynamo exporter names them by module path from the export wrapper (`hybrid_m
 graph, EncoderExportWrapperPaddable; none for CTCHeadExportWrapper). A weight consumed by MatMul is stored
 [in, out] and is transposed back to nn.Linear's [out, in]; Gemm honours transB. fp16 initializers are widened;
 ORT dynamic-quant weights (`<w>_quantized` uint8 + `<w>_scale` + `<w>_zero_point`, per output channel) are
-dequantised to f32 (the runtime activation quantisation of MatMulInteger is not reproduced).
+dequantised to f32 by state_dict_from_onnx, and handed over as they are by u8dq_from_onnx: the CTC graph runs them with
+the quantized graph's own arithmetic (DynamicQuantizeLinear + MatMulInteger on the GPU, fa_set_tensor_u8dq).
 Parity unpinned: no ONNX file ships in the reference (weights absent) and `onnx` is not installed; the reader is
 tested on files written by the repo's own encoder of the same wire format (tests/test_weights_io.py).
 """
@@ -131,6 +132,36 @@ def read_onnx(path):
     return inits, nodes
 
 
+def _key(name):
+    return name[len("hybrid_model."):] if name.startswith("hybrid_model.") else name
+
+
+def u8dq_from_onnx(path, inits=None):
+    """ORT dynamic-quant MatMul weights of an ONNX file, as stored: {state_dict weight name: (q [out][in] uint8,
+    scale [out] f32, zero_point [out] uint8)} (the `<w>_quantized` initializer is the MatMul B [in][out]; per output
+    channel scale / zero point, 02-Quantize-ONNX.py:38-46 per_channel=True, QUInt8)."""
+    if inits is None:
+        inits, _ = read_onnx(path)
+    out = {}
+    for name, a in inits.items():
+        if not name.endswith("_quantized"):
+            continue
+        base = name[: -len("_quantized")]
+        scale, zp = inits.get(base + "_scale"), inits.get(base + "_zero_point")
+        key = _key(base)
+        if scale is None or a.ndim != 2 or not key.endswith(".weight"):
+            continue
+        n_out = a.shape[1]
+        scale = np.asarray(scale, np.float32).ravel()
+        zp = np.zeros(n_out, np.uint8) if zp is None else np.asarray(zp).astype(np.uint8).ravel()
+        if scale.size == 1:  # per-tensor quantisation: one scale / zero point for every channel
+            scale, zp = np.repeat(scale, n_out), np.repeat(zp, n_out)
+        if scale.size != n_out or zp.size != n_out:
+            raise ValueError(f"{path}: {base}: scale / zero point do not match the {n_out} output channels")
+        out[key] = (np.ascontiguousarray(np.asarray(a, np.uint8).T), scale, zp)
+    return out
+
+
 def state_dict_from_onnx(path):
     """HybridSenseVoice state_dict entries (f32, nn.Linear [out, in]) held by an encoder or CTC ONNX file."""
     inits, nodes = read_onnx(path)
@@ -154,7 +185,7 @@ def state_dict_from_onnx(path):
             continue
         else:
             uses = consumers.get(name, [])
-        key = base[len("hybrid_model."):] if base.startswith("hybrid_model.") else base
+        key = _key(base)
         if not key.startswith(("audio_encoder.", "audio_adaptor.", "ctc_decoder.", "ctc_proj.")):
             continue
         w = np.asarray(a, np.float32)

@@ -71,6 +71,19 @@ int fa_weights_synthetic(fa_engine* e, uint32_t seed);
  * quantised to q8_0 on device with the ggml reference quantiser (gguf/quants.py:378-393). */
 int fa_set_tensor_f32(fa_engine* e, const char* name, const float* host, int64_t n);
 int fa_set_tensor_q8_0(fa_engine* e, const char* name, const uint8_t* blocks, int64_t n_bytes);
+/* One CTC-graph linear in ONNX Runtime dynamic-quant form, as Fun-ASR-Nano-CTC.int8.onnx holds it (02-Quantize-ONNX.py
+ * :38-46: quantize_dynamic over MatMul, per_channel, QUInt8 weights): q [rows = out][cols = in] uint8 (the ONNX
+ * `<w>_quantized` [in][out] initializer transposed), scale[out] (`<w>_scale`), zero_point[out] (`<w>_zero_point`). `name`
+ * is the f32 weight's state_dict name (ctc_decoder.* / ctc_proj.ctc_lo.weight). Once every CTC-graph linear has its
+ * int8 form, the CTC head runs the quantized graph's arithmetic (DynamicQuantizeLinear of each MatMul input per clip,
+ * MatMulInteger, f32 rescale; attention and LayerNorm f32) instead of the f32 graph — replaces the CTC InferenceSession
+ * over the int8 model (decoder.py:27, nano_onnx.py:21-46). */
+int fa_set_tensor_u8dq(fa_engine* e, const char* name, const uint8_t* q, const float* scale, const uint8_t* zero_point,
+                       int64_t rows, int64_t cols);
+/* 1 (default): the int8-dynamic CTC graph once all its weights are set; 0: the f32 (or fp16) CTC graph. */
+int fa_set_ctc_int8(fa_engine* e, int32_t on);
+/* *out = 1 when the next CTC head runs the int8-dynamic graph. */
+int fa_ctc_int8_active(fa_engine* e, int32_t* out);
 /* Decoder weights from a GGUF v3 file (q8_0 / f32 / f16 tensors) — replaces llama_model_load_from_file. */
 int fa_load_gguf(fa_engine* e, const char* path);
 /* Copy a decoder tensor back as ggml q8_0 blocks (test hook). */
