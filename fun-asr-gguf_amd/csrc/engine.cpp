@@ -161,6 +161,7 @@ struct Engine {
   // batch 32 1.223 / 1.239 / 1.358 ms: one step per graph replay stays the default
   int graph_steps = 1;
   bool pf_row_local = false;  // the prefill forward being run is row-local (see llm_forward)
+  int pf_rl_max = 1024;       // prompts longer than this prefill on the tiled forward, alone (FUNASR_PF_ROW_LOCAL_MAX)
   int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after a fused fan-in timeout
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
@@ -1378,6 +1379,41 @@ struct Engine {
     FA_REQUIRE(!fused_error(), "decode chunk re-run: error flag set on the 5-launch layer");
   }
 
+  // one prompt's prefill (fa_llm_prefill; also a long prompt of a row-local batch): row-local up to pf_rl_max rows (a
+  // prompt's arithmetic is then the same alone and in a row-local batch); above, the tiled forward (query-tiled
+  // attention, tiled GEMMs), which is faster there (scripts/prof_prefill_long.py: 2000 rows 19.8 vs 32.4 ms; 512 / 1024
+  // rows 5.5 / 12.4 ms row-local vs 11.0 / 13.4 tiled; 1536 rows row-local 21.5 ms)
+  void prefill_one(int seq, const float* embd, int n_tokens, int32_t* tok_out, float* logits_out) {
+    const int E = lc.n_embd;
+    FA_HIP(hipMemcpyAsync(lx, embd, (size_t)n_tokens * E * 4, hipMemcpyHostToDevice, stream));
+    std::vector<int> sq(n_tokens, seq), ps(n_tokens);
+    for (int i = 0; i < n_tokens; ++i) ps[i] = n_past[seq] + i;
+    FA_HIP(hipMemcpyAsync(d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipMemcpyAsync(d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, stream));
+    set_prefill_tiles(sq.data(), ps.data(), n_tokens);
+    pf_row_local = n_tokens <= pf_rl_max;
+    try {
+      llm_forward(n_tokens, false, n_past[seq] + n_tokens - 1);
+    } catch (...) {
+      pf_row_local = false;
+      throw;
+    }
+    pf_row_local = false;
+    n_ptiles = 0;
+    // the first token's draw is keyed by the last prompt row's (seq, position)
+    sample(1, d_tok_seq + (n_tokens - 1), d_tok_pos + (n_tokens - 1), nullptr, d_tok_cur, nullptr);
+    int tok = 0;
+    FA_HIP(hipMemcpyAsync(&tok, d_tok_cur, 4, hipMemcpyDeviceToHost, stream));
+    if (logits_out) FA_HIP(hipMemcpyAsync(logits_out, logits, (size_t)lc.n_vocab * 4, hipMemcpyDeviceToHost, stream));
+    FA_HIP(hipStreamSynchronize(stream));
+    prof_collect();
+    n_past[seq] += n_tokens;
+    last_tok[seq] = tok;
+    std::fill(logits_row.begin(), logits_row.end(), -1);
+    logits_row[seq] = 0;
+    if (tok_out) *tok_out = tok;
+  }
+
   // one decode step for the n active sequences: embed last token -> forward -> sample -> advance
   void decode_step(int n) {
     // profiled (eager) steps: give the host a head start so the sampled event pairs time back-to-back kernels,
@@ -1527,6 +1563,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_gemm_bf3_256 = 192;
     if (const char* g = getenv("FUNASR_BF3_256")) fa::g_gemm_bf3_256 = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_F16_GEMM")) fa::g_gemm_f16_b3 = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
     // scripts/ubench/attn_batch at batch 32, 42.7 MB of K/V: 14.65 vs 15.7-15.9 us for the split blocks
@@ -1927,31 +1964,8 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   FA_REQUIRE(n_tokens >= 1 && e->n_past[seq] + n_tokens <= e->lc.n_ctx, "prefill exceeds n_ctx");
-  const int E = e->lc.n_embd;
-  FA_HIP(hipMemcpyAsync(e->lx, embd, (size_t)n_tokens * E * 4, hipMemcpyHostToDevice, e->stream));
-  std::vector<int> sq(n_tokens, seq), ps(n_tokens);
-  for (int i = 0; i < n_tokens; ++i) ps[i] = e->n_past[seq] + i;
-  FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
-  FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, e->stream));
   e->set_sampling(s);
-  e->set_prefill_tiles(sq.data(), ps.data(), n_tokens);
-  e->pf_row_local = true;  // a prompt's prefill arithmetic is the same alone and in a row-local batch
-  e->llm_forward(n_tokens, false, e->n_past[seq] + n_tokens - 1);
-  e->pf_row_local = false;
-  e->n_ptiles = 0;
-  // the first token's draw is keyed by the last prompt row's (seq, position)
-  e->sample(1, e->d_tok_seq + (n_tokens - 1), e->d_tok_pos + (n_tokens - 1), nullptr, e->d_tok_cur, nullptr);
-  int tok = 0;
-  FA_HIP(hipMemcpyAsync(&tok, e->d_tok_cur, 4, hipMemcpyDeviceToHost, e->stream));
-  if (logits_out)
-    FA_HIP(hipMemcpyAsync(logits_out, e->logits, (size_t)e->lc.n_vocab * 4, hipMemcpyDeviceToHost, e->stream));
-  FA_HIP(hipStreamSynchronize(e->stream));
-  e->prof_collect();
-  e->n_past[seq] += n_tokens;
-  e->last_tok[seq] = tok;
-  std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
-  e->logits_row[seq] = 0;
-  if (tok_out) *tok_out = tok;
+  e->prefill_one(seq, embd, n_tokens, tok_out, logits_out);
   FA_API_END
 }
 
@@ -1963,36 +1977,45 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs, "prefill batch: n_seqs out of range");
   const int E = e->lc.n_embd;
   std::vector<char> seen(e->lc.max_seqs, 0);
-  int64_t total = 0;
+  std::vector<int64_t> off(n_seqs + 1, 0);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = seqs[i];
     FA_REQUIRE(q >= 0 && q < e->lc.max_seqs && !seen[q], "prefill batch: sequence ids must be distinct and in range");
     seen[q] = 1;
     FA_REQUIRE(n_tokens[i] >= 1 && n_tokens[i] <= e->pf_max && e->n_past[q] + n_tokens[i] <= e->lc.n_ctx,
                "prefill batch: prompt exceeds n_ctx or the row capacity");
-    total += n_tokens[i];
+    off[i + 1] = off[i] + n_tokens[i];
   }
   e->set_sampling(s);
   // within the invariant width the batch is row-local: every prompt gets exactly its fa_llm_prefill arithmetic (the
-  // reference prefills every segment alone)
-  e->pf_row_local = n_seqs <= e->invariant_width();
+  // reference prefills every segment alone). A prompt above pf_rl_max rows gets the tiled forward when alone, so it is
+  // prefilled alone here too.
+  const bool rl = n_seqs <= e->invariant_width();
+  std::vector<int> rest;
+  for (int i = 0; i < n_seqs; ++i) {
+    if (rl && n_tokens[i] > e->pf_rl_max) e->prefill_one(seqs[i], embd + off[i] * E, n_tokens[i], tok_out ? tok_out + i : nullptr, nullptr);
+    else rest.push_back(i);
+  }
+  e->pf_row_local = rl;
   // sequences in order, as many per forward as the row capacity holds; one weight pass per forward
-  int64_t off = 0;
-  for (int i0 = 0; i0 < n_seqs;) {
-    int i1 = i0, rows = 0;
-    while (i1 < n_seqs && rows + n_tokens[i1] <= e->pf_max) rows += n_tokens[i1++];
-    const int n = i1 - i0;
+  for (size_t i0 = 0; i0 < rest.size();) {
+    size_t i1 = i0;
+    int rows = 0;
+    while (i1 < rest.size() && rows + n_tokens[rest[i1]] <= e->pf_max) rows += n_tokens[rest[i1++]];
+    const int n = (int)(i1 - i0);
     std::vector<int> sq(rows), ps(rows), last(n), lseq(n), lpos(n);
-    for (int i = i0, r = 0; i < i1; ++i) {
+    for (size_t k = i0, r = 0; k < i1; ++k) {
+      const int i = rest[k];
+      FA_HIP(hipMemcpyAsync(e->lx + (size_t)r * E, embd + off[i] * E, (size_t)n_tokens[i] * E * 4, hipMemcpyHostToDevice,
+                            e->stream));
       for (int t = 0; t < n_tokens[i]; ++t, ++r) {
         sq[r] = seqs[i];
         ps[r] = e->n_past[seqs[i]] + t;
       }
-      last[i - i0] = r - 1;
-      lseq[i - i0] = seqs[i];
-      lpos[i - i0] = ps[r - 1];
+      last[k - i0] = (int)r - 1;
+      lseq[k - i0] = seqs[i];
+      lpos[k - i0] = ps[r - 1];
     }
-    FA_HIP(hipMemcpyAsync(e->lx, embd + off * E, (size_t)rows * E * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
@@ -2013,17 +2036,16 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     FA_HIP(hipStreamSynchronize(e->stream));
     e->prof_collect();
     std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
-    for (int i = i0; i < i1; ++i) {
+    for (size_t k = i0; k < i1; ++k) {
+      const int i = rest[k];
       e->n_past[seqs[i]] += n_tokens[i];
-      e->last_tok[seqs[i]] = tok[i - i0];
-      e->logits_row[seqs[i]] = i - i0;
-      if (tok_out) tok_out[i] = tok[i - i0];
+      e->last_tok[seqs[i]] = tok[k - i0];
+      e->logits_row[seqs[i]] = (int)(k - i0);
+      if (tok_out) tok_out[i] = tok[k - i0];
     }
-    off += rows;
     i0 = i1;
   }
   e->pf_row_local = false;
-  (void)total;
   FA_API_END
 }
 

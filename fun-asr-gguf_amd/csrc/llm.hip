@@ -1466,7 +1466,10 @@ int g_attn_lean = -1;      // -1: lean blocks when a launch needs more than 3 pe
 int g_attn_wide = 0;       // decode launches with at least this many (token, kv head) pairs: one 16-wave block each
 constexpr int AGI = 16;   // 4-key groups per wave per pass (registers: 16 int4 of K + 16 of V)
 constexpr int ASPLIT = ATTN_SPLITS;  // key splits (blocks) per (token, kv head)
-constexpr int AMIN_G = 8;            // minimum 4-key groups per split (32 keys = 16 KB of K+V)
+#ifndef FA_AMIN_G
+#define FA_AMIN_G 8
+#endif
+constexpr int AMIN_G = FA_AMIN_G;    // minimum 4-key groups per split (32 keys = 16 KB of K+V)
 constexpr int APART = ATTN_PART_FLOATS;  // per-split partial: o[GQ][128], m[GQ], l[GQ]
 // Within a split, keys are dealt to the waves in 4-key groups, round-robin (group q -> wave q % AWV).
 // Lane (kq = lane>>4, dq = lane&15) holds dims [8 dq, 8 dq + 8) of key 4 q + kq: each load instruction

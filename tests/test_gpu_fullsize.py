@@ -547,3 +547,33 @@ def test_llm_full_slot_reuse_above_width_bound(eng, g60):
             admitted = True
     assert admitted and all(k_of[c] == n_steps[c] for c in range(40))
     print(f"slot reuse above the width: worst cosine {worst:.6f}")
+
+
+def test_long_prompt_prefilled_alone_in_row_local_batch(monkeypatch):
+    """A prompt above the row-local limit (FUNASR_PF_ROW_LOCAL_MAX; default 1024 rows, above which the tiled forward is
+    faster: scripts/prof_prefill_long.py) prefills on the tiled forward when alone, so a row-local batch prefills it
+    alone too: every prompt's first token, and the logits of the next decode step (a batch of 3 within the invariant
+    width), equal its single-prompt run bit for bit."""
+    from fun_asr_gguf import _native
+    monkeypatch.setenv("FUNASR_PF_ROW_LOCAL_MAX", "100")
+    e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_FULL, n_ctx=512, max_seqs=4), max_batch=1, max_samples=SR * 2)
+    try:
+        e.synthetic_weights(0)
+        rng = np.random.default_rng(5)
+        prompts = [(rng.standard_normal((n, 1024)) * 0.05).astype(np.float32) for n in (204, 80, 150)]
+        single = []
+        for p in prompts:
+            e.llm_reset(0)
+            t, lg = e.llm_prefill(0, p, want_logits=True)
+            t1 = int(e.llm_generate([0], 1)[0][0])
+            single.append((int(t), lg, t1, e.llm_logits(0)))
+        for s in range(3):
+            e.llm_reset(s)
+        toks = e.llm_prefill_batch([0, 1, 2], prompts)
+        assert [int(t) for t in toks] == [x[0] for x in single]
+        assert np.array_equal(e.llm_logits(1), single[1][1])  # the row-local part of the batch (its last forward)
+        nxt = e.llm_generate([0, 1, 2], 1)[:, 0]
+        for s in range(3):
+            assert int(nxt[s]) == single[s][2] and np.array_equal(e.llm_logits(s), single[s][3]), f"prompt {s}"
+    finally:
+        e.close()
