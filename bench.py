@@ -292,7 +292,7 @@ def c4_leg(steps, warmup, device, model, barrier, dist):
     """configs[3] (C4): one 300 s file, segment_size 60 / overlap 4 -> 6 segments {0-60, 56-116, ..., 280-300}
     (orchestrator.py:123-136) through the public FunASREngine.transcribe long path. N=1: all segments as one
     device batch. N>1: segments assigned longest-first to ranks (fun_asr_gguf.parallel), records gathered to
-    rank 0 (gather_object over RCCL), merged there. Every segment decodes 253 greedy tokens, EOS ignored (the
+    rank 0 through the engine's own RCCL communicator (fa_comm_allgather_*), merged there. Every segment decodes 253 greedy tokens, EOS ignored (the
     20 s segment too, above its pinned 85: conservative). The PCM goes host -> HBM inside the call (PCIe-inclusive)."""
     from fun_asr_gguf import FunASREngine
     from fun_asr_gguf.synthetic import synth_audio
@@ -305,6 +305,9 @@ def c4_leg(steps, warmup, device, model, barrier, dist):
     m.prompt_builder.fixed_ids = (list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_PREFIX)),
                                   list(rng.integers(0, m.llm_cfg["n_vocab"] - 3, N_SUFFIX)))
     audio = synth_audio(300 * SR, 4000)
+    if dist is not None:  # the records gather to rank 0 through the engine's own RCCL communicator (fa_comm_*)
+        from fun_asr_gguf.parallel import init_native_comm
+        init_native_comm(m.engine, dist)
 
     def step():
         return eng.transcribe(audio, segment_size=60.0, overlap=4.0, temperature=0.0, verbose=False, ranks=dist)

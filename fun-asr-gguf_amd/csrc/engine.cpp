@@ -4,6 +4,9 @@
 // for max_batch x max_samples, the fp16 KV cache [layer][seq][kv head][n_ctx][128], one HIP stream.
 // Encoder math follows model_definition.py (SenseVoiceEncoderSmall / CorrectTransformerAdaptor /
 // CTC head); decoder math follows llama.cpp's qwen3 graph with ggml q8_0 numerics (oracle/qwen3.py).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -173,6 +176,13 @@ struct Engine {
   int* gk_cnt = nullptr;
   int64_t gk_part_n = 0, gk_cnt_n = 0;
 
+  // result gather over RCCL (fa_comm_*): this engine's communicator and its device staging buffers
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_world = 0;
+  int64_t* comm_sz = nullptr;  // [world]
+  uint8_t* comm_buf = nullptr;  // send (cap) + receive (world x cap)
+  int64_t comm_cap = 0;
+
   // profiling
   bool prof = false;
   struct ProfCls {
@@ -198,6 +208,7 @@ struct Engine {
     return (T*)p;
   }
   ~Engine() {
+    if (comm_buf) hipFree(comm_buf);
     for (auto& l : enc_lanes)
       if (l.s) hipStreamSynchronize(l.s);
     if (stream) hipStreamSynchronize(stream);
@@ -1563,6 +1574,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_gemm_bf3_256 = 192;
     if (const char* g = getenv("FUNASR_BF3_256")) fa::g_gemm_bf3_256 = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_F16_GEMM")) fa::g_gemm_f16_b3 = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_BF3_MID")) fa::g_gemm_bf3_mid = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
@@ -2160,6 +2172,113 @@ int fa_profile_read(fa_engine* h, int32_t cls, double* ms, int64_t* launches, do
 int fa_synchronize(fa_engine* h) {
   FA_API_BEGIN
   FA_HIP(hipStreamSynchronize(h->e->stream));
+  FA_API_END
+}
+
+// ---- result gather over RCCL: the only exchange of the sharded long-audio / clip-batch path. librccl is
+// resolved at first use (dlopen: no load-time dependency; a process that already holds RCCL, e.g. torch's, shares it)
+namespace {
+struct RcclApi {
+  bool ok = false;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+    api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+    api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+    api.ok = api.get_unique_id && api.comm_init_rank && api.all_gather && api.comm_destroy && api.error_string;
+  });
+  return api;
+}
+}  // namespace
+#define FA_NCCL(expr)                                                                                    \
+  do {                                                                                                   \
+    const ncclResult_t _r = (expr);                                                                      \
+    FA_REQUIRE(_r == ncclSuccess, std::string("RCCL: ") + rccl().error_string(_r) + " (" #expr ")"); \
+  } while (0)
+
+int fa_comm_unique_id(uint8_t* id_out) {
+  FA_API_BEGIN
+  FA_REQUIRE(id_out, "fa_comm_unique_id: id_out");
+  FA_REQUIRE(rccl().ok, "fa_comm_unique_id: librccl.so.1 not loadable");
+  ncclUniqueId id;
+  FA_NCCL(rccl().get_unique_id(&id));
+  std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  FA_API_END
+}
+
+int fa_comm_init(fa_engine* h, int32_t rank, int32_t world, const uint8_t* id) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(id && world >= 1 && rank >= 0 && rank < world, "fa_comm_init args");
+  FA_REQUIRE(!e->comm, "fa_comm_init: this engine already has a communicator");
+  FA_REQUIRE(rccl().ok, "fa_comm_init: librccl.so.1 not loadable");
+  FA_HIP(hipSetDevice(e->device));
+  ncclUniqueId uid;
+  std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+  FA_NCCL(rccl().comm_init_rank(&e->comm, world, uid, rank));
+  e->comm_rank = rank;
+  e->comm_world = world;
+  e->comm_sz = e->alloc<int64_t>(2 * world);
+  FA_API_END
+}
+
+int fa_comm_allgather_sizes(fa_engine* h, int64_t n, int64_t* sizes_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(e->comm && sizes_out && n >= 0, "fa_comm_allgather_sizes: no communicator / args");
+  FA_HIP(hipSetDevice(e->device));
+  FA_HIP(hipMemcpyAsync(e->comm_sz + e->comm_world, &n, 8, hipMemcpyHostToDevice, e->stream));
+  FA_NCCL(rccl().all_gather(e->comm_sz + e->comm_world, e->comm_sz, 1, ncclInt64, e->comm, e->stream));
+  FA_HIP(hipMemcpyAsync(sizes_out, e->comm_sz, (size_t)e->comm_world * 8, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_comm_allgather_bytes(fa_engine* h, const uint8_t* data, int64_t n, int64_t slot, uint8_t* out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(e->comm && out && n >= 0 && slot >= n && slot >= 1 && (n == 0 || data),
+             "fa_comm_allgather_bytes: no communicator / args (every rank passes the same slot >= its n)");
+  FA_HIP(hipSetDevice(e->device));
+  if (slot > e->comm_cap) {
+    if (e->comm_buf) FA_HIP(hipFree(e->comm_buf));
+    e->comm_buf = nullptr;
+    FA_HIP(hipMalloc(&e->comm_buf, (size_t)slot * (e->comm_world + 1)));
+    e->comm_cap = slot;
+  }
+  uint8_t* send = e->comm_buf + (size_t)e->comm_world * slot;
+  FA_HIP(hipMemsetAsync(send, 0, slot, e->stream));
+  if (n) FA_HIP(hipMemcpyAsync(send, data, n, hipMemcpyHostToDevice, e->stream));
+  FA_NCCL(rccl().all_gather(send, e->comm_buf, (size_t)slot, ncclUint8, e->comm, e->stream));
+  FA_HIP(hipMemcpyAsync(out, e->comm_buf, (size_t)slot * e->comm_world, hipMemcpyDeviceToHost, e->stream));
+  FA_HIP(hipStreamSynchronize(e->stream));
+  FA_API_END
+}
+
+int fa_comm_destroy(fa_engine* h) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  if (e->comm) {
+    FA_HIP(hipStreamSynchronize(e->stream));
+    FA_NCCL(rccl().comm_destroy(e->comm));
+    e->comm = nullptr;
+  }
+  if (e->comm_buf) FA_HIP(hipFree(e->comm_buf));
+  e->comm_buf = nullptr;
+  e->comm_cap = 0;
   FA_API_END
 }
 

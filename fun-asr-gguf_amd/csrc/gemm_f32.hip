@@ -647,7 +647,8 @@ int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ah
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
                            // 6 = 256x256x32
 int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
-int g_gemm_f16_b3 = 1;     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
+int g_gemm_f16_b3 = 1;
+int g_gemm_bf3_mid = 1;    // few-tile shapes with 256-1024 64x64 tiles (one clip: q|k|v, ffn1) on 128x64 tiles (FUNASR_BF3_MID)     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
 
 // P = 3: bf16x3 split operands (two bf16 planes per operand, three MFMAs per 16 of k); P = 1: the fp16 graph (C5):
 // one fp16 plane per operand (the activations are fp16 values, converted exactly while staged; W is the fp16 weight
@@ -1070,6 +1071,10 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
     launch_gemm_b3_256<AL, EPI, P>(al, w, ldw, M, N, K, epi, s);
   else if (big) launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
   else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
+  // 256 < 64x64 tiles <= 1024 (one clip's q|k|v and ffn1: 384 / 512 tiles, i.e. 1.5-2 rounds of one 147-KiB block per
+  // CU): 128x64 tiles, two K groups of 32-deep stages, loads two steps ahead -- one round of twice the work per block
+  else if (f == 7 || (f == 0 && g_gemm_bf3_mid && t64 > 256 && t64 <= 1024 && K % 64 == 0))
+    launch_gemm_b3<AL, EPI, 2, 1, 32, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
   else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
     if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
     else launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 1, P>(al, w, ldw, M, N, K, epi, s);

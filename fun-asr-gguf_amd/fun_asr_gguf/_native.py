@@ -22,7 +22,8 @@ EXPORTS = [
     "fa_vocab_load_gguf", "fa_vocab_free", "fa_vocab_info", "fa_tokenize", "fa_token_piece", "fa_gguf_read_tensor",
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
     "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head", "fa_set_tensor_u8dq", "fa_set_ctc_int8",
-    "fa_ctc_int8_active",
+    "fa_ctc_int8_active", "fa_comm_unique_id", "fa_comm_init", "fa_comm_allgather_sizes", "fa_comm_allgather_bytes",
+    "fa_comm_destroy",
 ]
 
 
@@ -70,6 +71,11 @@ def load():
     lib.fa_set_tensor_u8dq.argtypes = [P, ctypes.c_char_p, P, P, P, I64, I64]
     lib.fa_set_ctc_int8.argtypes = [P, I32]
     lib.fa_ctc_int8_active.argtypes = [P, P]
+    lib.fa_comm_unique_id.argtypes = [P]
+    lib.fa_comm_init.argtypes = [P, I32, I32, P]
+    lib.fa_comm_allgather_sizes.argtypes = [P, I64, P]
+    lib.fa_comm_allgather_bytes.argtypes = [P, P, I64, I64, P]
+    lib.fa_comm_destroy.argtypes = [P]
     lib.fa_get_tensor_q8_0.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_get_tensor_f32.argtypes = [P, ctypes.c_char_p, P, I64]
     lib.fa_weights_mark_unset.argtypes = [P, ctypes.c_char_p]
@@ -149,8 +155,38 @@ class Engine:
 
     def close(self):
         if getattr(self, "h", None):
+            if getattr(self, "comm_world", 0):
+                self.lib.fa_comm_destroy(self.h)
+                self.comm_world = 0
             self.lib.fa_engine_destroy(self.h)
             self.h = None
+
+    # ---- result gather over RCCL (fa_comm_*)
+    @staticmethod
+    def comm_unique_id():
+        """128-byte RCCL id, created on rank 0 and handed to every rank (fa_comm_unique_id)."""
+        lib = load()
+        buf = np.zeros(128, np.uint8)
+        _check(lib.fa_comm_unique_id(_ptr(buf)), "fa_comm_unique_id")
+        return buf.tobytes()
+
+    def comm_init(self, rank, world, uid):
+        """Join this engine to an RCCL communicator of `world` ranks (fa_comm_init)."""
+        b = np.frombuffer(bytes(uid), np.uint8).copy()
+        assert b.size == 128
+        _check(self.lib.fa_comm_init(self.h, rank, world, _ptr(b)), "fa_comm_init")
+        self.comm_rank, self.comm_world = rank, world
+
+    def comm_allgather(self, payload):
+        """Every rank's bytes, in rank order (two RCCL all-gathers: the sizes, then the padded payloads)."""
+        data = np.frombuffer(bytes(payload), np.uint8).copy() if payload else np.zeros(1, np.uint8)
+        n = len(payload)
+        sizes = np.zeros(self.comm_world, np.int64)
+        _check(self.lib.fa_comm_allgather_sizes(self.h, n, _ptr(sizes)), "fa_comm_allgather_sizes")
+        slot = max(1, int(sizes.max()))
+        out = np.zeros(slot * self.comm_world, np.uint8)
+        _check(self.lib.fa_comm_allgather_bytes(self.h, _ptr(data), n, slot, _ptr(out)), "fa_comm_allgather_bytes")
+        return [out[r * slot: r * slot + int(sizes[r])].tobytes() for r in range(self.comm_world)]
 
     def __del__(self):
         try:

@@ -2,9 +2,10 @@
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI on ROCm, "gloo" in CPU tests).
 Segments are assigned longest-first to the least-loaded rank (LPT); every rank decodes its share as one
-device batch; the only exchange is the result gather to rank 0 (tensor all_gathers of the JSON-encoded per-segment
-records: text, char timestamps, hotwords, CTC tokens, timings), after which rank 0 merges. No data-path
-collective: the PCM chunks are cut from the same input on every rank.
+device batch; the only exchange is the result gather to rank 0 (all-gathers of the JSON-encoded per-segment
+records: text, char timestamps, hotwords, CTC tokens, timings), after which rank 0 merges. The gather runs through the
+engine's own RCCL communicator when one was set up (init_native_comm -> fa_comm_*), else through torch.distributed.
+No data-path collective: the PCM chunks are cut from the same input on every rank.
 """
 import json
 from dataclasses import asdict
@@ -42,6 +43,37 @@ def _pack(records_by_index):
     return json.dumps(sorted(records_by_index.items()), ensure_ascii=False).encode("utf-8")
 
 
+def init_native_comm(engine, dist, group=None):
+    """Give `engine` its own RCCL communicator over the ranks of `dist` (fa_comm_init): rank 0 creates the 128-byte id
+    and broadcasts it over `dist` (any backend: it is only the bootstrap). Afterwards gather_to_root moves the records
+    through the engine (native RCCL all-gathers over xGMI), not through torch.distributed."""
+    import torch
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(engine.comm_unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, 0, group=group)
+    engine.comm_init(rank, world, bytes(uid.cpu().numpy()))
+    return engine
+
+
+def _merge(blobs, n_total):
+    merged = {}
+    for b in blobs:
+        for idx, rec in json.loads(b.decode("utf-8")):
+            merged[int(idx)] = rec
+    assert len(merged) == n_total, f"gather lost segments: {len(merged)} of {n_total}"
+    return [merged[i] for i in range(n_total)]
+
+
+def gather_native(records_by_index, n_total, engine):
+    """gather_to_root through the engine's own RCCL communicator (init_native_comm): every rank's JSON records,
+    merged on rank 0."""
+    blobs = engine.comm_allgather(_pack(records_by_index))
+    return _merge(blobs, n_total) if engine.comm_rank == 0 else None
+
+
 def gather_to_root(records_by_index, n_total, dist, group=None):
     """records_by_index: {segment index: record} of this rank -> full ordered list on rank 0, None elsewhere.
     Two tensor collectives over the process group (RCCL over xGMI with backend "nccl": device tensors; gloo: host): an
@@ -64,12 +96,7 @@ def gather_to_root(records_by_index, n_total, dist, group=None):
     dist.all_gather(bufs, buf, group=group)
     if rank != 0:
         return None
-    merged = {}
-    for b, k in zip(bufs, sizes):
-        for idx, rec in json.loads(bytes(b[:k].cpu().numpy()).decode("utf-8")):
-            merged[int(idx)] = rec
-    assert len(merged) == n_total, f"gather lost segments: {len(merged)} of {n_total}"
-    return [merged[i] for i in range(n_total)]
+    return _merge([bytes(b[:k].cpu().numpy()) for b, k in zip(bufs, sizes)], n_total)
 
 
 def sharded_decode(orch, chunks, language, context, verbose, temperature, top_p, top_k, dist):
@@ -79,5 +106,9 @@ def sharded_decode(orch, chunks, language, context, verbose, temperature, top_p,
     local = orch.decode_segments([chunks[i] for i in mine], language, context, verbose, temperature, top_p,
                                  top_k) if mine else []
     recs = {i: to_record(d) for i, d in zip(mine, local)}
-    full = gather_to_root(recs, len(chunks), dist)
+    eng = getattr(getattr(orch, "models", None), "engine", None)
+    if getattr(eng, "comm_world", 0) == world:  # the engine's own RCCL communicator (init_native_comm)
+        full = gather_native(recs, len(chunks), eng)
+    else:
+        full = gather_to_root(recs, len(chunks), dist)
     return None if full is None else [from_record(r) for r in full]

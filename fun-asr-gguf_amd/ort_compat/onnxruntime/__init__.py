@@ -25,7 +25,7 @@ if _PKG not in sys.path:
 from fun_asr_gguf import _native  # noqa: E402
 from fun_asr_gguf.core.model_manager import CTC_GROUPS, ENCODER_GROUPS, require_loaded  # noqa: E402
 from fun_asr_gguf.model_config import ENC_FULL, ENC_TINY, LLM_TINY  # noqa: E402
-from fun_asr_gguf.onnx_weights import read_onnx, state_dict_from_onnx  # noqa: E402
+from fun_asr_gguf.onnx_weights import read_onnx, state_dict_from_onnx, u8dq_from_onnx  # noqa: E402
 
 __version__ = "1.20.0+mi355x"
 PROVIDER = "MI355XExecutionProvider"
@@ -154,6 +154,10 @@ class InferenceSession:
             for k, v in sd.items():
                 if k.startswith(groups):
                     self._eng.set_tensor(k, v)
+            if self._kind == "ctc":  # Fun-ASR-Nano-CTC.int8.onnx: its dynamic-quant weights as stored (int8 graph)
+                for k, (q, sc, zp) in u8dq_from_onnx(path, inits).items():
+                    if k.startswith(groups):
+                        self._eng.set_tensor_u8dq(k, q, sc, zp)
             for g in groups:
                 require_loaded(self._eng, g, path)
         except Exception:

@@ -241,6 +241,16 @@ int fa_profile_enable(fa_engine* e, int32_t on);
 int fa_profile_read(fa_engine* e, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops);
 int fa_synchronize(fa_engine* e);
 
+/* ---- result gather over RCCL (the reference decodes segments sequentially, orchestrator.py:139-171,
+ * so this is the only exchange of the sharded path): one communicator per engine. Rank 0 creates a 128-byte id, the
+ * caller hands it to every rank by any side channel, each rank joins with fa_comm_init. The gather is two all-gathers
+ * (every rank calls both, in order): the record sizes, then the records zero-padded to one slot >= the largest. */
+int fa_comm_unique_id(uint8_t* id_out /* 128 bytes */);
+int fa_comm_init(fa_engine* e, int32_t rank, int32_t world, const uint8_t* id);
+int fa_comm_allgather_sizes(fa_engine* e, int64_t n, int64_t* sizes_out /* [world] */);
+int fa_comm_allgather_bytes(fa_engine* e, const uint8_t* data, int64_t n, int64_t slot, uint8_t* out /* [world * slot] */);
+int fa_comm_destroy(fa_engine* e);
+
 #ifdef __cplusplus
 }
 #endif

@@ -30,6 +30,60 @@ class _StubOrch:
         return out
 
 
+class _FakeCommEngine:
+    """The engine's fa_comm_* surface (comm_rank / comm_world / comm_allgather) over the gloo group: exercises
+    parallel.gather_native's protocol at world > 1 on CPU (the RCCL collectives themselves run in tests/test_gpu_dist.py)."""
+
+    def __init__(self, dist):
+        self.dist, self.comm_rank, self.comm_world = dist, dist.get_rank(), dist.get_world_size()
+        self.calls = 0
+
+    def comm_allgather(self, payload):
+        self.calls += 1
+        out = [None] * self.comm_world
+        self.dist.all_gather_object(out, bytes(payload))
+        return out
+
+
+def _native_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "fun-asr-gguf_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fun_asr_gguf.parallel import sharded_decode
+    orch = _StubOrch()
+    orch.models = type("M", (), {})()
+    orch.models.engine = _FakeCommEngine(dist)
+    chunks = [[0.0] * n for n in (960, 960, 960, 960, 960, 320)]
+    res = sharded_decode(orch, chunks, None, None, False, 0.0, 1.0, 50, dist)
+    assert orch.models.engine.calls == 1
+    if rank == 0:
+        q.put([(r.text, r.aligned, [(t.text, t.start) for t in r.ctc_results]) for r in res])
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_gather_protocol_world3():
+    """sharded_decode through the engine's own communicator (parallel.gather_native) at world 3: rank 0 gets exactly
+    the single-rank records."""
+    from fun_asr_gguf.parallel import to_record, from_record
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = [from_record(to_record(d)) for d in _StubOrch().decode_segments([[0.0] * n for n in (960, 960, 960, 960, 960, 320)])]
+    assert got == [(r.text, r.aligned, [(t.text, t.start) for t in r.ctc_results]) for r in single]
+
+
 def _worker(rank, world, port, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -134,3 +134,25 @@ def test_session_refuses_incomplete_graph(tmp_path):
     write_onnx(str(p), sd)
     with pytest.raises(ValueError, match="norm2"):
         rt.InferenceSession(str(p), providers=["CPUExecutionProvider"])
+
+
+def test_int8_ctc_session_runs_the_int8_graph(tmp_path):
+    """Fun-ASR-Nano-CTC.int8.onnx (the reference README's default CTC model): the session hands the file's dynamic-quant
+    weights to the engine as stored, so decoder.py:27's ctc_sess.run computes the int8 graph (oracle/ctc_int8.py over the
+    same quantized weights: ids equal wherever the oracle's top-2 margin exceeds 0.25, the int8 noise floor of
+    tests/test_gpu_ctc_int8.py), not an f32 graph of dequantised weights."""
+    from fun_asr_gguf.onnx_weights import state_dict_from_onnx, u8dq_from_onnx
+    from oracle import ctc_int8 as oi8
+    rt = ort()
+    _, c, _ = onnx_files(tmp_path, "int8")
+    cs = rt.InferenceSession(c, providers=["CPUExecutionProvider"])
+    assert cs._eng.ctc_int8_active()
+    g = np.load(os.path.join(ROOT, "tests", "golden", "encoder_tiny_3s.npz"))
+    enc = g["enc"][: int(g["t_lfr_valid"])].astype(np.float32)
+    ids = cs.run(None, {cs.get_inputs()[0].name: enc[None]})[0][0]
+    sd = state_dict_from_onnx(c)
+    Q = {k[: -len(".weight")]: v for k, v in u8dq_from_onnx(c).items()}
+    ref_ids, lg = oi8.ctc_ids_int8(enc, sd, Q, synth.ENC_TINY)
+    top2 = np.sort(lg, -1)[:, -2:]
+    bad = (ids != ref_ids) & ((top2[:, 1] - top2[:, 0]) > 0.25)
+    assert ids.shape == ref_ids.shape and bad.sum() == 0 and (ids != ref_ids).mean() < 0.1
