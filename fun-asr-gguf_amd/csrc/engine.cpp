@@ -2190,8 +2190,8 @@ RcclApi& rccl() {
   static RcclApi api;
   static std::once_flag once;
   std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) return;
     api.get_unique_id = (decltype(api.get_unique_id))dlsym(h, "ncclGetUniqueId");
     api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
