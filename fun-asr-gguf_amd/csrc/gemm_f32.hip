@@ -647,8 +647,9 @@ int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ah
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
                            // 6 = 256x256x32
 int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
-int g_gemm_f16_b3 = 1;
-int g_gemm_bf3_mid = 1;    // few-tile shapes with 256-1024 64x64 tiles (one clip: q|k|v, ffn1) on 128x64 tiles (FUNASR_BF3_MID)     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
+int g_gemm_f16_b3 = 1;     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
+int g_gemm_bf3_mid = 0;    // 1: one clip's 256-1024-tile shapes (q|k|v, ffn1) on 128x64 tiles (FUNASR_BF3_MID; A/B: one-clip
+                           // encode 10.47-10.94 vs 10.49 ms bf16x3, 8.74-8.75 vs 8.79-8.82 ms fp16: not kept)
 
 // P = 3: bf16x3 split operands (two bf16 planes per operand, three MFMAs per 16 of k); P = 1: the fp16 graph (C5):
 // one fp16 plane per operand (the activations are fp16 values, converted exactly while staged; W is the fp16 weight
