@@ -645,9 +645,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ahead (1 or 2; FUNASR_BF3_PF)
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
-                           // 6 = 256x256x32
+                           // 6 = 256x256x32, 7 = 128x64x32 K halves, 8 = 64x64 K quarters
 int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
 int g_gemm_f16_b3 = 1;     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
+int g_gemm_bf3_kw4 = 0;    // few-tile shapes with K >= 2048 (one clip's ffn2): four K groups per block (FUNASR_BF3_KW4;
+                           // A/B: ffn2 22.4 vs 23.7 us bf16x3, one-clip encode 10.43-10.63 vs 10.43-10.55 ms bf16x3,
+                           // 8.68-8.74 vs 8.77-8.87 ms fp16: within run-to-run noise, not kept)
 int g_gemm_bf3_mid = 0;    // 1: one clip's 256-1024-tile shapes (q|k|v, ffn1) on 128x64 tiles (FUNASR_BF3_MID; A/B: one-clip
                            // encode 10.47-10.94 vs 10.49 ms bf16x3, 8.74-8.75 vs 8.79-8.82 ms fp16: not kept)
 
@@ -750,9 +753,9 @@ __device__ __forceinline__ void store_b3(typename PrecB<P>::E* st, const float4 
   }
 }
 
-// KW = 2 (few-tile shapes): two groups of 4 waves per block split K in halves, each with its own LDS stages; group 1
-// hands its accumulators to group 0 through LDS (fixed order) and group 0 runs the epilogue. Twice the waves per CU
-// and half the dependent k-steps per wave, with no cross-block split-K seam.
+// KW = 2 / 4 (few-tile shapes): KW groups of 4 waves per block split K in equal parts, each with its own LDS stages;
+// groups 1..KW-1 hand their accumulators to group 0 through LDS (summed in a fixed order) and group 0 runs the
+// epilogue. KW times the waves per CU and 1/KW of the dependent k-steps per wave, with no cross-block split-K seam.
 // PF = 2: the global loads run two k-steps ahead (two register sets, the k loop unrolled by two), so a k-step's
 // tile has two steps of compute to land instead of one: few-tile shapes (one clip) have too little work per step to
 // cover the load latency.
@@ -838,25 +841,29 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
     }
   }
   if constexpr (KW > 1) {
-    float* xs = smem;  // [wave][i][j][16][64]: group 1's accumulators
+    constexpr int XS = 4 * WM * WN * 16 * 64;  // floats per group
+    float* xs = smem;  // [group - 1][wave][i][j][16][64]: groups 1..KW-1's accumulators
 #pragma unroll
     for (int i = 0; i < WM; ++i)
 #pragma unroll
       for (int j = 0; j < WN; ++j)
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-          if (grp == 1) xs[(((wave * WM + i) * WN + j) * 16 + q) * 64 + lane] = acc[i][j][q];
+          if (grp > 0) xs[(grp - 1) * XS + (((wave * WM + i) * WN + j) * 16 + q) * 64 + lane] = acc[i][j][q];
     __syncthreads();
     if (grp == 0) {
 #pragma unroll
-      for (int i = 0; i < WM; ++i)
+      for (int g = 1; g < KW; ++g)  // fixed order: K quarters ascending
 #pragma unroll
-        for (int j = 0; j < WN; ++j)
+        for (int i = 0; i < WM; ++i)
 #pragma unroll
-          for (int q = 0; q < 16; ++q) acc[i][j][q] += xs[(((wave * WM + i) * WN + j) * 16 + q) * 64 + lane];
+          for (int j = 0; j < WN; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+              acc[i][j][q] += xs[(g - 1) * XS + (((wave * WM + i) * WN + j) * 16 + q) * 64 + lane];
     }
     __syncthreads();  // the epilogue may reuse the LDS
-    if (grp == 1) return;
+    if (grp > 0) return;
   }
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -878,7 +885,7 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
   const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM));
   // >= EpiArgmax / EpiArgmax128 scratch, >= the KW = 2 accumulator hand-off
   const size_t lds = std::max<size_t>({(size_t)KW * 2 * T::STAGE * 2, (size_t)(1024 + 4 * 32 * 33) * 4,
-                                       KW > 1 ? (size_t)4 * WM * WN * 16 * 64 * 4 : 0});
+                                       (size_t)(KW - 1) * 4 * WM * WN * 16 * 64 * 4});
   static bool attr = false;
   if (!attr && lds > 65536) {
     (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF, P>,
@@ -1076,7 +1083,11 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   // CU): 128x64 tiles, two K groups of 32-deep stages, loads two steps ahead -- one round of twice the work per block
   else if (f == 7 || (f == 0 && g_gemm_bf3_mid && t64 > 256 && t64 <= 1024 && K % 64 == 0))
     launch_gemm_b3<AL, EPI, 2, 1, 32, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
-  else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
+  else if (f == 8 || (f == 0 && g_gemm_bf3_kw4 && t64 < 256 && K >= 2048 && K % 256 == 0)) {
+    // 1024 threads: 16 waves per CU; P = 3 keeps 32-deep stages (4 groups x 2 stages x 20 KiB = 160 KiB)
+    if constexpr (P == 1) launch_gemm_b3<AL, EPI, 1, 1, 64, 4, 2, P>(al, w, ldw, M, N, K, epi, s);
+    else launch_gemm_b3<AL, EPI, 1, 1, 32, 4, 2, P>(al, w, ldw, M, N, K, epi, s);
+  } else if (f == 4 || (f == 0 && t64 < 256 && K % 128 == 0)) {
     if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
     else launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 1, P>(al, w, ldw, M, N, K, epi, s);
   } else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2, 1, P>(al, w, ldw, M, N, K, epi, s);

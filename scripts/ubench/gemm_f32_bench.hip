@@ -81,8 +81,8 @@ int main(int argc, char** argv) {
   WSplit wb; wb.hi = Wh; wb.lo = Wl;
   for (int sk = 0; sk < 3; ++sk) {  // bf16x3 spot checks (M=100 N=96 K=72; M=70 N=64 K=2048; K halves M=100 N=96 K=256)
     const int M = sk == 1 ? 70 : 100, N = sk == 1 ? 64 : 96, K = sk == 1 ? 2048 : sk == 2 ? 256 : 72;
-    for (int v : {1, 2, 3, 4, 5, 6}) {
-      if ((sk == 1 && v == 2) || (sk < 2 && (v == 4 || v == 5)) || (sk == 2 && v < 4)) continue;
+    for (int v : {1, 2, 3, 4, 5, 6, 8}) {
+      if ((sk == 1 && v == 2) || (sk < 2 && (v == 4 || v == 5)) || (sk == 2 && v < 4) || (v == 8 && sk != 1)) continue;
       g_gemm_bf3_force = v;
       gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s, nullptr, sk ? &wk : nullptr, wb);
       CK(hipStreamSynchronize(s));
@@ -160,14 +160,15 @@ int main(int argc, char** argv) {
         const char* nm[] = {"", "64x64x32", "128x128x32", "64x64x64", "64x64x128", "64x64x32 split-K", "engine default"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
-      for (int v : {1, 3, 4, 5, 2, 6, 0}) {
+      for (int v : {1, 3, 4, 5, 8, 2, 6, 0}) {
         if ((v == 4 || v == 5) && (M > 2000 || sh.K % 128)) continue;
+        if (v == 8 && (M > 2000 || sh.K < 2048)) continue;
         g_gemm_bf3_force = v;
         const double us = time_graph([&] { gemm_linear(A, sh.K + pad, W, sh.K + pad, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s,
                                                        nullptr, &wk, wb); },
                                      M > 2000 ? 10 : 50);
         const char* nm[] = {"bf3 default", "bf3 64x64x32", "bf3 128x128x32", "bf3 64x64x64", "bf3 64x64x64 K/2", "bf3 64x64x32 K/2",
-                            "bf3 256x256x32"};
+                            "bf3 256x256x32", "", "bf3 64x64x32 K/4"};
         printf("  %s %7.1f us %5.1f TF/s", nm[v], us, 2.0 * M * sh.N * sh.K / us / 1e6);
       }
       g_gemm_bf3_force = 0;
