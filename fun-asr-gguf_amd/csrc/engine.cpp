@@ -118,6 +118,10 @@ struct Engine {
   float* tap_lfr = nullptr;
   // last encode geometry
   int last_batch = 0, last_tstride = 0;
+  int64_t enc_gen = 0;         // +1 per encode / CTC-head call: the adaptor rows fa_llm_prefill_rows may read
+  float* d_prow = nullptr;     // fa_llm_prefill_rows: the caller's host rows on the device (grown on demand)
+  int64_t prow_cap = 0;
+  int* d_rowsrc = nullptr;     // fa_llm_prefill_rows: row codes of one forward
   std::vector<int> h_tlfr, h_tgt, h_ctclen;
 
   // decoder
@@ -209,6 +213,7 @@ struct Engine {
   }
   ~Engine() {
     if (comm_buf) hipFree(comm_buf);
+    if (d_prow) hipFree(d_prow);
     for (auto& l : enc_lanes)
       if (l.s) hipStreamSynchronize(l.s);
     if (stream) hipStreamSynchronize(stream);
@@ -765,6 +770,7 @@ struct Engine {
     FA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_hist), (size_t)lc.max_seqs * hist_max * 4, hipHostMallocDefault));
     FA_HIP(hipEventCreateWithFlags(&ev_gen, hipEventDisableTiming));
     d_ids = alloc<int>(m_max);
+    d_rowsrc = alloc<int>(pf_max);
     d_samp = alloc<SampleParams>(1);
     attn_wk.max_tokens = pf_max;
     attn_wk.max_split_tokens = m_max;
@@ -1012,6 +1018,7 @@ struct Engine {
     h_ctclen = cl;
     last_batch = batch;
     last_tstride = tl_max;  // clip b's rows start at b tl_max
+    ++enc_gen;
   }
 
   void encode_device(const float* pcm, const int64_t* n_samples, int batch, int64_t stride) {
@@ -1039,6 +1046,7 @@ struct Engine {
     const int rows = batch * ts;
     last_batch = batch;
     last_tstride = ts;
+    ++enc_gen;
     // the per-clip lengths go up from pinned host memory owned by the engine (one region per encode lane), so no
     // copy depends on when the runtime reads a pageable source (the lane loop reuses the host vectors at once)
     int64_t* hm = meta_region();
@@ -1108,6 +1116,7 @@ struct Engine {
     FA_REQUIRE(T >= 1 && T <= tl_max, "fa_ctc_head: T out of range (1 .. the T_lfr of max_samples)");
     const int d = ec.d_model;
     last_batch = 0;
+    ++enc_gen;
     if (enc_fp16) prepare_fp16();
     else if (enc_gemm) prepare_bf3();
     int32_t* hm32 = reinterpret_cast<int32_t*>(meta_region() + max_batch);
@@ -1394,9 +1403,33 @@ struct Engine {
   // prompt's arithmetic is then the same alone and in a row-local batch); above, the tiled forward (query-tiled
   // attention, tiled GEMMs), which is faster there (scripts/prof_prefill_long.py: 2000 rows 19.8 vs 32.4 ms; 512 / 1024
   // rows 5.5 / 12.4 ms row-local vs 11.0 / 13.4 tiled; 1536 rows row-local 21.5 ms)
-  void prefill_one(int seq, const float* embd, int n_tokens, int32_t* tok_out, float* logits_out) {
+  // where a prefill's input rows come from: a host array [rows, n_embd] (fa_llm_prefill / _batch), or row codes
+  // (fa_llm_prefill_rows: the caller's rows already in d_prow, or adaptor rows of the last encode)
+  struct PromptSrc {
+    const float* embd = nullptr;
+    const int32_t* codes = nullptr;
+  };
+  // rows [off, off + n) of each part, back to back into lx
+  void load_prompt_rows(const PromptSrc& src, const std::vector<std::pair<int64_t, int>>& parts) {
     const int E = lc.n_embd;
-    FA_HIP(hipMemcpyAsync(lx, embd, (size_t)n_tokens * E * 4, hipMemcpyHostToDevice, stream));
+    if (src.embd) {
+      int64_t r = 0;
+      for (const auto& p : parts) {
+        FA_HIP(hipMemcpyAsync(lx + r * E, src.embd + p.first * E, (size_t)p.second * E * 4, hipMemcpyHostToDevice,
+                              stream));
+        r += p.second;
+      }
+      return;
+    }
+    std::vector<int32_t> c;
+    for (const auto& p : parts) c.insert(c.end(), src.codes + p.first, src.codes + p.first + p.second);
+    FA_REQUIRE((int64_t)c.size() <= pf_max, "prompt rows exceed the row capacity");
+    FA_HIP(hipMemcpyAsync(d_rowsrc, c.data(), c.size() * 4, hipMemcpyHostToDevice, stream));
+    fa::prompt_rows(d_prow, ad, last_tstride, d_rowsrc, (int)c.size(), E, lx, stream);
+  }
+
+  void prefill_one(int seq, const PromptSrc& src, int64_t off, int n_tokens, int32_t* tok_out, float* logits_out) {
+    load_prompt_rows(src, {{off, n_tokens}});
     std::vector<int> sq(n_tokens, seq), ps(n_tokens);
     for (int i = 0; i < n_tokens; ++i) ps[i] = n_past[seq] + i;
     FA_HIP(hipMemcpyAsync(d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, stream));
@@ -1978,35 +2011,36 @@ int fa_llm_prefill(fa_engine* h, int32_t seq, const float* embd, int32_t n_token
   FA_REQUIRE(seq >= 0 && seq < e->lc.max_seqs, "seq out of range");
   FA_REQUIRE(n_tokens >= 1 && e->n_past[seq] + n_tokens <= e->lc.n_ctx, "prefill exceeds n_ctx");
   e->set_sampling(s);
-  e->prefill_one(seq, embd, n_tokens, tok_out, logits_out);
+  Engine::PromptSrc src;
+  src.embd = embd;
+  e->prefill_one(seq, src, 0, n_tokens, tok_out, logits_out);
   FA_API_END
 }
 
-int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, const float* embd, const int32_t* n_tokens,
-                         const fa_sampling* s, int32_t* tok_out) {
-  FA_API_BEGIN
-  Engine* e = h->e;
+static void check_prefill_batch(Engine* e, const int32_t* seqs, int32_t n_seqs, const int32_t* n_tokens) {
   FA_REQUIRE(!e->gen_pending, "a generate call is in flight (fa_llm_generate_end first)");
   FA_REQUIRE(n_seqs >= 1 && n_seqs <= e->lc.max_seqs, "prefill batch: n_seqs out of range");
-  const int E = e->lc.n_embd;
   std::vector<char> seen(e->lc.max_seqs, 0);
-  std::vector<int64_t> off(n_seqs + 1, 0);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = seqs[i];
     FA_REQUIRE(q >= 0 && q < e->lc.max_seqs && !seen[q], "prefill batch: sequence ids must be distinct and in range");
     seen[q] = 1;
     FA_REQUIRE(n_tokens[i] >= 1 && n_tokens[i] <= e->pf_max && e->n_past[q] + n_tokens[i] <= e->lc.n_ctx,
                "prefill batch: prompt exceeds n_ctx or the row capacity");
-    off[i + 1] = off[i] + n_tokens[i];
   }
-  e->set_sampling(s);
+}
+
+static void prefill_batch(Engine* e, const int32_t* seqs, int32_t n_seqs, const Engine::PromptSrc& src,
+                          const int32_t* n_tokens, int32_t* tok_out) {
+  std::vector<int64_t> off(n_seqs + 1, 0);
+  for (int i = 0; i < n_seqs; ++i) off[i + 1] = off[i] + n_tokens[i];
   // within the invariant width the batch is row-local: every prompt gets exactly its fa_llm_prefill arithmetic (the
   // reference prefills every segment alone). A prompt above pf_rl_max rows gets the tiled forward when alone, so it is
   // prefilled alone here too.
   const bool rl = n_seqs <= e->invariant_width();
   std::vector<int> rest;
   for (int i = 0; i < n_seqs; ++i) {
-    if (rl && n_tokens[i] > e->pf_rl_max) e->prefill_one(seqs[i], embd + off[i] * E, n_tokens[i], tok_out ? tok_out + i : nullptr, nullptr);
+    if (rl && n_tokens[i] > e->pf_rl_max) e->prefill_one(seqs[i], src, off[i], n_tokens[i], tok_out ? tok_out + i : nullptr, nullptr);
     else rest.push_back(i);
   }
   e->pf_row_local = rl;
@@ -2017,10 +2051,10 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     while (i1 < rest.size() && rows + n_tokens[rest[i1]] <= e->pf_max) rows += n_tokens[rest[i1++]];
     const int n = (int)(i1 - i0);
     std::vector<int> sq(rows), ps(rows), last(n), lseq(n), lpos(n);
+    std::vector<std::pair<int64_t, int>> parts;
     for (size_t k = i0, r = 0; k < i1; ++k) {
       const int i = rest[k];
-      FA_HIP(hipMemcpyAsync(e->lx + (size_t)r * E, embd + off[i] * E, (size_t)n_tokens[i] * E * 4, hipMemcpyHostToDevice,
-                            e->stream));
+      parts.emplace_back(off[i], n_tokens[i]);
       for (int t = 0; t < n_tokens[i]; ++t, ++r) {
         sq[r] = seqs[i];
         ps[r] = e->n_past[seqs[i]] + t;
@@ -2029,6 +2063,7 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
       lseq[k - i0] = seqs[i];
       lpos[k - i0] = ps[r - 1];
     }
+    e->load_prompt_rows(src, parts);
     FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
@@ -2059,6 +2094,63 @@ int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, cons
     i0 = i1;
   }
   e->pf_row_local = false;
+}
+
+int fa_llm_prefill_batch(fa_engine* h, const int32_t* seqs, int32_t n_seqs, const float* embd, const int32_t* n_tokens,
+                         const fa_sampling* s, int32_t* tok_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  check_prefill_batch(e, seqs, n_seqs, n_tokens);
+  e->set_sampling(s);
+  Engine::PromptSrc src;
+  src.embd = embd;
+  prefill_batch(e, seqs, n_seqs, src, n_tokens, tok_out);
+  FA_API_END
+}
+
+int fa_encode_generation(fa_engine* h, int64_t* gen_out) {
+  FA_API_BEGIN
+  FA_REQUIRE(gen_out, "fa_encode_generation args");
+  *gen_out = h->e->last_batch > 0 ? h->e->enc_gen : -1;
+  FA_API_END
+}
+
+int fa_llm_prefill_rows(fa_engine* h, const int32_t* seqs, int32_t n_seqs, const float* host_rows, int32_t n_host_rows,
+                        const int32_t* row_src, const int32_t* n_tokens, int64_t enc_gen, const fa_sampling* s,
+                        int32_t* tok_out) {
+  FA_API_BEGIN
+  Engine* e = h->e;
+  FA_REQUIRE(row_src && n_tokens && n_host_rows >= 0 && (host_rows || n_host_rows == 0), "fa_llm_prefill_rows args");
+  check_prefill_batch(e, seqs, n_seqs, n_tokens);
+  const int E = e->lc.n_embd;
+  int64_t total = 0;
+  for (int i = 0; i < n_seqs; ++i) total += n_tokens[i];
+  for (int64_t r = 0; r < total; ++r) {
+    const int32_t c = row_src[r];
+    if (c >= 0) {
+      FA_REQUIRE(c < n_host_rows, "fa_llm_prefill_rows: host row index out of range");
+    } else {
+      const int v = -1 - c, b = v >> 16, t = v & 0xffff;
+      FA_REQUIRE(e->last_batch > 0 && enc_gen == e->enc_gen,
+                 "fa_llm_prefill_rows: the adaptor rows of that encode are gone (another encode or CTC-head call ran)");
+      FA_REQUIRE(e->ec.d_llm == E, "fa_llm_prefill_rows: adaptor width != n_embd");
+      FA_REQUIRE(b < e->last_batch && t < e->h_tgt[b], "fa_llm_prefill_rows: audio row out of range");
+    }
+  }
+  if (n_host_rows > e->prow_cap) {
+    if (e->d_prow) FA_HIP(hipFree(e->d_prow));
+    e->d_prow = nullptr;
+    e->prow_cap = 0;
+    FA_HIP(hipMalloc(&e->d_prow, (size_t)n_host_rows * E * 4));
+    e->prow_cap = n_host_rows;
+  }
+  if (n_host_rows > 0)
+    FA_HIP(hipMemcpyAsync(e->d_prow, host_rows, (size_t)n_host_rows * E * 4, hipMemcpyHostToDevice, e->stream));
+  e->set_sampling(s);
+  Engine::PromptSrc src;
+  src.codes = row_src;
+  if (n_seqs == 1) e->prefill_one(seqs[0], src, 0, n_tokens[0], tok_out, nullptr);  // fa_llm_prefill's path
+  else prefill_batch(e, seqs, n_seqs, src, n_tokens, tok_out);
   FA_API_END
 }
 

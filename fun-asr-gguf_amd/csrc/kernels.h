@@ -213,6 +213,8 @@ extern int g_ffn_pair_min_m;  // small decode batches from this width: two token
 void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);
 // dst[i] = src[rows[i]] (n rows of E floats; row stride E both sides)
 void gather_rows(const float* src, const int* rows, int n, int E, float* dst, hipStream_t s);
+void prompt_rows(const float* host, const float* audio, int64_t ts, const int* codes, int n, int E, float* dst,
+                 hipStream_t s);
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s);
 // Decode-step tail fused into the sampler: embedding row of the sampled token -> x (the next step's input), and

@@ -2187,6 +2187,30 @@ void gather_rows(const float* src, const int* rows, int n, int E, float* dst, hi
   if (n > 0) hipLaunchKernelGGL(k_gather_rows, dim3(1, n), dim3(256), 0, s, src, rows, E, dst);
 }
 
+// prompt rows assembled on the device (fa_llm_prefill_rows): code >= 0 is row `code` of the caller's rows (uploaded);
+// code < 0 an adaptor output row of the last encode: v = -1 - code, clip v >> 16, row v & 0xffff (clip b's rows start
+// at row b * ts). A verbatim copy either way, so the rows equal the host concatenation bit for bit.
+__global__ void k_prompt_rows(const float* __restrict__ host, const float* __restrict__ audio, int64_t ts,
+                              const int* __restrict__ codes, int E, float* __restrict__ dst) {
+  const int m = blockIdx.y;
+  const int c = codes[m];
+  const float* src;
+  if (c >= 0) {
+    src = host + (int64_t)c * E;
+  } else {
+    const int v = -1 - c;
+    src = audio + ((int64_t)(v >> 16) * ts + (v & 0xffff)) * E;
+  }
+  for (int i = threadIdx.x * 4; i < E; i += blockDim.x * 4)
+    *reinterpret_cast<float4*>(dst + (int64_t)m * E + i) = *reinterpret_cast<const float4*>(src + i);
+}
+
+void prompt_rows(const float* host, const float* audio, int64_t ts, const int* codes, int n, int E, float* dst,
+                 hipStream_t s) {
+  FA_REQUIRE(E % 4 == 0, "prompt_rows: E % 4");
+  if (n > 0) hipLaunchKernelGGL(k_prompt_rows, dim3(1, n), dim3(256), 0, s, host, audio, ts, codes, E, dst);
+}
+
 void embed_rows(const int8_t* qs, const __half* d, const int* ids, int n, int E, int fp16_round, float* out,
                 hipStream_t s) {
   hipLaunchKernelGGL(k_embed, dim3(cdiv(E, 256), n), dim3(256), 0, s, qs, d, ids, n, E, fp16_round, out);

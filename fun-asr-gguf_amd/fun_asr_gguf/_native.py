@@ -23,7 +23,7 @@ EXPORTS = [
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
     "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head", "fa_set_tensor_u8dq", "fa_set_ctc_int8",
     "fa_ctc_int8_active", "fa_comm_unique_id", "fa_comm_init", "fa_comm_allgather_sizes", "fa_comm_allgather_bytes",
-    "fa_comm_destroy",
+    "fa_comm_destroy", "fa_llm_prefill_rows", "fa_encode_generation",
 ]
 
 
@@ -99,6 +99,8 @@ def load():
     lib.fa_llm_generate_begin.argtypes = [P, P, I32, I32, ctypes.POINTER(Sampling)]
     lib.fa_llm_generate_end.argtypes = [P, P]
     lib.fa_llm_prefill_batch.argtypes = [P, P, I32, P, P, ctypes.POINTER(Sampling), P]
+    lib.fa_llm_prefill_rows.argtypes = [P, P, I32, P, I32, P, P, I64, ctypes.POINTER(Sampling), P]
+    lib.fa_encode_generation.argtypes = [P, P]
     lib.fa_llm_logits.argtypes = [P, I32, P]
     lib.fa_llm_set_token.argtypes = [P, I32, I32]
     lib.fa_llm_invariant_width.argtypes = [P, ctypes.c_void_p]
@@ -335,7 +337,7 @@ class Engine:
             _check(self.lib.fa_encode(self.h, _ptr(pcm), _ptr(ns), B, stride, _ptr(emb), tgt_stride, _ptr(ids),
                                       ids_stride, _ptr(tl), _ptr(tg), _ptr(enc)), "fa_encode")
         out = dict(audio_embd=[emb[b, :tg[b]] for b in range(B)], ctc_ids=[ids[b, :tl[b]] for b in range(B)],
-                   t_lfr=tl, target_len=tg)
+                   t_lfr=tl, target_len=tg, enc_gen=self.encode_generation())
         if want_enc:
             out["enc"] = [enc[b, :tl[b]] for b in range(B)]
         if debug_lfr:
@@ -345,6 +347,12 @@ class Engine:
             out["lfr_embedded"] = lfr[:t0]
             _check(self.lib.fa_set_debug(self.h, 0), "fa_set_debug")
         return out
+
+    def encode_generation(self):
+        """Generation of the adaptor rows the last encode left in HBM (-1: none held); fa_encode_generation."""
+        g = ctypes.c_int64()
+        _check(self.lib.fa_encode_generation(self.h, ctypes.byref(g)), "fa_encode_generation")
+        return g.value
 
     def ctc_head(self, enc):
         """The CTC graph alone over encoder rows enc [T, d_model] -> argmax ids [T] int32 (fa_ctc_head)."""
@@ -393,6 +401,40 @@ class Engine:
         s = self._sampling(**samp)
         _check(self.lib.fa_llm_prefill_batch(self.h, _ptr(seqs), len(seqs), _ptr(e), _ptr(n), ctypes.byref(s), _ptr(tok)),
                "fa_llm_prefill_batch")
+        return tok.tolist()
+
+    def llm_prefill_rows(self, seqs, prompts, **samp):
+        """llm_prefill (one prompt) / llm_prefill_batch with every prompt's audio rows read where the last encode
+        left them (fa_llm_prefill_rows). prompts: objects with .pre / .suf (host rows [n, n_embd]), .clip (the clip's
+        index in that encode), .n_audio and .enc_gen (core/decoder.PromptRows). The distinct prefix / suffix arrays
+        are uploaded once. -> first tokens, one per sequence."""
+        seqs = np.ascontiguousarray(seqs, dtype=np.int32)
+        blocks, offs, codes = [], {}, []
+        gen = None
+        for p in prompts:
+            part = []
+            for arr in (p.pre, None, p.suf):
+                if arr is None:
+                    part.append(-1 - ((p.clip << 16) | np.arange(p.n_audio, dtype=np.int32)))
+                    continue
+                if len(arr) == 0:
+                    continue
+                k = id(arr)
+                if k not in offs:
+                    offs[k] = sum(len(b) for b in blocks)
+                    blocks.append(arr)
+                part.append(offs[k] + np.arange(len(arr), dtype=np.int32))
+            codes.append(np.concatenate(part).astype(np.int32))
+            gen = p.enc_gen if gen is None else gen
+            assert p.enc_gen == gen, "prompts of different encodes"
+        n = np.array([len(c) for c in codes], np.int32)
+        rs = np.ascontiguousarray(np.concatenate(codes))
+        host = np.ascontiguousarray(np.concatenate(blocks, 0), np.float32) if blocks else None
+        tok = np.zeros(len(seqs), np.int32)
+        s = self._sampling(**samp)
+        _check(self.lib.fa_llm_prefill_rows(self.h, _ptr(seqs), len(seqs), _ptr(host), 0 if host is None else len(host),
+                                            _ptr(rs), _ptr(n), int(gen), ctypes.byref(s), _ptr(tok)),
+               "fa_llm_prefill_rows")
         return tok.tolist()
 
     def llm_generate(self, seqs, n_steps, **samp):

@@ -89,11 +89,44 @@ def invariant_width(eng):
     return f() if f is not None else 1
 
 
+class PromptRows:
+    """One prompt, [prefix rows | audio rows | suffix rows], whose audio rows are the adaptor output of clip `clip` of
+    the engine's encode generation `enc_gen`, still in HBM. The reference concatenates the three on the host
+    (core/decoder.py:199: np.concatenate([p_embd, audio_embd.astype(np.float32), s_embd])); prefill_group has the
+    engine assemble them on the device instead (fa_llm_prefill_rows: no host concatenation, no upload of the audio
+    rows), bit for bit the same rows. np.asarray(prompt) is that concatenation (the host path, e.g. after another
+    encode replaced the rows)."""
+    __slots__ = ("pre", "audio", "suf", "clip", "enc_gen")
+
+    def __init__(self, pre, audio, suf, clip, enc_gen):
+        self.pre, self.audio, self.suf, self.clip, self.enc_gen = pre, audio, suf, int(clip), int(enc_gen)
+
+    @property
+    def n_audio(self):
+        return len(self.audio)
+
+    @property
+    def shape(self):
+        return (len(self.pre) + len(self.audio) + len(self.suf), self.audio.shape[1])
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __array__(self, dtype=None, copy=None):
+        a = np.concatenate([self.pre, np.asarray(self.audio, np.float32), self.suf], 0)
+        return a if dtype is None else a.astype(dtype, copy=False)
+
+
 def prefill_group(eng, seqs, embds, samp):
     """Prefill `embds` into slots `seqs` -> first tokens. One prompt: llama_decode of its batch. Several: their
     prompts share forwards (one weight pass per forward, fa_llm_prefill_batch); within the engine's invariant width
     that batch is row-local, so every sequence gets exactly its single-sequence prefill (the reference decodes every
-    segment alone, core/decoder.py:70-123); wider groups agree to the q8_0 noise floor."""
+    segment alone, core/decoder.py:70-123); wider groups agree to the q8_0 noise floor. PromptRows of the encode the
+    engine still holds are assembled on the device (fa_llm_prefill_rows), with the same results."""
+    if all(isinstance(e, PromptRows) for e in embds) and hasattr(eng, "llm_prefill_rows") \
+            and len({e.enc_gen for e in embds}) == 1 and embds[0].enc_gen == eng.encode_generation():
+        return eng.llm_prefill_rows(list(seqs), embds, **samp)
+    embds = [np.asarray(e, np.float32) for e in embds]
     if len(embds) == 1:
         return [eng.llm_prefill(seqs[0], embds[0], **samp)]
     return eng.llm_prefill_batch(list(seqs), embds, **samp)
@@ -268,10 +301,14 @@ class StreamDecoder:
         # 3. prompt
         t = time.perf_counter()
         jobs = []
+        gen = out.get("enc_gen", -1)
         for b in range(B):
             pe, se, n_p, n_s, _ = m.prompt_builder.build_prompt(hotwords[b], language, context)
-            jobs.append(dict(embd=np.concatenate([pe, out["audio_embd"][b].astype(np.float32), se], 0),
-                             ctc_results=ctc_results[b], hotwords=hotwords[b], n_p=n_p, n_s=n_s,
+            # the prompt rows stay unassembled while the engine holds this encode (PromptRows); else the reference's
+            # host concatenation
+            embd = PromptRows(pe, out["audio_embd"][b], se, b, gen) if gen >= 0 else \
+                np.concatenate([pe, out["audio_embd"][b].astype(np.float32), se], 0)
+            jobs.append(dict(embd=embd, ctc_results=ctc_results[b], hotwords=hotwords[b], n_p=n_p, n_s=n_s,
                              audio_embd=out["audio_embd"][b], timings=timings[b]))
         dt = time.perf_counter() - t
         for tm in timings:

@@ -170,6 +170,19 @@ int fa_llm_prefill(fa_engine* e, int32_t seq, const float* embd, int32_t n_token
  * per-sequence llama_decode of a prompt batch (decoder.py:70-80 run per stream). */
 int fa_llm_prefill_batch(fa_engine* e, const int32_t* seqs, int32_t n_seqs, const float* embd, const int32_t* n_tokens,
                          const fa_sampling* s, int32_t* tok_out);
+/* fa_llm_prefill / fa_llm_prefill_batch with the prompt rows assembled on the device instead of uploaded: the
+ * reference concatenates [prefix rows | audio_embd | suffix rows] on the host (core/decoder.py:199) and hands the
+ * result to llama_decode (decoder.py:73-77); here the audio rows stay where the last encode left them. row_src holds
+ * one code per prompt row (sum n_tokens, prompts back to back): code >= 0 = row `code` of host_rows [n_host_rows,
+ * n_embd] (the caller's prefix / suffix rows, uploaded once per call); code < 0 = adaptor output row t of clip b of
+ * the last encode, code = -1 - (b << 16 | t) (t < target_len[b]). enc_gen = fa_encode_generation() right after that
+ * encode: the call fails (FA_ERR_ARG) if another encode or CTC-head call has run since. The rows equal the host
+ * concatenation bit for bit, so the results are fa_llm_prefill's (n_seqs == 1) / fa_llm_prefill_batch's. */
+int fa_llm_prefill_rows(fa_engine* e, const int32_t* seqs, int32_t n_seqs, const float* host_rows, int32_t n_host_rows,
+                        const int32_t* row_src, const int32_t* n_tokens, int64_t enc_gen, const fa_sampling* s,
+                        int32_t* tok_out);
+/* Generation of the last encode's outputs (-1 if none are held, e.g. after fa_ctc_head). */
+int fa_encode_generation(fa_engine* e, int64_t* gen_out);
 /* Run n_steps decode steps for n_seqs sequences (distinct ids) in one continuous batch: each step feeds
  * every sequence's last sampled token at its next position and samples the next one on device
  * (decoder.py:91-98). tokens_out [n_seqs, n_steps]. No host round trip inside the call. */

@@ -577,3 +577,61 @@ def test_long_prompt_prefilled_alone_in_row_local_batch(monkeypatch):
             assert int(nxt[s]) == single[s][2] and np.array_equal(e.llm_logits(s), single[s][3]), f"prompt {s}"
     finally:
         e.close()
+
+
+def test_prefill_rows_assembled_on_device_equal_host_prompts(eng):
+    """fa_llm_prefill_rows (prompt rows assembled in HBM from the caller's prefix / suffix rows and the last encode's
+    adaptor rows, core/decoder.PromptRows) against the reference's host concatenation (core/decoder.py:199) through
+    fa_llm_prefill / fa_llm_prefill_batch: first tokens and last-row logits bit-identical for one prompt, a row-local
+    batch of 3 and a tiled batch of 8 (above the invariant width); a later encode invalidates the rows (loud failure,
+    and prefill_group falls back to the host rows)."""
+    from fun_asr_gguf.core.decoder import PromptRows, prefill_group
+    from fun_asr_gguf.synthetic import synth_audio
+    rng = np.random.default_rng(77)
+    clips = [synth_audio(int(s * SR), 700 + i) for i, s in enumerate((9.5, 4.2, 7.0, 3.1, 5.5, 6.6, 2.2, 8.8))]
+    pre = [eng.embd_rows(rng.integers(0, 151933, 73).astype(np.int32)) for _ in range(2)]
+    suf = eng.embd_rows(rng.integers(0, 151933, 5).astype(np.int32))
+
+    def run(n):
+        out = eng.encode(clips[:n])
+        gen = out["enc_gen"]
+        assert gen >= 0 and gen == eng.encode_generation()
+        rows = [PromptRows(pre[b % 2], out["audio_embd"][b], suf, b, gen) for b in range(n)]
+        host = [np.concatenate([pre[b % 2], out["audio_embd"][b], suf], 0) for b in range(n)]
+        assert all(np.array_equal(np.asarray(r), h) for r, h in zip(rows, host))
+        seqs = list(range(n))
+        for s in seqs:
+            eng.llm_reset(s)
+        if n == 1:
+            t_host, lg_host = eng.llm_prefill(0, host[0], want_logits=True)
+            t_host, lg_host = [t_host], [lg_host]
+        else:
+            t_host = eng.llm_prefill_batch(seqs, host)
+            lg_host = [eng.llm_logits(s) for s in seqs]
+        for s in seqs:
+            eng.llm_reset(s)
+        t_dev = eng.llm_prefill_rows(seqs, rows)
+        assert [int(t) for t in t_dev] == [int(t) for t in t_host], f"batch {n}: first tokens"
+        for s in seqs:
+            assert np.array_equal(eng.llm_logits(s), lg_host[s]), f"batch {n}: logits of prompt {s}"
+        return rows
+
+    run(1)
+    run(3)
+    rows = run(8)
+    eng.encode(clips[:1])  # replaces the adaptor rows the PromptRows point at
+    for s in range(8):
+        eng.llm_reset(s)
+    with pytest.raises(RuntimeError, match="adaptor rows"):
+        eng.llm_prefill_rows(list(range(8)), rows)
+    for s in range(8):
+        eng.llm_reset(s)
+    t_fb = prefill_group(eng, list(range(8)), rows, dict(temperature=0.0))  # host fallback
+    for s in range(8):
+        eng.llm_reset(s)
+    t_ref = eng.llm_prefill_batch(list(range(8)), [np.asarray(r) for r in rows])
+    assert [int(t) for t in t_fb] == [int(t) for t in t_ref]
+    bad = PromptRows(pre[0], rows[0].audio, suf, 5, eng.encode_generation())  # clip 5 of a 1-clip encode
+    eng.llm_reset(0)
+    with pytest.raises(RuntimeError, match="out of range"):
+        eng.llm_prefill_rows([0], [bad])
