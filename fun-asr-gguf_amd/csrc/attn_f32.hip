@@ -378,7 +378,9 @@ __device__ __forceinline__ f16x4a ld_tr4h(const _Float16* p) {
 // scores after the dot), and O^T += V^T . P^T is two (P^T split into f16 hi + lo in registers, V^T exact): the
 // attention stays f32 arithmetic on fp16 inputs with its output rounded to fp16, the oracle's contract
 // (oracle/encoder_fp16.py); 3 MFMAs per 16 keys x 16 dims instead of the exact-f32 form's 8 x 64 cycles
-template <int D, int P = 3>
+// S = 1: write-after-barrier staging (as k_gemm_bf3_256 S = 1): the registers holding key tile kt + 1, loaded a whole
+// step earlier, go to the free stage at the top of step kt and then take tile kt + 2's loads. Same MFMA order.
+template <int D, int P = 3, int S = 0>
 __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
@@ -433,11 +435,17 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
   if (kt0 < kt1) {
     attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt0, pk, pv);
     attn3_store_tile<D, P>(lds, pk, pv);
+    if (S == 1 && kt0 + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt0 + 1, pk, pv);
   }
   __syncthreads();
   for (int kt = kt0; kt < kt1; ++kt) {
     const int stage = (kt - kt0) & 1;
-    if (kt + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 1, pk, pv);  // in flight
+    if constexpr (S == 1) {
+      if (kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
+      if (kt + 2 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 2, pk, pv);  // in flight
+    } else {
+      if (kt + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 1, pk, pv);  // in flight
+    }
     const __bf16* kh_ = reinterpret_cast<const __bf16*>(lds + stage * L::STAGE);
     const float* vs_ = lds + stage * L::STAGE + L::VOFF;
     const int k0 = kt * AK;
@@ -541,7 +549,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o[i], 0, 0, 0);
       }
     }
-    if (kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
+    if (S == 0 && kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
     __syncthreads();
   }
   attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, P == 1 ? 1 : 0,
@@ -550,6 +558,25 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
 
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
 int g_attn_f16_mfma = 1;          // fp16 graph attention on f16 MFMAs (k_attn_bf3<D, 1>); 0: exact f32 + rounding (A/B)
+int g_attn_wab = 0;               // k_attn_bf3 write-after-barrier staging (S = 1; FUNASR_ATTN_WAB)
+
+template <int D, int P>
+static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const float* K, const float* V, int64_t ldq,
+                            int64_t ldk, int64_t ldv, float* O, int64_t ldo, int t_stride, const int* lens, float scale,
+                            int KS, const AttnF32Work& wk) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<D, P, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<D>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_attn_bf3<D, P, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<D>::BYTES);
+    attr = true;
+  }
+  if (g_attn_wab)
+    hipLaunchKernelGGL((k_attn_bf3<D, P, 1>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+  else
+    hipLaunchKernelGGL((k_attn_bf3<D, P, 0>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
+                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+}
 
 int attn_f32_splits(int batch, int t_stride, int n_heads) {
   if (g_attn_f32_force_splits > 0) return g_attn_f32_force_splits;
@@ -576,30 +603,18 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<128>::BYTES);
     (void)hipFuncSetAttribute((const void*)k_attn_f32<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<64>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_attn_bf3<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<128>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_attn_bf3<64>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<64>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_attn_bf3<128, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<128>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_attn_bf3<64, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<64>::BYTES);
     attr_set = true;
   }
   if (r16 && g_attn_f16_mfma) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
-    if (head_dim == 128)
-      hipLaunchKernelGGL((k_attn_bf3<128, 1>), grid, dim3(256), AttnLds3<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                         t_stride, lens, scale, KS, wk.part, wk.cnt);
-    else
-      hipLaunchKernelGGL((k_attn_bf3<64, 1>), grid, dim3(256), AttnLds3<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    if (head_dim == 128) launch_attn_bf3<128, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
+    else launch_attn_bf3<64, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
     return;
   }
   if (bf3 && !r16) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
-    if (head_dim == 128)
-      hipLaunchKernelGGL(k_attn_bf3<128>, grid, dim3(256), AttnLds3<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                         t_stride, lens, scale, KS, wk.part, wk.cnt);
-    else
-      hipLaunchKernelGGL(k_attn_bf3<64>, grid, dim3(256), AttnLds3<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                         t_stride, lens, scale, KS, wk.part, wk.cnt);
+    if (head_dim == 128) launch_attn_bf3<128, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
+    else launch_attn_bf3<64, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
     return;
   }
   if (head_dim == 128) {

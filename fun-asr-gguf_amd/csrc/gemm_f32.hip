@@ -645,9 +645,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 int g_gemm_bf3_pf = 2;     // few-tile bf16x3 shapes: global loads PF k-steps ahead (1 or 2; FUNASR_BF3_PF)
 int g_gemm_bf3_force = 0;  // microbenchmark hook: 1 = 64x64x32, 2 = 128x128x32, 3 = 64x64x64, 4 / 5 = 64x64x64 / x32 K halves,
-                           // 6 = 256x256x32, 7 = 128x64x32 K halves, 8 = 64x64 K quarters
+                           // 6 = 256x256x32, 7 = 128x64x32 K halves, 8 = 64x64 K quarters, 9 / 10 = 64x64x128
+                           // (10: K halves for fp16)
 int g_gemm_bf3_256 = 0;    // 256x256 tiles when a launch has at least this many (0 = off; FUNASR_BF3_256)
 int g_gemm_f16_b3 = 1;     // fp16 graph GEMMs on the k_gemm_bf3 kernel family (P = 1); 0: k_gemm_f16 (FUNASR_F16_GEMM, A/B)
+int g_gemm_bf3_256_s = 1;  // 256x256 / 128x128 tiles: 1 = write-after-barrier staging (FUNASR_BF3_256_S; A/B at
+                           // M = 32032, scripts/ubench/gemm_f32_bench sched: 272-328 vs 185-222 TF/s, bit-identical;
+                           // batch-32 encode 128.5-129.2 -> 109.7-109.9 ms)
+int g_gemm_f16_deep = 1;   // fp16 graph one-clip shapes on 128-deep stages (FUNASR_F16_DEEP)
 int g_gemm_bf3_kw4 = 0;    // few-tile shapes with K >= 2048 (one clip's ffn2): four K groups per block (FUNASR_BF3_KW4;
                            // A/B: ffn2 22.4 vs 23.7 us bf16x3, one-clip encode 10.43-10.63 vs 10.43-10.55 ms bf16x3,
                            // 8.68-8.74 vs 8.77-8.87 ms fp16: within run-to-run noise, not kept)
@@ -819,6 +824,18 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
       if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
       __syncthreads();
     }
+  } else if constexpr (PF == 3) {
+    // write-after-barrier (k_gemm_bf3_256 S = 1): tile kt + 1, loaded a whole step earlier, goes to the free stage at
+    // the top of step kt, then the same registers take tile kt + 2's loads
+    if (nk > 1) load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rh, rl, t);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
+      if (kt + 2 < nk)
+        load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 2) * KB, M, N, ke, ra, rh, rl, t);
+      compute(sh + cur * T::STAGE);
+      __syncthreads();
+    }
   } else {
     // set A (ra, rh, rl) carries the odd k-steps, set B the even ones from step 2 on; step j is loaded right after
     // step j - 2's set was stored, i.e. two compute steps before it is stored itself
@@ -904,7 +921,8 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
 // planes x 256 rows x 80 B = 160 KiB (fp16: 2 planes, 80 KiB).
 #ifndef B3B_VARIANT
 // A/B only (scripts/gpu_r3_g256b.sh, M = 32032): 1 = MFMA blocks at raised wave priority (275-325 TF/s), 2 = also the
-// next stage stored between the k halves (193-229 TF/s); 0 (292-330 TF/s) stays
+// next stage stored between the k halves (193-229 TF/s); 0 (292-330 TF/s) stays. Diagnostics (wrong results):
+// 3 = no global loads after the first stage (LDS reads + MFMAs only), 4 = no MFMAs (loads, stores, LDS reads only)
 #define B3B_VARIANT 0
 #endif
 constexpr int B3B_T = 512, B3B_BM = 256, B3B_BN = 256, B3B_KB = 32, B3B_LDK = B3B_KB + 8;
@@ -968,7 +986,10 @@ __device__ __forceinline__ void store_b3b(typename PrecB<P>::E* st, const float4
   }
 }
 
-template <class AL, class EPI, int P = 3>
+// S = 1: write-after-barrier staging (cdna_hip_programming.md T14): step kt first stores the registers holding tile
+// kt + 1 (loaded a whole step earlier) into the free stage, re-issues the loads of tile kt + 2 into the same registers,
+// then computes tile kt; S = 0 loads tile kt + 1 at the top of step kt and stores it after the compute. Same MFMA order.
+template <class AL, class EPI, int P = 3, int S = 0>
 __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename PrecB<P>::E* __restrict__ Wh,
                                                             const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw,
                                                             int M, int N, int K, EPI epi) {
@@ -993,11 +1014,18 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
   uint4 rh[B3B_NB], rl[B3B_NB];
   load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl, t);
   store_b3b<P>(sh, ra, rh, rl, t);
-  __syncthreads();
   const int nk = (K + B3B_KB - 1) / B3B_KB;
+  if (S == 1 && nk > 1) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, B3B_KB, M, N, K, ra, rh, rl, t);
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, (kt + 1) * B3B_KB, M, N, K, ra, rh, rl, t);
+    if constexpr (S == 1) {
+      if (kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
+      if (kt + 2 < nk) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, (kt + 2) * B3B_KB, M, N, K, ra, rh, rl, t);
+    }
+#if B3B_VARIANT != 3
+    if (S == 0 && kt + 1 < nk) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, (kt + 1) * B3B_KB, M, N, K, ra, rh, rl, t);
+#endif
     const E* stage = sh + cur * STAGE;
     const E* a = stage + (wr * 32 * WM + r) * LDK + 8 * h;
     const E* b = stage + OB + (wc * 32 * WN + r) * LDK + 8 * h;
@@ -1017,19 +1045,26 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
         ah[i] = *reinterpret_cast<const V8*>(a + 32 * i * LDK + 16 * kk);
         if constexpr (P == 3) alo[i] = *reinterpret_cast<const V8*>(a + B3B_PA + 32 * i * LDK + 16 * kk);
       }
-#if B3B_VARIANT >= 1
+#if B3B_VARIANT == 1 || B3B_VARIANT == 2
       __builtin_amdgcn_s_setprio(1);
 #endif
+#if B3B_VARIANT == 4
+#pragma unroll
+      for (int i = 0; i < WM; ++i) asm volatile("" ::"v"(ah[i]), "v"(alo[i]));
+#pragma unroll
+      for (int j = 0; j < WN; ++j) asm volatile("" ::"v"(bh[j]), "v"(blo[j]));
+#else
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j) mma_step<P>(acc[i][j], ah[i], alo[i], bh[j], blo[j]);
-#if B3B_VARIANT >= 1
+#endif
+#if B3B_VARIANT == 1 || B3B_VARIANT == 2
       __builtin_amdgcn_s_setprio(0);
 #endif
     }
-#if B3B_VARIANT != 2
-    if (kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
+#if B3B_VARIANT != 2 && B3B_VARIANT != 3
+    if (S == 0 && kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
 #endif
     __syncthreads();
   }
@@ -1040,20 +1075,27 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
   epi.finish(m0, n0, M, N, smem);
 }
 
-template <class AL, class EPI, int P = 3>
-static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
-                               hipStream_t s) {
+template <class AL, class EPI, int P, int S>
+static void launch_gemm_b3_256_s(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                                 hipStream_t s) {
   typedef typename PrecB<P>::E E;
-  FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3_256: K and ldw must be multiples of 8");
   static bool attr = false;
   if (!attr) {
-    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI, P>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI, P, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)B3BT<P>::LDS));
     attr = true;
   }
   const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
-  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P>), grid, dim3(B3B_T), B3BT<P>::LDS, s, al,
+  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P, S>), grid, dim3(B3B_T), B3BT<P>::LDS, s, al,
                      reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
+}
+
+template <class AL, class EPI, int P = 3>
+static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                               hipStream_t s) {
+  FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3_256: K and ldw must be multiples of 8");
+  if (g_gemm_bf3_256_s) launch_gemm_b3_256_s<AL, EPI, P, 1>(al, w, ldw, M, N, K, epi, s);
+  else launch_gemm_b3_256_s<AL, EPI, P, 0>(al, w, ldw, M, N, K, epi, s);
 }
 
 // microbenchmark helper: resident blocks per CU of the 128x128x32 bf16x3 kernel (linear epilogue), its dynamic LDS
@@ -1077,13 +1119,27 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   // 256x256 tiles while they still give most CUs a block (f == 6 forces them)
   if (f == 6 || (f == 0 && g_gemm_bf3_256 && (int64_t)cdiv(M, 256) * cdiv(N, 256) >= g_gemm_bf3_256))
     launch_gemm_b3_256<AL, EPI, P>(al, w, ldw, M, N, K, epi, s);
-  else if (big) launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
+  else if (big) {
+    if (g_gemm_bf3_256_s) launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 3, P>(al, w, ldw, M, N, K, epi, s);
+    else launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
+  }
+  // fp16 graph, one clip: 128-deep stages (half the k-steps; fp16 planes leave the LDS for them). q|k|v and ffn1 keep
+  // their per-element MFMA order (bit-identical to 64-deep stages); ffn2 also splits K in halves. scripts/ubench/
+  // gemm_f32_bench kscan, graph-timed: q|k|v 10.1 -> 9.8, ffn1 10.9 -> 10.3, ffn2 14.7 -> 13.8 us (bf16x3: slower)
+  else if (P == 1 && f == 0 && g_gemm_f16_deep && t64 > 256 && t64 <= 1024 && K % 128 == 0)
+    launch_gemm_b3<AL, EPI, 1, 1, 128, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
+  else if (P == 1 && f == 0 && g_gemm_f16_deep && t64 < 256 && K >= 2048 && K % 256 == 0)
+    launch_gemm_b3<AL, EPI, 1, 1, 128, P == 1 ? 2 : 1, 2, P>(al, w, ldw, M, N, K, epi, s);
   else if (f == 1) launch_gemm_b3<AL, EPI, 1, 1, 32, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
   // 256 < 64x64 tiles <= 1024 (one clip's q|k|v and ffn1: 384 / 512 tiles, i.e. 1.5-2 rounds of one 147-KiB block per
   // CU): 128x64 tiles, two K groups of 32-deep stages, loads two steps ahead -- one round of twice the work per block
   else if (f == 7 || (f == 0 && g_gemm_bf3_mid && t64 > 256 && t64 <= 1024 && K % 64 == 0))
     launch_gemm_b3<AL, EPI, 2, 1, 32, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
-  else if (f == 8 || (f == 0 && g_gemm_bf3_kw4 && t64 < 256 && K >= 2048 && K % 256 == 0)) {
+  else if (f == 9) launch_gemm_b3<AL, EPI, 1, 1, 128, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
+  else if (f == 10) {  // 128-deep stages in two K groups (fp16: 2 x 2 x 34 KiB of LDS; bf16x3 has no room for it)
+    if constexpr (P == 1) launch_gemm_b3<AL, EPI, 1, 1, 128, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
+    else launch_gemm_b3<AL, EPI, 1, 1, 128, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
+  } else if (f == 8 || (f == 0 && g_gemm_bf3_kw4 && t64 < 256 && K >= 2048 && K % 256 == 0)) {
     // 1024 threads: 16 waves per CU; P = 3 keeps 32-deep stages (4 groups x 2 stages x 20 KiB = 160 KiB)
     if constexpr (P == 1) launch_gemm_b3<AL, EPI, 1, 1, 64, 4, 2, P>(al, w, ldw, M, N, K, epi, s);
     else launch_gemm_b3<AL, EPI, 1, 1, 32, 4, 2, P>(al, w, ldw, M, N, K, epi, s);

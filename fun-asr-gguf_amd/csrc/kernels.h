@@ -34,6 +34,9 @@ struct GemmF32Work {
 extern int g_gemm_f32_split;  // 1 (default): K splits where the tiles leave the chip idle; 0: none
 extern int g_attn_f16_mfma;  // 1 (default): fp16-graph attention on f16 MFMAs; 0: exact f32 + fp16 rounding
 extern int g_gemm_f16_b3;  // 1 (default): fp16-graph GEMMs on the bf16x3 kernel family with one f16 plane; 0: k_gemm_f16
+extern int g_attn_wab;  // k_attn_bf3: 1 = write-after-barrier K/V staging
+extern int g_gemm_bf3_256_s;  // 256x256 tile: 1 = write-after-barrier staging
+extern int g_gemm_f16_deep;  // fp16 one-clip GEMMs on 128-deep stages (default 1)
 extern int g_gemm_bf3_kw4;  // 1: four K groups per block for few-tile K >= 2048 shapes (FUNASR_BF3_KW4)
 extern int g_gemm_bf3_mid;  // 1: 128x64 tiles for one clip's 256-1024-tile GEMM shapes (A/B, default 0)
 // bf16x3 split of an f32 weight (raw bf16 bits): hi = bf16_rn(w), lo = bf16_rn(w - hi), planes laid out as w

@@ -10,3 +10,11 @@ timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --c3
 python3 -c "
 import json; d=json.loads(open('gpurun_out/b_rows.json').read().strip().splitlines()[-1])
 print('C2', d['value'], d.get('stage_ms')); c3=d.get('c3', {}); print('C3', c3.get('value'), c3.get('ms_per_step'), c3.get('stage_ms'))"
+# 256x256 bf16x3 tile diagnostics at M = 32032: default / no global loads / no MFMAs
+for v in "" _v3 _v4; do
+  timeout -k 10 300 scripts/ubench/gemm_f32_bench$v > gpurun_out/g256diag$v.txt 2>&1 || { tail -5 gpurun_out/g256diag$v.txt; exit 1; }
+  echo "== gemm$v"; grep -E "M=32032" gpurun_out/g256diag$v.txt | sed 's/.*bf3 128x128x32/bf3 128x128x32/'
+done
+timeout -k 10 120 scripts/ubench/gemm_f32_bench kscan > gpurun_out/kscan.txt 2>&1 || { tail -5 gpurun_out/kscan.txt; exit 1; }
+cat gpurun_out/kscan.txt
+bash scripts/gpu_r4_exp6.sh

@@ -9,6 +9,7 @@
 namespace fa {
 extern int g_gemm_f32_force;
 extern int g_gemm_bf3_force;
+extern int g_gemm_bf3_256_s;
 int gemm_bf3_occupancy_128();
 extern int g_gemm_ks_force;
 void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
@@ -81,8 +82,9 @@ int main(int argc, char** argv) {
   WSplit wb; wb.hi = Wh; wb.lo = Wl;
   for (int sk = 0; sk < 3; ++sk) {  // bf16x3 spot checks (M=100 N=96 K=72; M=70 N=64 K=2048; K halves M=100 N=96 K=256)
     const int M = sk == 1 ? 70 : 100, N = sk == 1 ? 64 : 96, K = sk == 1 ? 2048 : sk == 2 ? 256 : 72;
-    for (int v : {1, 2, 3, 4, 5, 6, 8}) {
+    for (int v : {1, 2, 3, 4, 5, 6, 8, 9, 10}) {
       if ((sk == 1 && v == 2) || (sk < 2 && (v == 4 || v == 5)) || (sk == 2 && v < 4) || (v == 8 && sk != 1)) continue;
+      if (v >= 9 && sk == 0) continue;
       g_gemm_bf3_force = v;
       gemm_linear(A, K, W, K, bias, C, N, M, N, K, 0, nullptr, 0, nullptr, 0, s, nullptr, sk ? &wk : nullptr, wb);
       CK(hipStreamSynchronize(s));
@@ -100,6 +102,96 @@ int main(int argc, char** argv) {
     }
   }
   g_gemm_bf3_force = 0;
+  if (argc > 1 && std::string(argv[1]) == "sched") {  // 256x256 staging schedules A/B, interleaved rounds, M = 32032
+    struct Sh { const char* name; int N, K; };
+    const Sh sh4[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
+    const int M = 32032;
+    g_gemm_bf3_force = 6;
+    for (const Sh& sh : sh4) {
+      std::vector<float> c0((size_t)M * sh.N), c1(c0.size());
+      for (int sc = 0; sc < 2; ++sc) {
+        g_gemm_bf3_256_s = sc;
+        CK(hipMemsetAsync(C, 0, c0.size() * 4, s));
+        gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s, nullptr, &wk, wb);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy((sc ? c1 : c0).data(), C, c0.size() * 4, hipMemcpyDeviceToHost));
+      }
+      size_t nd = 0;
+      for (size_t i = 0; i < c0.size(); ++i) nd += c0[i] != c1[i];
+      printf("M=%d %-9s: schedule 1 vs 0: %zu outputs differ;", M, sh.name, nd);
+      for (int round = 0; round < 3; ++round)
+        for (int sc = 0; sc < 2; ++sc) {
+          g_gemm_bf3_256_s = sc;
+          const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0,
+                                                         s, nullptr, &wk, wb); }, 10);
+          printf("  s%d %6.1f us %5.1f TF/s", sc, us, 2.0 * M * sh.N * sh.K / us / 1e6);
+        }
+      printf("\n");
+    }
+    g_gemm_bf3_force = 2;  // the 128x128 tile, same A/B
+    for (const Sh& sh : sh4) {
+      printf("M=%d %-9s 128x128:", M, sh.name);
+      for (int round = 0; round < 2; ++round)
+        for (int sc = 0; sc < 2; ++sc) {
+          g_gemm_bf3_256_s = sc;
+          const double us = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, nullptr, 0, nullptr, 0,
+                                                         s, nullptr, &wk, wb); }, 10);
+          printf("  s%d %6.1f us %5.1f TF/s", sc, us, 2.0 * M * sh.N * sh.K / us / 1e6);
+        }
+      printf("\n");
+    }
+    g_gemm_bf3_256_s = 1;
+    g_gemm_bf3_force = 0;
+    return 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "kscan") {  // fixed vs per-k-step cost of the one-clip GEMMs (M = 1001)
+    __half* W16;
+    CK(hipMalloc(&W16, (size_t)Nmax * Kmax * 2));
+    launch_f2h_initializer(W, W16, nullptr, (int64_t)Nmax * Kmax, s);
+    CK(hipStreamSynchronize(s));
+    struct Sh { const char* name; int N, K; };
+    for (const Sh& sh : {Sh{"sanm qkv", 1536, 512}, Sh{"sanm out", 512, 512}, Sh{"ffn1", 2048, 512}, Sh{"ffn2", 512, 2048}}) {
+      printf("M=1001 %-9s:", sh.name);
+      for (int v : {0, 9, 10}) {
+        g_gemm_bf3_force = v;
+        const double b3 = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, 1001, sh.N, sh.K, 0, nullptr, 0, nullptr, 0,
+                                                       s, nullptr, &wk, wb); }, 50);
+        const double f16 = time_graph([&] { gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, 1001, sh.N, sh.K, 0, nullptr, 0, nullptr, 0,
+                                                        s, W16, &wk); }, 50);
+        CK(hipGetLastError());
+        double dev[2];
+        for (int p16 = 0; p16 < 2; ++p16) {  // this variant vs the default policy, same precision
+          std::vector<float> c0((size_t)1001 * sh.N), c1(c0.size());
+          for (int pass = 0; pass < 2; ++pass) {
+            g_gemm_bf3_force = pass ? v : 0;
+            CK(hipMemsetAsync(C, 0, c0.size() * 4, s));
+            gemm_linear(A, sh.K, W, sh.K, bias, C, sh.N, 1001, sh.N, sh.K, 0, nullptr, 0, nullptr, 0, s, p16 ? W16 : nullptr,
+                        &wk, p16 ? WSplit{} : wb);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy((pass ? c1 : c0).data(), C, c0.size() * 4, hipMemcpyDeviceToHost));
+          }
+          double e = 0, mx = 0;
+          for (size_t i = 0; i < c0.size(); ++i) { e = std::max(e, (double)std::fabs(c0[i] - c1[i])); mx = std::max(mx, (double)std::fabs(c0[i])); }
+          dev[p16] = e / mx;
+        }
+        g_gemm_bf3_force = v;
+        printf("  force %2d: bf16x3 %6.1f fp16 %6.1f us (dev %.0e / %.0e)", v, b3, f16, dev[0], dev[1]);
+      }
+      g_gemm_bf3_force = 0;
+      printf("\n");
+    }
+    for (int N : {512, 1536}) {
+      for (int K : {64, 128, 256, 512, 1024, 2048}) {
+        const double b3 = time_graph([&] { gemm_linear(A, K, W, K, bias, C, N, 1001, N, K, 0, nullptr, 0, nullptr, 0, s,
+                                                       nullptr, &wk, wb); }, 50);
+        const double f16 = time_graph([&] { gemm_linear(A, K, W, K, bias, C, N, 1001, N, K, 0, nullptr, 0, nullptr, 0, s,
+                                                        W16, &wk); }, 50);
+        CK(hipGetLastError());
+        printf("M=1001 N=%4d K=%4d: bf16x3 %6.1f us  fp16 %6.1f us\n", N, K, b3, f16);
+      }
+    }
+    return 0;
+  }
   struct Sh { const char* name; int N, K; };
   const Sh shapes[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
   if (ksmode) {
