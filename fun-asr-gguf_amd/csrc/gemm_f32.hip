@@ -415,7 +415,8 @@ static int k_splits(int64_t tiles, int K, const GemmF32Work* wk, int kmin) {
   return ks;
 }
 
-template <class AL, class EPI, int WM, int WN, int KB, bool SPLIT = false>
+// S = 1: write-after-barrier staging (k_gemm_bf3_256 S = 1); same MFMA order
+template <class AL, class EPI, int WM, int WN, int KB, bool SPLIT = false, int S = 0>
 __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict__ W, int64_t ldw, int M, int N, int K,
                                                   EPI epi, float* __restrict__ part, int* __restrict__ cnt) {
   using T = Tile<WM, WN, KB>;
@@ -438,11 +439,18 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
   const int kb0 = blockIdx.z * kper, ke = min(K, kb0 + kper);  // this split's k range (zero-filled past ke)
   load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0, M, N, ke, ra, rb);
   store_tiles<WM, WN, KB>(smem, smem + T::BM * LDK, ra, rb);
-  __syncthreads();
   const int nk = (ke - kb0 + KB - 1) / KB;
+  if (S == 1 && nk > 1) load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rb);
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rb);
+    if constexpr (S == 1) {
+      if (kt + 1 < nk)
+        store_tiles<WM, WN, KB>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
+      if (kt + 2 < nk) load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0 + (kt + 2) * KB, M, N, ke, ra, rb);
+    } else {
+      if (kt + 1 < nk) load_tiles<WM, WN, KB>(al, W, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rb);
+    }
     const float* a = smem + cur * T::STAGE + (wr * 32 * WM + r) * LDK + h;
     const float* b = smem + cur * T::STAGE + T::BM * LDK + (wc * 32 * WN + r) * LDK + h;
 #pragma unroll
@@ -457,7 +465,8 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
 #pragma unroll
         for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tiles<WM, WN, KB>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
+    if (S == 0 && kt + 1 < nk)
+      store_tiles<WM, WN, KB>(smem + (cur ^ 1) * T::STAGE, smem + (cur ^ 1) * T::STAGE + T::BM * LDK, ra, rb);
     __syncthreads();
   }
   if constexpr (SPLIT && WM == 1 && WN == 1)
@@ -469,27 +478,36 @@ __global__ __launch_bounds__(256) void k_gemm_f32(AL al, const float* __restrict
   epi.finish(m0, n0, M, N, smem);
 }
 
-template <class AL, class EPI, int WM, int WN, int KB = BK>
-static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
-                        const GemmF32Work* wk = nullptr) {
+int g_gemm_f32_wab = 0;  // exact-f32 tiles: 1 = write-after-barrier staging (FUNASR_F32_WAB)
+
+template <class AL, class EPI, int WM, int WN, int KB, int S>
+static void launch_gemm_s(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
+                          const GemmF32Work* wk) {
   using T = Tile<WM, WN, KB>;
   const int ks = WM == 1 && WN == 1 ? k_splits((int64_t)cdiv(N, T::BN) * cdiv(M, T::BM), K, wk, 512) : 1;
   const dim3 grid = xcd_grid(cdiv(N, T::BN), cdiv(M, T::BM), ks);
   const size_t lds = 2 * T::STAGE * sizeof(float);
   static bool attr = false;
   if (!attr && lds > 65536) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB, false, S>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_gemm_f32<AL, EPI, WM, WN, KB, true, S>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   if (ks > 1)
-    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB, true>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi,
+    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB, true, S>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi,
                        wk->part, wk->cnt);
   else
-    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi, nullptr,
-                       nullptr);
+    hipLaunchKernelGGL((k_gemm_f32<AL, EPI, WM, WN, KB, false, S>), grid, dim3(256), lds, s, al, W, ldw, M, N, K, epi,
+                       nullptr, nullptr);
+}
+
+template <class AL, class EPI, int WM, int WN, int KB = BK>
+static void launch_gemm(const AL& al, const float* W, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
+                        const GemmF32Work* wk = nullptr) {
+  if (g_gemm_f32_wab) launch_gemm_s<AL, EPI, WM, WN, KB, 1>(al, W, ldw, M, N, K, epi, s, wk);
+  else launch_gemm_s<AL, EPI, WM, WN, KB, 0>(al, W, ldw, M, N, K, epi, s, wk);
 }
 
 // 128x128 blocks (4 MFMA accumulators per wave: half the LDS reads per MFMA) when they still give every CU

@@ -1113,7 +1113,9 @@ __device__ __forceinline__ void qt_store(uint8_t* st, int t, const i32x4_t (&rw)
   sc[(T::NM * 2 + blk) * 128 + row] = rdx;
 }
 
-template <int EPI>
+// S = 1: write-after-barrier staging (the encoder GEMM tiles' schedule): the registers holding K-step kt + 1, loaded a
+// whole step earlier, go to the free stage at the top of step kt and then take step kt + 2's loads
+template <int EPI, int S = 0>
 __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
   using T = QTile<EPI>;
   constexpr int NM = T::NM;
@@ -1133,11 +1135,17 @@ __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
   const int nk = K / 64;
   qt_load<EPI>(a, K, o0, t0, 0, t, rw, rx, rdw, rdx);
   qt_store<EPI>(qsm, t, rw, rx, rdw, rdx);
+  if (S == 1 && nk > 1) qt_load<EPI>(a, K, o0, t0, 2, t, rw, rx, rdw, rdx);
   __syncthreads();
   const i32x16_t zero = {};
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) qt_load<EPI>(a, K, o0, t0, 2 * (kt + 1), t, rw, rx, rdw, rdx);
+    if constexpr (S == 1) {
+      if (kt + 1 < nk) qt_store<EPI>(qsm + (cur ^ 1) * T::STAGE, t, rw, rx, rdw, rdx);
+      if (kt + 2 < nk) qt_load<EPI>(a, K, o0, t0, 2 * (kt + 2), t, rw, rx, rdw, rdx);
+    } else {
+      if (kt + 1 < nk) qt_load<EPI>(a, K, o0, t0, 2 * (kt + 1), t, rw, rx, rdw, rdx);
+    }
     const uint8_t* st = qsm + cur * T::STAGE;
     const float* sc = reinterpret_cast<const float*>(st + (NM + 1) * T::W);
 #pragma unroll 1
@@ -1174,7 +1182,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
           __builtin_amdgcn_sched_barrier(0);  // one (matrix, row tile) at a time: two MFMA results live, not eight
         }
     }
-    if (kt + 1 < nk) qt_store<EPI>(qsm + (cur ^ 1) * T::STAGE, t, rw, rx, rdw, rdx);
+    if (S == 0 && kt + 1 < nk) qt_store<EPI>(qsm + (cur ^ 1) * T::STAGE, t, rw, rx, rdw, rdx);
     __syncthreads();
   }
   // epilogue: lane -> token t0 + wc 64 + jj 32 + r; reg -> row o0 + wr 64 + i 32 + (reg & 3) + 8 (reg >> 2) + 4 h
@@ -1230,21 +1238,29 @@ __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
 
 int g_gemm_t_min_m = 512;  // token count from which prefill GEMMs take the tiled kernel (FUNASR_GEMM_T_MIN_M)
 
-static bool gemm_q8_t(const GemvArgs& a, int K, int epi, hipStream_t s) {
-  if (a.M < g_gemm_t_min_m || epi == 3 || K % 64 || a.O % 32) return false;
-  const dim3 grid(cdiv(a.O, 128), cdiv(a.M, 128));
+int g_gemm_t_wab = 0;  // k_gemm_q8_t write-after-barrier staging (FUNASR_GEMM_T_WAB)
+
+template <int S>
+static void launch_gemm_q8_t(const GemvArgs& a, int K, int epi, dim3 grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<0>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<0>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<1>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<1>::BYTES);
-    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<2>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<2>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<0, S>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<0>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<1, S>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<1>::BYTES);
+    (void)hipFuncSetAttribute((const void*)k_gemm_q8_t<2, S>, hipFuncAttributeMaxDynamicSharedMemorySize, QTile<2>::BYTES);
     attr = true;
   }
   switch (epi) {
-    case 0: hipLaunchKernelGGL(k_gemm_q8_t<0>, grid, dim3(256), QTile<0>::BYTES, s, a, K); break;
-    case 1: hipLaunchKernelGGL(k_gemm_q8_t<1>, grid, dim3(256), QTile<1>::BYTES, s, a, K); break;
-    default: hipLaunchKernelGGL(k_gemm_q8_t<2>, grid, dim3(256), QTile<2>::BYTES, s, a, K); break;
+    case 0: hipLaunchKernelGGL((k_gemm_q8_t<0, S>), grid, dim3(256), QTile<0>::BYTES, s, a, K); break;
+    case 1: hipLaunchKernelGGL((k_gemm_q8_t<1, S>), grid, dim3(256), QTile<1>::BYTES, s, a, K); break;
+    default: hipLaunchKernelGGL((k_gemm_q8_t<2, S>), grid, dim3(256), QTile<2>::BYTES, s, a, K); break;
   }
+}
+
+static bool gemm_q8_t(const GemvArgs& a, int K, int epi, hipStream_t s) {
+  if (a.M < g_gemm_t_min_m || epi == 3 || K % 64 || a.O % 32) return false;
+  const dim3 grid(cdiv(a.O, 128), cdiv(a.M, 128));
+  if (g_gemm_t_wab) launch_gemm_q8_t<1>(a, K, epi, grid, s);
+  else launch_gemm_q8_t<0>(a, K, epi, grid, s);
   return true;
 }
 
