@@ -15,7 +15,9 @@ from typing import List, Optional
 
 import numpy as np
 
-from ..nano_ctc import align_timestamps, decode_ctc_pairs
+from concurrent.futures import Future, ThreadPoolExecutor
+
+from ..nano_ctc import align_timestamps, ctc_pair_rows, tokens_of
 from ..nano_dataclass import DecodeResult, LLMDecodeResult, RecognitionStream, Timings
 
 STOP_TOKENS = (151643, 151645)          # decoder.py:53
@@ -260,6 +262,18 @@ class LLMDecoder:
         return final
 
 
+_TOKEN_POOL = None
+
+
+def _token_pool():
+    """One background thread that builds the CTC Token lists (tens of thousands of objects per 32-clip batch) while the
+    main thread waits on the GPU in prefill / generate (ctypes releases the GIL inside the engine calls)."""
+    global _TOKEN_POOL
+    if _TOKEN_POOL is None:
+        _TOKEN_POOL = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ctc-tokens")
+    return _TOKEN_POOL
+
+
 class StreamDecoder:
     def __init__(self, models):
         self.models = models
@@ -293,8 +307,11 @@ class StreamDecoder:
             blank = max(m.ctc_id2token.keys()) if m.ctc_id2token else 0
             pairs = eng.ctc_collapse(blank, B)
             for b in range(B):
-                txt, ctc_results[b] = decode_ctc_pairs(pairs[b][0], pairs[b][1], m.ctc_id2token)
-                hotwords[b] = m.match_hotwords(txt, m.config.max_hotwords)
+                texts, starts = ctc_pair_rows(pairs[b][0], pairs[b][1], m.ctc_id2token)
+                hotwords[b] = m.match_hotwords("".join(texts), m.config.max_hotwords)
+                # the Token list (decode_ctc_pairs' second result) is built off the critical path; back() collects it
+                ctc_results[b] = _token_pool().submit(tokens_of, texts, starts) if len(texts) > 64 else \
+                    tokens_of(texts, starts)
         dt = time.perf_counter() - t
         for tm in timings:
             tm.ctc = tm.ctc_decode = dt / B
@@ -320,6 +337,8 @@ class StreamDecoder:
         """Step 5 for one stream: alignment of the LLM text to the CTC tokens -> DecodeResult."""
         text = r.text.strip()
         tm = job["timings"]
+        if isinstance(job["ctc_results"], Future):
+            job["ctc_results"] = job["ctc_results"].result()
         tm.inject, tm.llm_generate = r.t_inject, r.t_gen
         t = time.perf_counter()
         aligned = align_timestamps(job["ctc_results"], text) if job["ctc_results"] else None

@@ -11,13 +11,14 @@ import base64
 import ctypes
 import os
 from dataclasses import dataclass
+from itertools import repeat
 
 import numpy as np
 
 from . import _native
 
 
-@dataclass
+@dataclass(slots=True)  # the reference's fields, order, eq and repr (nano_ctc.py:7-10); slots: ~2x faster to build
 class Token:
     text: str
     start: float
@@ -40,16 +41,26 @@ def load_ctc_tokens(filename):
     return id2token
 
 
+def ctc_pair_rows(ids, frames, id2token):
+    """(texts, starts) of the collapsed pairs, empty tokens dropped: the Token fields of decode_ctc_pairs as two lists.
+    start = max((frame * 60 - 240) / 1000, 0) in float64 (exactly the reference's Python arithmetic)."""
+    ids = ids.tolist() if hasattr(ids, "tolist") else list(ids)
+    texts = list(map(id2token.get, ids, repeat("")))
+    starts = np.maximum((np.asarray(frames, np.int64) * 60 - 240) / 1000.0, 0.0).tolist()
+    if "" in texts:
+        keep = [k for k, x in enumerate(texts) if x]
+        texts, starts = [texts[k] for k in keep], [starts[k] for k in keep]
+    return texts, starts
+
+
+def tokens_of(texts, starts):
+    return list(map(Token, texts, starts))
+
+
 def decode_ctc_pairs(ids, frames, id2token):
     """(text, [Token]) from collapsed pairs; blank and empty tokens never appear in the output."""
-    res = []
-    get = id2token.get
-    for tid, fr in zip(ids.tolist() if hasattr(ids, "tolist") else ids, frames.tolist() if hasattr(frames, "tolist") else frames):
-        txt = get(tid, "")
-        if not txt:
-            continue
-        res.append(Token(txt, max((fr * 60 + -240) / 1000.0, 0.0)))
-    return "".join(r.text for r in res), res
+    texts, starts = ctc_pair_rows(ids, frames, id2token)
+    return "".join(texts), tokens_of(texts, starts)
 
 
 def collapse_ids(ids, blank_id):

@@ -178,3 +178,31 @@ def test_ignore_eos_pinned_length_protocol():
     res = dec.decode_many([np.full((2, 4), s, np.float32) for s in sorted(scripts)], 253, temperature=0.0)
     assert [r.n_gen for r in res] == [253] * len(scripts)
     assert not any(r.is_aborted for r in res)
+
+
+def test_deferred_ctc_tokens_equal_decode_ctc_pairs():
+    """front() builds each clip's CTC Token list on a background thread (long lists) and back() collects it: the results
+    carry exactly decode_ctc_pairs' tokens for the clip's collapsed pairs (reference nano_ctc.py:38-116)."""
+    import numpy as np
+    from fake_engine import fake_models
+    from fun_asr_gguf.core.decoder import StreamDecoder
+    from fun_asr_gguf.nano_ctc import Token, decode_ctc_pairs
+    from fun_asr_gguf.nano_dataclass import RecognitionStream
+    m = fake_models(max_batch=4, n_predict=8)
+    dec = StreamDecoder(m)
+    rng = np.random.default_rng(3)
+    clips = [(rng.standard_normal(int(16000 * s)) * 0.1).astype(np.float32) for s in (30.0, 0.5, 12.0)]
+    streams = []
+    for c in clips:
+        st = RecognitionStream()
+        st.accept_waveform(16000, c)
+        streams.append(st)
+    rs = dec.decode_streams(streams, verbose=False, temperature=0.0)
+    blank = max(m.ctc_id2token.keys())
+    m.engine.encode(clips)
+    pairs = m.engine.ctc_collapse(blank, len(clips))
+    assert max(len(p[0]) for p in pairs) > 64  # the background path ran
+    for r, (ids, fr) in zip(rs, pairs):
+        _, want = decode_ctc_pairs(ids, fr, m.ctc_id2token)
+        assert isinstance(r.ctc_results, list) and all(type(t) is Token for t in r.ctc_results)
+        assert r.ctc_results == want
