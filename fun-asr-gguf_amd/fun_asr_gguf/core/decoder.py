@@ -274,6 +274,27 @@ def _token_pool():
     return _TOKEN_POOL
 
 
+def _pair_tokens(ids, frames, id2token):
+    return tokens_of(*ctc_pair_rows(ids, frames, id2token))
+
+
+_BLANK = {}
+
+
+def _blank_of(id2token):
+    """The CTC blank id = the largest id of the vocabulary (tokens.txt's last line, decoder.py:27); cached per table
+    (max over 60k keys costs ~1 ms per call)."""
+    if not id2token:
+        return 0
+    key = (id(id2token), len(id2token))
+    hit = _BLANK.get(key)
+    if hit is None or hit[0] is not id2token:  # (holding the table keeps its id from being reused)
+        if len(_BLANK) > 8:
+            _BLANK.clear()
+        hit = _BLANK[key] = (id2token, max(id2token.keys()))
+    return hit[1]
+
+
 class StreamDecoder:
     def __init__(self, models):
         self.models = models
@@ -304,14 +325,18 @@ class StreamDecoder:
         t = time.perf_counter()
         ctc_results, hotwords = [[] for _ in range(B)], [[] for _ in range(B)]
         if m.config.enable_ctc:
-            blank = max(m.ctc_id2token.keys()) if m.ctc_id2token else 0
-            pairs = eng.ctc_collapse(blank, B)
+            pairs = eng.ctc_collapse(_blank_of(m.ctc_id2token), B)
+            # the hotword step needs the CTC text before the prompt; without a hotword source the prompt does not depend
+            # on it, and the whole host decode of the pairs runs off the critical path (back() collects the Tokens)
+            need_text = getattr(m, "hotword_source", None) is not None
             for b in range(B):
-                texts, starts = ctc_pair_rows(pairs[b][0], pairs[b][1], m.ctc_id2token)
-                hotwords[b] = m.match_hotwords("".join(texts), m.config.max_hotwords)
-                # the Token list (decode_ctc_pairs' second result) is built off the critical path; back() collects it
-                ctc_results[b] = _token_pool().submit(tokens_of, texts, starts) if len(texts) > 64 else \
-                    tokens_of(texts, starts)
+                if need_text or len(pairs[b][0]) <= 64:
+                    texts, starts = ctc_pair_rows(pairs[b][0], pairs[b][1], m.ctc_id2token)
+                    hotwords[b] = m.match_hotwords("".join(texts), m.config.max_hotwords)
+                    ctc_results[b] = _token_pool().submit(tokens_of, texts, starts) if len(texts) > 64 else \
+                        tokens_of(texts, starts)
+                else:
+                    ctc_results[b] = _token_pool().submit(_pair_tokens, pairs[b][0], pairs[b][1], m.ctc_id2token)
         dt = time.perf_counter() - t
         for tm in timings:
             tm.ctc = tm.ctc_decode = dt / B

@@ -13,7 +13,10 @@ import sqlite3
 import sys
 from collections import defaultdict
 
-CLASSES = {  # kernel-name substring -> class
+CLASSES = {  # kernel-name substring -> class (first match; the fp16 graph's P = 1 instances of the bf16x3 family first)
+    "PrecB<1>": "encoder GEMM (fp16 graph)",
+    "k_attn_bf3<128, 1": "encoder attention (fp16 graph)",
+    "k_attn_bf3<64, 1": "encoder attention (fp16 graph)",
     "k_gemm_bf3": "encoder GEMM (bf16x3)",
     "k_attn_bf3": "encoder attention (bf16x3)",
     "k_gemm_f32": "encoder GEMM (exact f32 / STFT / mel)",
