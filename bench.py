@@ -186,11 +186,12 @@ def c3_leg(batch, steps, warmup, device, model, barrier, dist):
     m.engine.synchronize()
     barrier()
     t0 = time.perf_counter()
-    stage = np.zeros(4)
+    stage = np.zeros(6)
     for _ in range(steps):
         rs = step()
         tm = rs[0].timings
-        stage += [tm.encode, tm.inject, tm.llm_generate, tm.align * batch]
+        # per-stream shares (ctc, prepare, inject, align are the batch's time / batch) -> the batch's time
+        stage += [tm.encode, tm.ctc * batch, tm.prepare * batch, tm.inject * batch, tm.llm_generate, tm.align * batch]
     m.engine.synchronize()
     dt = time.perf_counter() - t0
     barrier()
@@ -205,7 +206,8 @@ def c3_leg(batch, steps, warmup, device, model, barrier, dist):
                         f"batch {batch}, 204-token prefill per clip, 253 greedy steps, EOS ignored)",
             "value": round(CLIP_S * batch * steps * world / dt, 2), "unit": "audio_s/s", "steps": steps,
             "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 2),
-            "stage_ms": {k: round(v / steps * 1e3, 2) for k, v in zip(["encode", "prefill", "generate", "align"], stage)}}
+            "stage_ms": {k: round(v / steps * 1e3, 2) for k, v in zip(["encode", "ctc", "prompt", "prefill", "generate",
+                                                                        "align"], stage)}}
 
 
 def c3_varlen_leg(n_clips, batch, device, model, barrier, dist):
