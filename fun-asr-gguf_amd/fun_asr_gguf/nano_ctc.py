@@ -78,17 +78,22 @@ def collapse_ids(ids, blank_id):
 def align_timestamps(ctc_results, llm_text):
     if not ctc_results or not llm_text:
         return []
-    chars, starts = [], []
-    for item in ctc_results:
-        for i, ch in enumerate(item.text):
-            chars.append(ch)
-            starts.append(item.start + i * 0.08)
+    texts = [item.text for item in ctc_results]
+    chars = list("".join(texts))
+    if len(chars) == len(texts) and "" not in texts:  # one char per token (the common case): the starts as they are
+        starts = [item.start for item in ctc_results]
+    else:  # char i of a token starts at start + i * 0.08 (nano_ctc.py:128-131)
+        starts = []
+        for item in ctc_results:
+            starts.extend([item.start + i * 0.08 for i in range(len(item.text))])
     llm_chars = list(llm_text)
     if not chars:  # every CTC token empty: the reference DP aligns nothing -> all starts 0.0
         return [{"char": c, "start": 0.0} for c in llm_chars]
-    keys = {}
-    ck = np.array([keys.setdefault(c.lower(), len(keys)) for c in chars], np.int32)
-    lk = np.array([keys.setdefault(c.lower(), len(keys)) for c in llm_chars], np.int32)
+    # the DP compares lower-cased chars for equality only: one id per distinct lower-cased char, over both strings
+    low = {}
+    cid = {c: low.setdefault(c.lower(), len(low)) for c in set(chars).union(llm_chars)}
+    ck = np.fromiter(map(cid.__getitem__, chars), np.int32, len(chars))
+    lk = np.fromiter(map(cid.__getitem__, llm_chars), np.int32, len(llm_chars))
     st = np.array(starts, np.float64)
     out = np.empty(len(llm_chars), np.float64)
     lib = _native.load()
