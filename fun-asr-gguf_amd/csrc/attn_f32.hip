@@ -311,6 +311,11 @@ typedef _Float16 f16x4a __attribute__((ext_vector_type(4)));
 #ifndef FA_ATTN_TRV
 #define FA_ATTN_TRV 1
 #endif
+// FA_ATTN_DIAG (microbenchmark builds only; wrong results by construction): 1 = no K/V global loads or LDS stores in
+// the key loop, 2 = no S MFMAs, 3 = no PV MFMAs, 4 = no softmax (exp / max / sum)
+#ifndef FA_ATTN_DIAG
+#define FA_ATTN_DIAG 0
+#endif
 template <int D>
 struct AttnLds3 {
   static constexpr int SK = D + 8;                   // K plane row (bf16): 16-B reads of 16 rows, distinct bank groups
@@ -443,7 +448,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     if constexpr (S == 1) {
       if (kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
       if (kt + 2 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 2, pk, pv);  // in flight
-    } else {
+    } else if (FA_ATTN_DIAG != 1) {
       if (kt + 1 < kt1) attn_load_tile<D>(Kp, V, ldk, ldv, row_base, head, t_stride, kt + 1, pk, pv);  // in flight
     }
     const __bf16* kh_ = reinterpret_cast<const __bf16*>(lds + stage * L::STAGE);
@@ -463,12 +468,22 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
       for (int st = 0; st < NKS; ++st) {
         const bf16x8 kh = *reinterpret_cast<const bf16x8*>(kh_ + r * L::SK + 16 * st + 8 * h);
         const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kh_ + L::KP + r * L::SK + 16 * st + 8 * h);
+#if FA_ATTN_DIAG == 2
+        asm volatile("" ::"v"(kh), "v"(kl), "v"(qh[st]), "v"(ql[st]));
+        s[st] += (float)kh[0];
+#else
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qh[st], s, 0, 0, 0);
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], s, 0, 0, 0);
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], s, 0, 0, 0);
+#endif
       }
     }
     // mask + online softmax (as k_attn_f32)
+#if FA_ATTN_DIAG == 4
+    float alpha = 1.f;
+    asm volatile("" : "+v"(alpha));
+    m_run = 0.f;
+#else
     float mt = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
@@ -492,6 +507,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     ls += __shfl_xor(ls, 32, 64);
     l_run = l_run * alpha + ls;
     m_run = m_new;
+#endif
 #pragma unroll
     for (int i = 0; i < NDT; ++i) o[i] *= alpha;
     // O^T[d][q] += V^T[d][key] P^T[key][q]: P^T k-step s2 = registers 8 s2 .. 8 s2 + 7 (keys 16 s2 + kl(j))
@@ -544,12 +560,17 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
             vl[j] = (__bf16)(x - (float)vh[j]);
           }
         }
+#if FA_ATTN_DIAG == 3
+        asm volatile("" ::"v"(vh), "v"(vl), "v"(ph), "v"(pl));
+        o[i][0] += (float)vh[0];
+#else
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, ph, o[i], 0, 0, 0);
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o[i], 0, 0, 0);
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o[i], 0, 0, 0);
+#endif
       }
     }
-    if (S == 0 && kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
+    if (S == 0 && FA_ATTN_DIAG != 1 && kt + 1 < kt1) attn3_store_tile<D, P>(lds + (stage ^ 1) * L::STAGE, pk, pv);
     __syncthreads();
   }
   attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, P == 1 ? 1 : 0,
