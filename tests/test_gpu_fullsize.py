@@ -635,3 +635,26 @@ def test_prefill_rows_assembled_on_device_equal_host_prompts(eng):
     eng.llm_reset(0)
     with pytest.raises(RuntimeError, match="out of range"):
         eng.llm_prefill_rows([0], [bad])
+
+
+def test_write_after_barrier_gemm_staging_bit_identical(monkeypatch):
+    """The 256x256 / 128x128 bf16x3 tiles' write-after-barrier staging (FUNASR_BF3_256_S=1, the default) keeps every
+    product's MFMA order: a batch of eight 60 s clips (M = 8008: the encoder GEMMs and the CTC projection with its fused
+    argmax on the 256x256 tile) encodes bit-identically with the earlier load-then-store schedule."""
+    from fun_asr_gguf import _native
+    from fun_asr_gguf.synthetic import synth_audio
+    clips = [synth_audio(SR * 60, 300 + i) for i in range(8)]
+    outs = []
+    for sched in ("0", "1"):
+        monkeypatch.setenv("FUNASR_BF3_256_S", sched)
+        e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=8,
+                           max_samples=SR * 62)
+        try:
+            e.synthetic_weights(0)
+            outs.append(e.encode(clips, want_enc=True))
+        finally:
+            e.close()
+    for b in range(len(clips)):
+        assert np.array_equal(outs[0]["enc"][b], outs[1]["enc"][b]), f"clip {b}: encoder rows"
+        assert np.array_equal(outs[0]["audio_embd"][b], outs[1]["audio_embd"][b]), f"clip {b}: adaptor rows"
+        assert np.array_equal(outs[0]["ctc_ids"][b], outs[1]["ctc_ids"][b]), f"clip {b}: CTC ids"
