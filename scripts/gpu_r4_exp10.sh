@@ -1,5 +1,5 @@
 #!/bin/bash
-# encoder attention ablations (FA_ATTN_DIAG 1-4: no K/V staging / no S MFMAs / no PV MFMAs / no softmax) vs the full
+# (binaries: scripts/ubench/build_diag.sh) encoder attention ablations (FA_ATTN_DIAG 1-4: no K/V staging / no S MFMAs / no PV MFMAs / no softmax) vs the full
 # kernel, graph-replayed, one clip and batch 32
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
