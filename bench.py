@@ -416,9 +416,15 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     args.launcher = os.environ.get("BENCH_LAUNCHER", "torchrun" if world > 1 else "single")
     dist = None
-    if world > 1:
+    # BENCH_FORCE_DIST=1: the multi-rank code path (RCCL process group, barriers, max-over-ranks timing, sharded
+    # transcribe with the engine-native gather) at world size 1 -- a one-GPU rehearsal of what N > 1 runs
+    if world > 1 or os.environ.get("BENCH_FORCE_DIST") == "1":
         import torch
         import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
