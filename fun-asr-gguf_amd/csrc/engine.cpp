@@ -1614,6 +1614,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_ATTN_WAB")) fa::g_attn_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_T_WAB")) fa::g_gemm_t_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_LM_TR")) fa::g_lm_tr = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):

@@ -257,11 +257,69 @@ __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int 
 #ifndef FA_RES0_PRELOAD
 #define FA_RES0_PRELOAD 1
 #endif
-template <int NCH, int MT, int EPI>
+// One level of a transposed wave reduction: lanes l and l ^ (1 << B) exchange halves of their N partial sums, so every
+// lane keeps N / 2 of them, each now summed over both lanes. Levels B = 0..5 add the lanes in exactly wave_sum's
+// pairs (xor 1, xor 2, then quads, 8-lane halves, rows 0+1 / 2+3, and the two row pairs: row_half_mirror and
+// row_mirror pair the same groups once the lower levels made their lanes equal), so every sum is bit-identical to
+// wave_sum of that value, for N values at the cost of about 3 N / 2 instructions instead of 11 N.
+template <int N, int B>
+__device__ __forceinline__ void tr_level(float (&v)[32], int lane) {
+  const bool hi = (lane >> B) & 1;
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const float keep = hi ? v[k + N / 2] : v[k];
+    const float send = hi ? v[k] : v[k + N / 2];
+    float recv;
+    if constexpr (B == 0) recv = dpp_f<DPP_XOR1>(send);
+    else if constexpr (B == 1) recv = dpp_f<DPP_XOR2>(send);
+    else recv = __shfl_xor(send, 1 << B, 64);
+    v[k] = keep + recv;
+  }
+}
+
+template <int NCH, int MT, int EPI, bool TR = false>
 __device__ __forceinline__ void compute_group(const GemvArgs& a, int row_base, int r0, int lane, int m0, int mt,
                                               const int8_t* s_q, const float* s_d, const RowGroup<NCH, EPI>& G,
                                               float (&best_v)[MT], int (&best_i)[MT], const float (&res0)[4]) {
   constexpr int K = NCH * 1024, NB = K / 32;
+  if constexpr (TR) {
+    static_assert(EPI == 3 && MT > 1 && MT <= 8, "compute_group: transposed reduction for the LM head of 2-8 tokens");
+    // LM head of 2-8 tokens: the 4 rows x MT tokens of the group reduced together (slot rr * 8 + m); afterwards lane l
+    // (and l ^ 32) holds slot 16 b0 + 8 b1 + 4 b2 + 2 b3 + b4 of its bits, i.e. row rr = 2 b0 + b1 and token
+    // m = 4 b2 + 2 b3 + b4, and keeps the running argmax of its (rr, m) in best_v[0] / best_i[0]; the tokens' argmax
+    // partials are gathered once per wave after the row loop (argmax_combine is order-free: max, lowest index on ties)
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m >= mt) break;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int4 xv = *reinterpret_cast<const int4*>(s_q + m * K + c * 1024 + lane * 16);
+        const float xdv = s_d[m * NB + c * 32 + (lane >> 1)];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          int si = dot16(G.w[rr][c], xv, 0);
+          si += dpp_i<DPP_XOR1>(si);
+          if (!(lane & 1)) v[rr * 8 + m] += (float)si * (G.dw[rr][c] * xdv);
+        }
+      }
+    }
+    tr_level<32, 0>(v, lane);
+    tr_level<16, 1>(v, lane);
+    tr_level<8, 2>(v, lane);
+    tr_level<4, 3>(v, lane);
+    tr_level<2, 4>(v, lane);
+    const float y = v[0] + __shfl_xor(v[0], 32, 64);
+    const int rr = 2 * (lane & 1) + ((lane >> 1) & 1), m = 4 * ((lane >> 2) & 1) + 2 * ((lane >> 3) & 1) + ((lane >> 4) & 1);
+    const int row = row_base + r0 + rr;
+    if (lane < 32 && m < mt && (r0 + rr < a.rpw) && row < a.O) {
+      a.out[(int64_t)(m0 + m) * a.ldo + row] = y;
+      argmax_combine(best_v[0], best_i[0], y, row);
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     if (m >= mt) break;
@@ -320,7 +378,8 @@ void gemm_stamps_read(unsigned long long* host, int n) {
 
 // PS (fused decode, M = 1, K = 1024): the activation row is first completed as x + psum[0] + ... + psum[7] (the split
 // down projection of the previous fused layer), and block 0 stores that row to a.xsum (the residual stream).
-template <int NCH, int MT, bool FUSED, int EPI, bool PS = false>
+// TR: the LM head of 2-8 tokens with the transposed row x token reduction (compute_group; same sums, same argmax)
+template <int NCH, int MT, bool FUSED, int EPI, bool PS = false, bool TR = false>
 __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   static_assert(!PS || (NCH == 1 && MT == 1 && FUSED), "partial-sum prologue: M = 1, K = 1024 only");
   GSTAMP(0);
@@ -446,13 +505,31 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   // two-deep register pipeline over 4-row groups (static buffer names, no runtime-indexed arrays)
   for (int r0 = 0; r0 < a.rpw; r0 += 8) {
     if (r0 + 4 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 4, lane, G1);
-    compute_group<NCH, MT, EPI>(a, row_base, r0, lane, m0, mt, s_q, s_d, G0, best_v, best_i, res0);
+    compute_group<NCH, MT, EPI, TR>(a, row_base, r0, lane, m0, mt, s_q, s_d, G0, best_v, best_i, res0);
     if (r0 + 4 >= a.rpw) break;
     if (r0 + 8 < a.rpw) load_group<NCH, EPI>(a, row_base, r0 + 8, lane, G0);
-    compute_group<NCH, MT, EPI>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i, res0);
+    compute_group<NCH, MT, EPI, TR>(a, row_base, r0 + 4, lane, m0, mt, s_q, s_d, G1, best_v, best_i, res0);
   }
   GSTAMP(2);
-  if (EPI == 3 && lane == 0) {
+  if constexpr (TR) {  // compute_group's lane-spread argmax: token m's 4 lanes -> lane 0
+    const int part = blockIdx.x * 4 + wave;
+    const float bv = best_v[0];
+    const int bi = best_i[0];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float v = -INFINITY;
+      int i = 0x7fffffff;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // lanes of token m: bits 0-1 = row, bits 2-4 = m's bits 2, 1, 0
+        const int l = q + 4 * ((m >> 2) & 1) + 8 * ((m >> 1) & 1) + 16 * (m & 1);
+        argmax_combine(v, i, __shfl(bv, l, 64), __shfl(bi, l, 64));
+      }
+      if (lane == 0 && m < mt) {
+        a.pval[(int64_t)(m0 + m) * a.n_part + part] = v;
+        a.pidx[(int64_t)(m0 + m) * a.n_part + part] = i;
+      }
+    }
+  } else if (EPI == 3 && lane == 0) {
     const int part = blockIdx.x * 4 + wave;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -464,9 +541,18 @@ __global__ __launch_bounds__(256) void k_gemv_q8(GemvArgs a) {
   }
 }
 
+int g_lm_tr = 1;  // LM head of 2-8 tokens: transposed row x token reduction (FUNASR_LM_TR; A/B, scripts/gpu_r4_exp11.sh:
+                  // batch-6 decode step 0.933-0.946 -> 0.914-0.931 ms, C4 1038 -> 1051 audio-s/s; bit-identical logits)
+
 template <int NCH, int MT, bool FUSED, int EPI, bool PS = false>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   dim3 grid(cdiv(a.O, 4 * a.rpw), cdiv(a.M, MT));
+  if constexpr (EPI == 3 && MT > 1 && MT <= 8) {
+    if (g_lm_tr) {
+      hipLaunchKernelGGL((k_gemv_q8<NCH, MT, FUSED, EPI, PS, true>), grid, dim3(256), 0, s, a);
+      return;
+    }
+  }
   hipLaunchKernelGGL((k_gemv_q8<NCH, MT, FUSED, EPI, PS>), grid, dim3(256), 0, s, a);
 }
 
