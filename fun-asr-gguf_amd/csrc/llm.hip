@@ -3418,7 +3418,7 @@ void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, 
 
 int g_ffn_pair_min_m = 4;  // decode batches from this width run the fused FFN with two tokens per block
 // (three tokens per block, tried in round 4: 184 VGPRs, 2 blocks per CU; at batches 3-6 the in-launch fan-ins timed out
-// and every chunk fell back to the 5-launch layer, scripts/gpu_r4_exp12.sh: not kept)
+// and every chunk fell back to the 5-launch layer: not kept)
 
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
