@@ -1290,13 +1290,24 @@ struct Engine {
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       if (use_fused == 1) {
+        // batch 1: extra blocks of the attention launch pull this layer's FFN weights and the next layer's attention
+        // weights / K/V rows into the L2 of the XCDs that will read them (llm.hip l2_prefetch)
+        fa::L2Prefetch pf;
+        pf.gq = w.gate.q; pf.gd = w.gate.d; pf.uq = w.up.q; pf.ud = w.up.d; pf.dq = w.down.q; pf.dd = w.down.d;
+        pf.F = F;
+        if (l + 1 < lc.n_layer) {
+          const LlmLayerW& wn = layers[l + 1];
+          pf.qkv_q = wn.qkv.q; pf.qkv_d = wn.qkv.d; pf.o_q = wn.o.q; pf.o_d = wn.o.d;
+          pf.kc = kcache + (size_t)(l + 1) * layer_stride;
+          pf.vc = vcache + (size_t)(l + 1) * layer_stride;
+        }
         // a q8_0 weight-streaming layer launch (class 0, like C): algorithmic bytes = q|k|v + Wo weights + the K/V
         // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
         hipEvent_t ev;
         prof_begin(0, &ev);
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
-                         w.o.q, w.o.d, E, attn_wk, fdw, stream, M, (debug_flags & 2) ? 1 : 0);
+                         w.o.q, w.o.d, E, attn_wk, fdw, stream, M, (debug_flags & 2) ? 1 : 0, &pf);
         prof_end(0, (double)(E * H * D + (size_t)QKV * E) * 34.0 / 32.0 + (M == 1 ? 4.0 * KV * D * (prof_pos + 1.0) : 0.0),
                  2.0 * M * (E * H * D + (double)QKV * E));
       } else {
@@ -1615,6 +1626,16 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GEMM_T_WAB")) fa::g_gemm_t_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_LM_TR")) fa::g_lm_tr = atoi(g) != 0;
+    {  // process-wide decode-path knobs: re-read (or reset) at every engine creation
+      const char* g = getenv("FUNASR_L2PF");
+      // 16 blocks per kv head (one block per CU with the 128 compute blocks), after 0.5 us: graph-replayed batch-1
+      // step 0.4537-0.4549 vs 0.4740-0.4784 ms (scripts/gpu_r4_l2pf.sh; 8 / 12 / 20 / 24 blocks and 1.0-2.5 us slower)
+      fa::g_l2pf_blocks = g ? std::min(64, std::max(0, atoi(g))) : 16;
+      const char* d = getenv("FUNASR_L2PF_DELAY");
+      fa::g_l2pf_delay = d ? std::max(0, atoi(d)) : 50;
+      const char* k = getenv("FUNASR_L2PF_MASK");
+      fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
+    }
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):

@@ -197,6 +197,20 @@ struct FusedDecodeWork {
   unsigned long long* gpart = nullptr; // [FUSED_MAX_M][FUSED_PARTS][ATTN_SPLITS][ATTN_PART_FLOATS] attention split
                                        // partials of the two-launch layer as granules (zeroed once)
 };
+// L2 prefetch of the batch-1 two-launch layer (llm.hip l2_prefetch): the bytes the blocks of the NEXT launches read,
+// pulled into the L2 of the XCD those blocks run on by extra blocks of the attention launch (its chain leaves HBM idle).
+// ffn_*: this layer's FFN launch; qkv_* / o_* / kc / vc: the next layer's attention launch (nullptr: none).
+struct L2Prefetch {
+  const int8_t *gq = nullptr, *uq = nullptr, *dq = nullptr;
+  const __half *gd = nullptr, *ud = nullptr, *dd = nullptr;
+  const int8_t *qkv_q = nullptr, *o_q = nullptr;
+  const __half *qkv_d = nullptr, *o_d = nullptr;
+  const __half *kc = nullptr, *vc = nullptr;
+  int F = 0;
+};
+extern int g_l2pf_blocks;  // L2 prefetch blocks per kv head in the batch-1 attention launch (0 = off)
+extern int g_l2pf_delay;   // their start delay, ticks of the 100 MHz clock
+extern int g_l2pf_mask;    // A/B: which byte sets they pull (1 FFN weights, 2 next attention weights, 4 next K/V)
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
                   const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,
@@ -207,7 +221,8 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s, int M = 1, int dbg_drop = 0);
+                      const FusedDecodeWork& fw, hipStream_t s, int M = 1, int dbg_drop = 0,
+                      const L2Prefetch* pf = nullptr);
 // M tokens (rows of x / xsum, slabs of the workspace); M = 1: the batch-1 layer
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,

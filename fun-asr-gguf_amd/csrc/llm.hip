@@ -229,6 +229,12 @@ struct RowGroup {
   float du[4][NCH];
 };
 
+// FA_LM_HEAD_NT = 0 (A/B builds only): the LM head's rows (EPI 3) with default-policy loads instead of nt, so that
+// they might stay in the Infinity Cache across steps. Graph-replayed batch-1 step (scripts/gpu_r4_l2pf.sh LMT=1):
+// 0.4695 vs 0.4740-0.4771 ms without the L2 prefetch blocks, 0.4600 vs 0.4537-0.4549 ms with them: nt stays.
+#ifndef FA_LM_HEAD_NT
+#define FA_LM_HEAD_NT 1
+#endif
 template <int NCH, int EPI>
 __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int r0, int lane, RowGroup<NCH, EPI>& G) {
   constexpr int K = NCH * 1024, NB = K / 32;
@@ -241,7 +247,10 @@ __device__ __forceinline__ void load_group(const GemvArgs& a, int row_base, int 
     const int row = min(row0, a.O - 1);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      G.w[rr][c] = ld_nt16(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
+      if (EPI == 3 && !FA_LM_HEAD_NT)
+        G.w[rr][c] = *reinterpret_cast<const int4*>(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
+      else
+        G.w[rr][c] = ld_nt16(a.wq + (int64_t)row * K + c * 1024 + lane * 16);
       const float dv = __half2float(a.wd[(int64_t)row * NB + c * 32 + (lane >> 1)]);
       G.dw[rr][c] = ok ? dv : 0.f;
       if (EPI == 2) {
@@ -2817,6 +2826,8 @@ struct AttnOArgs {
   unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
   int dbg_drop;        // test hook (fa_set_debug bit 1): block (0, 0) publishes no q|k|v granules -> fan-in timeout
   unsigned long long* gpart;  // FA_PART_GRANULE: [KV][ASPLIT][APART] split partials as granules {value, tag}
+  L2Prefetch pf;       // l2_prefetch (blockIdx.y >= ASPLIT; pf_blocks of them per kv head, token slab 0 only)
+  int pf_blocks, pf_delay, pf_mask;  // pf_mask (A/B): 1 the FFN weights, 2 the next q|k|v / o weights, 4 the next K/V
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
@@ -2864,6 +2875,71 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
   load_kv_groups<AKV_PRE, AWV>(vb, a.KV, g0, n_keys, lane >> 4, lane & 15, pv);
 }
 
+int g_l2pf_blocks = 16;
+int g_l2pf_delay = 50;
+int g_l2pf_mask = 7;
+
+// L2 prefetch blocks of the batch-1 two-launch layer (blockIdx.y >= ASPLIT of k_attn_o<true>, kv head g = blockIdx.x).
+// After its weight stream the attention launch is a latency chain (hand-offs, attention, split fan-in, o slice) that
+// leaves HBM idle for ~6 us. Extra blocks of the launch, dispatched after the 128 compute blocks and placed on XCD g
+// by the same round-robin (linear block id % 8), sleep pf_delay ticks and then pull into THIS XCD's L2 the bytes that
+// the next two launches' blocks on XCD g will read: the FFN launch's gate|up rows of blocks b = g + 8 i (rows
+// [12 b, +12)) and its down rows of slices bi = g + 8 j (all 8 groups: whole rows [32 bi, +32)); the next layer's
+// q|k|v rows of kv head g, the o columns [256 g, +256) and head g's K/V rows [0, pos]. LDS-DMA loads into a scratch slot
+// (no VGPR results), drained before the block ends. Bytes and results are untouched: a prefetch only moves lines.
+// nseg segments of SU 16-B units, STRIDE bytes apart (compile-time shape: the unit -> address map is a multiply-shift)
+template <int NSEG, int SU, int64_t STRIDE>
+__device__ __forceinline__ void pf_family(const void* base, int tid, int T, __attribute__((address_space(3))) void* lds) {
+  constexpr int U = NSEG * SU;
+  for (int u = tid; u < U; u += T) {
+    const int seg = u / SU, off = u - seg * SU;
+    __builtin_amdgcn_global_load_lds((const void*)((const char*)base + seg * STRIDE + (int64_t)off * 16), lds, 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb) {
+  __shared__ __attribute__((aligned(16))) int4 s_pf[AWV][64];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.pf_delay) __builtin_amdgcn_s_sleep(4);
+  const L2Prefetch& p = a.pf;
+  const int T = a.pf_blocks * AWV * 64, tid = pb * AWV * 64 + threadIdx.x;
+  auto* lds = (__attribute__((address_space(3))) void*)&s_pf[threadIdx.x >> 6][0];
+  // the Qwen3-0.6B shape the fused layer requires (host: qkv_attn_o_fused); FR / DR: FF_ROWS / FD_ROWS of the FFN
+  // launch (static_assert with their definitions below)
+  constexpr int D = 128, E = 1024, F = 3072, H = 16, KV = 8, FR = 12, DR = 32, NBF = F / FR;
+  constexpr int ER = E / 32 * 2, FRB = F / 32 * 2;  // scale bytes per row of K = E / K = F
+  if (a.pf_mask & 1) {  // the FFN launch (block b on XCD b % 8)
+    pf_family<NBF / 8, FR * E / 16, (int64_t)FR * 8 * E>(p.gq + (int64_t)FR * g * E, tid, T, lds);
+    pf_family<NBF / 8, FR * E / 16, (int64_t)FR * 8 * E>(p.uq + (int64_t)FR * g * E, tid, T, lds);
+    pf_family<NBF / 8, FR * ER / 16, (int64_t)FR * 8 * ER>((const char*)p.gd + (int64_t)FR * g * ER, tid, T, lds);
+    pf_family<NBF / 8, FR * ER / 16, (int64_t)FR * 8 * ER>((const char*)p.ud + (int64_t)FR * g * ER, tid, T, lds);
+    pf_family<E / DR / 8, DR * F / 16, (int64_t)DR * 8 * F>(p.dq + (int64_t)DR * g * F, tid, T, lds);
+    pf_family<E / DR / 8, DR * FRB / 16, (int64_t)DR * 8 * FRB>((const char*)p.dd + (int64_t)DR * g * FRB, tid, T, lds);
+  }
+  // the last layer (qkv_q == nullptr): the LM head comes next
+  if (p.qkv_q && (a.pf_mask & 2)) {  // the next layer's attention launch (kv head g's 16 blocks on XCD g)
+    const int rq = GQ * g * D, rk = (H + g) * D, rv = (H + KV + g) * D;
+    pf_family<1, GQ * D * E / 16, 0>(p.qkv_q + (int64_t)rq * E, tid, T, lds);
+    pf_family<1, D * E / 16, 0>(p.qkv_q + (int64_t)rk * E, tid, T, lds);
+    pf_family<1, D * E / 16, 0>(p.qkv_q + (int64_t)rv * E, tid, T, lds);
+    pf_family<1, GQ * D * ER / 16, 0>((const char*)p.qkv_d + (int64_t)rq * ER, tid, T, lds);
+    pf_family<1, D * ER / 16, 0>((const char*)p.qkv_d + (int64_t)rk * ER, tid, T, lds);
+    pf_family<1, D * ER / 16, 0>((const char*)p.qkv_d + (int64_t)rv * ER, tid, T, lds);
+    pf_family<E, GQ * D / 16, (int64_t)H * D>(p.o_q + GQ * D * g, tid, T, lds);
+    pf_family<E, GQ * D / 32 * 2 / 16, (int64_t)H * D / 32 * 2>((const char*)p.o_d + GQ * D * g / 32 * 2, tid, T, lds);
+  }
+  if (p.qkv_q && (a.pf_mask & 4)) {  // ... and its K/V rows [0, pos] of kv head g
+    const int pos = a.tok_pos[0], seq = a.tok_seq[0];
+    const int64_t kvo = (int64_t)seq * a.seq_stride + (int64_t)g * a.head_stride;
+    const int U = (pos + 1) * D * 2 / 16;
+    for (int u = tid; u < U; u += T) {
+      __builtin_amdgcn_global_load_lds((const void*)(p.kc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may land after the block's LDS is released
+}
+
 // QKV = true: the two-launch batch-1 layer. The 16 split blocks of kv head g first compute the 512 q|k|v rows that
 // head's attention reads (q heads GQ g .. GQ g + 1, k head g, v head g), FQ_ROWS each, with the prologue and the
 // arithmetic of k_gemv_q8<1, 1, true, 0, PS> (x = x_mid + sum dpart, rmsnorm + q8_0 in LDS, exact block dots, the
@@ -2877,6 +2953,10 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   constexpr int D = 128, FS = ASPLIT;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int g = blockIdx.x, sp = blockIdx.y, mt = blockIdx.z;
+  if (QKV && sp >= FS) {  // L2 prefetch blocks (batch 1 only: the host adds them to a one-token grid)
+    l2_prefetch(a0, g, sp - FS);
+    return;
+  }
   AttnOArgs a = a0;
   {
     const int nq = (a.H + 2 * a.KV) * D;
@@ -3188,7 +3268,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
                       const __half* wqkv_d, float* qkv, const float* qn, const float* kn, float eps, const float* rcos,
                       const float* rsin, __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos,
                       int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk,
-                      const FusedDecodeWork& fw, hipStream_t s, int M, int dbg_drop) {
+                      const FusedDecodeWork& fw, hipStream_t s, int M, int dbg_drop, const L2Prefetch* pf) {
   FA_REQUIRE(M >= 1 && M <= FUSED_MAX_M && M <= wk.max_split_tokens, "qkv_attn_o_fused: 1 <= M <= FUSED_MAX_M");
   FA_REQUIRE(H == KV * GQ && KV == FUSED_PARTS && E == FO_ROWS * ASPLIT && E == 1024 &&
                  (GQ + 2) * 128 == FQ_ROWS * ASPLIT,
@@ -3201,7 +3281,18 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
               fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop, fw.gpart};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   FA_REQUIRE(!FA_PART_GRANULE || fw.gpart, "qkv_attn_o_fused: partial granule workspace");
-  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, M), dim3(AWV * 64), 0, s, a);
+  int ny = ASPLIT;
+  if (pf && M == 1 && g_l2pf_blocks > 0) {
+    FA_REQUIRE(pf->F == 3072 && pf->gq && pf->uq && pf->dq && pf->gd && pf->ud && pf->dd &&
+                   (!pf->qkv_q || (pf->qkv_d && pf->o_q && pf->o_d && pf->kc && pf->vc)),
+               "qkv_attn_o_fused: L2 prefetch set");
+    a.pf = *pf;
+    a.pf_blocks = g_l2pf_blocks;
+    a.pf_delay = g_l2pf_delay;
+    a.pf_mask = g_l2pf_mask;
+    ny += g_l2pf_blocks;
+  }
+  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ny, M), dim3(AWV * 64), 0, s, a);
 }
 
 struct FfnArgs {
@@ -3232,6 +3323,7 @@ constexpr int FF_ROWS = 12;                        // gate|up rows per block (3 
 constexpr int FF_GROUP_BLOCKS = 32;                // blocks per down-projection group: 384 act rows = 12 q8_0 blocks
 constexpr int FF_GROUP_ROWS = FF_ROWS * FF_GROUP_BLOCKS;
 constexpr int FD_ROWS = 32;                        // down-projection rows per block (E / FF_GROUP_BLOCKS)
+static_assert(FF_ROWS == 12 && FD_ROWS == 32 && FF_GROUP_BLOCKS == 32, "l2_prefetch mirrors the FFN launch's row map");
 
 // CT tokens per block (small decode batches: CT = 2 from 4 tokens on, so every block's weights serve two tokens and
 // the token slabs fit the chip at once); tokens m0 = CT blockIdx.y .. m0 + ct - 1 (ct = min(CT, M - m0), block-uniform).

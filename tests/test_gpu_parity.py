@@ -577,6 +577,37 @@ def test_two_launch_layer_long_context():
         _check_step(l1[k], ref)
 
 
+def test_two_launch_layer_l2_prefetch_bit_identical(monkeypatch):
+    """The batch-1 attention launch's L2 prefetch blocks (FUNASR_L2PF, default 16 per kv head) only move lines into
+    the L2 of the XCDs that read them next: tokens and logits of 48 greedy steps (graph-replayed chunk and single
+    eager steps, n_past 300-348, both layers: layer 0 prefetches layer 1's attention inputs, the last layer only its
+    FFN weights) equal the run without them bit for bit."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(5)
+    prompt = (rng.standard_normal((300, 1024)) * 0.5).astype(np.float32)
+    runs = []
+    for pf in ("0", "16", "4"):
+        monkeypatch.setenv("FUNASR_L2PF", pf)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=512, max_seqs=2), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            eng.set_decode_fused(1)
+            eng.llm_reset(1)
+            toks = [eng.llm_prefill(1, prompt)]
+            toks += [int(t) for t in eng.llm_generate([1], 40)[0]]
+            lgs = [eng.llm_logits(1)]
+            for _ in range(8):
+                toks.append(int(eng.llm_generate([1], 1)[0][0]))
+                lgs.append(eng.llm_logits(1))
+            runs.append((toks, lgs))
+        finally:
+            eng.close()
+    for toks, lgs in runs[1:]:
+        assert toks == runs[0][0]
+        assert all(np.array_equal(a, b) for a, b in zip(lgs, runs[0][1]))
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
