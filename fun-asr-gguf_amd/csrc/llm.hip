@@ -2826,7 +2826,7 @@ struct AttnOArgs {
   unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
   int dbg_drop;        // test hook (fa_set_debug bit 1): block (0, 0) publishes no q|k|v granules -> fan-in timeout
   unsigned long long* gpart;  // FA_PART_GRANULE: [KV][ASPLIT][APART] split partials as granules {value, tag}
-  L2Prefetch pf;       // l2_prefetch (blockIdx.y >= ASPLIT; pf_blocks of them per kv head, token slab 0 only)
+  L2Prefetch pf;       // l2_prefetch (pf_blocks > 0: the last z slab, pf_blocks blocks per kv head)
   int pf_blocks, pf_delay, pf_mask;  // pf_mask (A/B): 1 the FFN weights, 2 the next q|k|v / o weights, 4 the next K/V
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
@@ -2877,9 +2877,11 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
 
 int g_l2pf_blocks = 16;
 int g_l2pf_delay = 50;
+int g_l2pf_max_m = 1;
 int g_l2pf_mask = 7;
 
-// L2 prefetch blocks of the batch-1 two-launch layer (blockIdx.y >= ASPLIT of k_attn_o<true>, kv head g = blockIdx.x).
+// L2 prefetch blocks of the two-launch layer (the last z slab of k_attn_o<true>, after the M token slabs: block
+// (g, pb) with pb < pf_blocks <= ASPLIT; kv head g = blockIdx.x).
 // After its weight stream the attention launch is a latency chain (hand-offs, attention, split fan-in, o slice) that
 // leaves HBM idle for ~6 us. Extra blocks of the launch, dispatched after the 128 compute blocks and placed on XCD g
 // by the same round-robin (linear block id % 8), sleep pf_delay ticks and then pull into THIS XCD's L2 the bytes that
@@ -2897,7 +2899,7 @@ __device__ __forceinline__ void pf_family(const void* base, int tid, int T, __at
   }
 }
 
-__device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb) {
+__device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb, int n_tok) {
   __shared__ __attribute__((aligned(16))) int4 s_pf[AWV][64];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.pf_delay) __builtin_amdgcn_s_sleep(4);
@@ -2929,12 +2931,14 @@ __device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb) {
     pf_family<E, GQ * D / 32 * 2 / 16, (int64_t)H * D / 32 * 2>((const char*)p.o_d + GQ * D * g / 32 * 2, tid, T, lds);
   }
   if (p.qkv_q && (a.pf_mask & 4)) {  // ... and its K/V rows [0, pos] of kv head g
-    const int pos = a.tok_pos[0], seq = a.tok_seq[0];
-    const int64_t kvo = (int64_t)seq * a.seq_stride + (int64_t)g * a.head_stride;
-    const int U = (pos + 1) * D * 2 / 16;
-    for (int u = tid; u < U; u += T) {
-      __builtin_amdgcn_global_load_lds((const void*)(p.kc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+    for (int m = 0; m < n_tok; ++m) {  // every token of the launch (its own sequence)
+      const int pos = a.tok_pos[m], seq = a.tok_seq[m];
+      const int64_t kvo = (int64_t)seq * a.seq_stride + (int64_t)g * a.head_stride;
+      const int U = (pos + 1) * D * 2 / 16;
+      for (int u = tid; u < U; u += T) {
+        __builtin_amdgcn_global_load_lds((const void*)(p.kc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may land after the block's LDS is released
@@ -2953,8 +2957,8 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   constexpr int D = 128, FS = ASPLIT;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int g = blockIdx.x, sp = blockIdx.y, mt = blockIdx.z;
-  if (QKV && sp >= FS) {  // L2 prefetch blocks (batch 1 only: the host adds them to a one-token grid)
-    l2_prefetch(a0, g, sp - FS);
+  if (QKV && a0.pf_blocks > 0 && mt == (int)gridDim.z - 1) {  // the L2 prefetch slab (after the M token slabs)
+    if (sp < a0.pf_blocks) l2_prefetch(a0, g, sp, mt);
     return;
   }
   AttnOArgs a = a0;
@@ -3281,18 +3285,18 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
               fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop, fw.gpart};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   FA_REQUIRE(!FA_PART_GRANULE || fw.gpart, "qkv_attn_o_fused: partial granule workspace");
-  int ny = ASPLIT;
-  if (pf && M == 1 && g_l2pf_blocks > 0) {
+  int nz = M;
+  if (pf && M <= g_l2pf_max_m && g_l2pf_blocks > 0) {
     FA_REQUIRE(pf->F == 3072 && pf->gq && pf->uq && pf->dq && pf->gd && pf->ud && pf->dd &&
                    (!pf->qkv_q || (pf->qkv_d && pf->o_q && pf->o_d && pf->kc && pf->vc)),
                "qkv_attn_o_fused: L2 prefetch set");
     a.pf = *pf;
-    a.pf_blocks = g_l2pf_blocks;
+    a.pf_blocks = std::min(g_l2pf_blocks, ASPLIT);
     a.pf_delay = g_l2pf_delay;
     a.pf_mask = g_l2pf_mask;
-    ny += g_l2pf_blocks;
+    nz += 1;
   }
-  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ny, M), dim3(AWV * 64), 0, s, a);
+  hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, nz), dim3(AWV * 64), 0, s, a);
 }
 
 struct FfnArgs {
