@@ -1190,6 +1190,14 @@ struct Engine {
       if (small) { a.x = lx; a.ldx = E; a.norm_w = w.attn_norm; }
       else if (nrm && l > 0) { a.xq = lxq; a.xd = lxd; a.ssp = d_ssp; }  // rows from the previous down epilogue
       else { prep_q8(lx, E, w.attn_norm, lc.rms_eps, M, E, lxq, lxd, stream); a.xq = lxq; a.xd = lxd; }
+      // batched decode: each split-K GEMM pulls the next one's weight rows into the reading XCDs' L2 (gemm_l2_prefetch)
+      const bool gpf = nrm && fa::g_gemm_pf;
+      auto set_pf = [&](GemvArgs& x, int bit, const Q8Mat& m, const Q8Mat* m2, int O, int K) {
+        if (!gpf || !(fa::g_gemm_pf & bit)) return;
+        x.pf_q = m.q; x.pf_d = m.d; x.pf_q2 = m2 ? m2->q : nullptr; x.pf_d2 = m2 ? m2->d : nullptr;
+        x.pf_O = O; x.pf_K = K; x.pf_slabs = fa::g_gemm_pf_slabs; x.pf_delay = fa::g_gemm_pf_delay;
+      };
+      set_pf(a, 8, w.o, nullptr, E, H * D);
       gemv(a, E, 0);
       {
         hipEvent_t ev;
@@ -1215,6 +1223,7 @@ struct Engine {
       if (small) { o.x = latt; o.ldx = H * D; }
       else { o.xq = lxq2; o.xd = lxd2; }
       if (nrm) { o.ssp_out = d_ssp; o.qout = lxq; o.dout = lxd; o.qn_w = w.ffn_norm; }
+      set_pf(o, 1, w.gate, &w.up, F, E);
       gemv(o, H * D, 1);
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
       GemvArgs g{};
@@ -1227,6 +1236,7 @@ struct Engine {
         else { prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream); g.xq = lxq; g.xd = lxd; }
         g.qout = lxq2; g.dout = lxd2;  // SwiGLU epilogue quantises act for the down GEMM (no prep launch)
       }
+      set_pf(g, 2, w.down, nullptr, E, F);
       gemv(g, E, 2);
       // x += Wdown . act
       GemvArgs dn{};
@@ -1239,6 +1249,7 @@ struct Engine {
         dn.ssp_out = d_ssp; dn.qout = lxq; dn.dout = lxd;
         dn.qn_w = l + 1 < lc.n_layer ? layers[l + 1].attn_norm : out_norm;
       }
+      if (l + 1 < lc.n_layer) set_pf(dn, 4, layers[l + 1].qkv, nullptr, QKV, E);
       gemv(dn, F, 1);
     }
     prof_sample = true;
@@ -1627,6 +1638,12 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_LM_TR")) fa::g_lm_tr = atoi(g) != 0;
     {  // process-wide decode-path knobs: re-read (or reset) at every engine creation
+      const char* gp = getenv("FUNASR_GEMM_PF");
+      fa::g_gemm_pf = gp ? atoi(gp) & 15 : 0;
+      const char* gs = getenv("FUNASR_GEMM_PF_SLABS");
+      fa::g_gemm_pf_slabs = gs ? std::min(8, std::max(1, atoi(gs))) : 1;
+      const char* gd = getenv("FUNASR_GEMM_PF_DELAY");
+      fa::g_gemm_pf_delay = gd ? std::max(0, atoi(gd)) : 100;
       const char* g = getenv("FUNASR_L2PF");
       // 16 blocks per kv head (one block per CU with the 128 compute blocks), after 0.5 us: graph-replayed batch-1
       // step 0.4537-0.4549 vs 0.4740-0.4784 ms (scripts/gpu_r4_l2pf.sh; 8 / 12 / 20 / 24 blocks and 1.0-2.5 us slower)

@@ -136,7 +136,15 @@ struct GemvArgs {
   // holds (fa_llm_prefill, and fa_llm_prefill_batch within the invariant width): every GEMM on the K-in-block MFMA
   // kernel, whose per-row result does not depend on the token count (no split-K, no 128-token tiles)
   int row_local;
+  // batched decode, split-K form only: extra grid slabs (pf_slabs) that pull the NEXT GEMM's weight rows ([pf_O][pf_K]
+  // q8_0, two matrices for SwiGLU) into the L2 of the XCD whose blocks will read them (gemm_l2_prefetch); nullptr: off
+  const int8_t* pf_q; const __half* pf_d; const int8_t* pf_q2; const __half* pf_d2;
+  int pf_O, pf_K, pf_slabs, pf_delay;
 };
+extern int g_gemm_pf;        // batched-decode GEMM L2 prefetch: bit 1 o -> gate|up, 2 gate|up -> down, 4 down -> next q|k|v,
+                             // 8 q|k|v -> o (0 = off)
+extern int g_gemm_pf_slabs;  // prefetch slabs per GEMM launch
+extern int g_gemm_pf_delay;  // their start delay, ticks of the 100 MHz clock
 void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int K, int8_t* xq, float* xd, hipStream_t s);
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
 int gemv_rows_per_wave(int O);

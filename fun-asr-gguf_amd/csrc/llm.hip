@@ -640,8 +640,45 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
 // rstd = 1/sqrtf(sum/K + eps) scales every block uniformly, so the q8_0 rows of y = (x * rstd) * w are the same
 // integers (up to float rounding at .5 ties) with scale f16(rstd * d_z): this GEMM only applies rstd, and the two
 // k_prep_q8 launches per layer (with their kernel boundaries) disappear.
+int g_gemm_pf = 0;
+int g_gemm_pf_slabs = 1;
+int g_gemm_pf_delay = 100;
+
+// L2 prefetch slabs of a batched-decode split-K GEMM (blockIdx.z >= KS): the next GEMM of the layer chain is split-K
+// too, with 32-row tiles x on XCD x % 8 (linear block id % 8, tile count a multiple of 8), so XCD g's blocks read
+// rows [32 x, +32) for x = g + 8 i in full (every K split of a tile shares its XCD). After pf_delay ticks (this launch's
+// own weights have landed) the prefetch blocks on XCD g pull those rows and their scales into g's L2 with LDS-DMA
+// loads into a scratch slot, drained before the block ends. Only lines move; no result changes.
+__device__ __forceinline__ void gemm_l2_prefetch(const GemvArgs& a, int KS) {
+  __shared__ __attribute__((aligned(16))) int4 s_pf[4][64];
+  const int nxy = gridDim.x * gridDim.y;
+  const int idx = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (blockIdx.z - KS));  // host: nxy % 8 == 0
+  const int g = idx & 7, pb = idx >> 3, P = nxy * (gridDim.z - KS) / 8;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.pf_delay) __builtin_amdgcn_s_sleep(4);
+  auto* lds = (__attribute__((address_space(3))) void*)&s_pf[threadIdx.x >> 6][0];
+  const int T = P * 256, tid = pb * 256 + threadIdx.x, K = a.pf_K;
+  for (int x = g; x < a.pf_O / 32; x += 8) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int8_t* q = m ? a.pf_q2 : a.pf_q;
+      const __half* d = m ? a.pf_d2 : a.pf_d;
+      if (!q) continue;
+      const char* qb = (const char*)(q + (int64_t)32 * x * K);  // 32 rows x K bytes
+      for (int u = tid; u < 2 * K; u += T) __builtin_amdgcn_global_load_lds((const void*)(qb + (int64_t)u * 16), lds, 16, 0, 0);
+      const char* db = (const char*)(d + (int64_t)32 * x * (K / 32));  // 32 rows x K / 32 f16 scales
+      for (int u = tid; u < K / 8; u += T) __builtin_amdgcn_global_load_lds((const void*)(db + (int64_t)u * 16), lds, 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may land after the block's LDS is released
+}
+
 template <int EPI, int NBW, int KSM, bool NRM = false>
 __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
+  if ((int)blockIdx.z >= KS) {  // L2 prefetch slabs (host: only with a.pf_q set)
+    gemm_l2_prefetch(a, KS);
+    return;
+  }
   constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
   constexpr int NS = EPI == 2 ? 2 : 1;
   static_assert(!NRM || EPI != 1, "k_gemm_q8_sk: NRM inputs feed q|k|v, gate|up and the LM head");
@@ -1471,7 +1508,8 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     FA_REQUIRE(a.kpart && a.kcnt && (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) <= a.kcnt_n &&
                    (int64_t)cdiv(a.O, 32) * cdiv(a.M, 32) * KS * (epi == 2 ? 2 : 1) * 1024 <= a.kpart_n,
                "gemm_q8: split-K workspace too small");
-  const dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
+  dim3 grid(cdiv(a.O, 32), cdiv(a.M, 32), KS);
+  if (a.pf_q && a.pf_slabs > 0 && grid.x % 8 == 0 && a.pf_O % 256 == 0 && a.pf_K % 128 == 0) grid.z += a.pf_slabs;
   const int ksm = KS == 1 ? 1 : KS <= 4 ? 4 : 16;
   if (a.ssp) {  // batched decode (M <= 32): inputs quantised by the previous residual epilogue, rstd applied here
     switch (epi * 1000 + NBW * 100 + ksm) {
