@@ -1638,12 +1638,15 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_LM_TR")) fa::g_lm_tr = atoi(g) != 0;
     {  // process-wide decode-path knobs: re-read (or reset) at every engine creation
+      // o -> gate|up, gate|up -> down, down -> next q|k|v with 4 slabs after 0.5 us: graph-replayed step at batch
+      // 8 / 16 / 24 / 32 1.145 / 1.163 / 1.228 / 1.241-1.246 -> 1.104 / 1.124 / 1.187 / 1.194 ms
+      // (profiles/r04_exp_gemm_pf.txt; q|k|v -> o across the attention launch: slower)
       const char* gp = getenv("FUNASR_GEMM_PF");
-      fa::g_gemm_pf = gp ? atoi(gp) & 15 : 0;
+      fa::g_gemm_pf = gp ? atoi(gp) & 15 : 7;
       const char* gs = getenv("FUNASR_GEMM_PF_SLABS");
-      fa::g_gemm_pf_slabs = gs ? std::min(8, std::max(1, atoi(gs))) : 1;
+      fa::g_gemm_pf_slabs = gs ? std::min(8, std::max(1, atoi(gs))) : 4;
       const char* gd = getenv("FUNASR_GEMM_PF_DELAY");
-      fa::g_gemm_pf_delay = gd ? std::max(0, atoi(gd)) : 100;
+      fa::g_gemm_pf_delay = gd ? std::max(0, atoi(gd)) : 50;
       const char* g = getenv("FUNASR_L2PF");
       // 16 blocks per kv head (one block per CU with the 128 compute blocks), after 0.5 us: graph-replayed batch-1
       // step 0.4537-0.4549 vs 0.4740-0.4784 ms (scripts/gpu_r4_l2pf.sh; 8 / 12 / 20 / 24 blocks and 1.0-2.5 us slower)

@@ -640,9 +640,9 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
 // rstd = 1/sqrtf(sum/K + eps) scales every block uniformly, so the q8_0 rows of y = (x * rstd) * w are the same
 // integers (up to float rounding at .5 ties) with scale f16(rstd * d_z): this GEMM only applies rstd, and the two
 // k_prep_q8 launches per layer (with their kernel boundaries) disappear.
-int g_gemm_pf = 0;
-int g_gemm_pf_slabs = 1;
-int g_gemm_pf_delay = 100;
+int g_gemm_pf = 7;
+int g_gemm_pf_slabs = 4;
+int g_gemm_pf_delay = 50;
 
 // L2 prefetch slabs of a batched-decode split-K GEMM (blockIdx.z >= KS): the next GEMM of the layer chain is split-K
 // too, with 32-row tiles x on XCD x % 8 (linear block id % 8, tile count a multiple of 8), so XCD g's blocks read

@@ -608,6 +608,32 @@ def test_two_launch_layer_l2_prefetch_bit_identical(monkeypatch):
         assert all(np.array_equal(a, b) for a, b in zip(lgs, runs[0][1]))
 
 
+def test_batched_decode_gemm_l2_prefetch_bit_identical(monkeypatch):
+    """The batched-decode split-K GEMMs' L2 prefetch slabs (FUNASR_GEMM_PF: o -> gate|up, gate|up -> down,
+    down -> next q|k|v, q|k|v -> o) only move lines: a batch of 12 sequences decodes 24 graph-replayed steps and one
+    eager step with the same tokens and logits as without them."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(8)
+    prompts = [(rng.standard_normal((40 + 9 * q, 1024)) * 0.5).astype(np.float32) for q in range(12)]
+    runs = []
+    for pf in ("0", "15"):
+        monkeypatch.setenv("FUNASR_GEMM_PF", pf)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=12), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            for q in range(12):
+                eng.llm_reset(q)
+                eng.llm_prefill(q, prompts[q])
+            toks = eng.llm_generate(list(range(12)), 24)
+            toks1 = eng.llm_generate(list(range(12)), 1)
+            runs.append((toks, toks1, [eng.llm_logits(q) for q in range(12)]))
+        finally:
+            eng.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
