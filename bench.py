@@ -584,8 +584,9 @@ def headline(args, world, dt, dt_prof, prof, stage):
     audio_s = CLIP_S * args.steps * world
     value = audio_s / dt
     ms_step = dt / args.steps * 1e3
-    # dominant kernel class by estimated device time: decoder layer classes are timed on layer 0 only
-    # (identical shapes in all layers), so their sampled ms stand for n_layer x as much device time
+    # dominant kernel class by estimated device time: decoder layer classes are timed on one layer only (layer 1:
+    # identical shapes in all layers, L2-warm weights from the prefetch slabs as in every layer but 0), so their
+    # sampled ms stand for n_layer x as much device time
     bf3 = os.environ.get("FUNASR_ENC_GEMM", "bf16x3") != "f32"
     enc_peak = BF16X3_PEAK_TFS if bf3 else FP32_MFMA_PEAK_TFS
     names = {0: "q8_0 GEMV/GEMM (decoder layers)",

@@ -1177,7 +1177,9 @@ struct Engine {
     }
     for (int l = 0; l < (fused ? 0 : lc.n_layer); ++l) {
       const LlmLayerW& w = layers[l];
-      prof_sample = l == 0;  // sampled timing: layer 0's launches stand for every layer (identical shapes)
+      // sampled timing: one layer's launches stand for every layer (identical shapes); layer 1, not 0: from layer 1 on
+      // the weights arrive L2-warm from the previous launches' prefetch slabs, and layer 0 also carries the first slabs
+      prof_sample = l == (lc.n_layer > 2 ? 1 : 0);
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       GemvArgs a{};
@@ -1297,7 +1299,7 @@ struct Engine {
     const int QKV = (H + 2 * KV) * D;
     for (int l = 0; l < lc.n_layer; ++l) {
       const LlmLayerW& w = layers[l];
-      prof_sample = l == 0;
+      prof_sample = l == (lc.n_layer > 2 ? 1 : 0);  // as in llm_forward
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       if (use_fused == 1) {
@@ -1311,6 +1313,12 @@ struct Engine {
           pf.qkv_q = wn.qkv.q; pf.qkv_d = wn.qkv.d; pf.o_q = wn.o.q; pf.o_d = wn.o.d;
           pf.kc = kcache + (size_t)(l + 1) * layer_stride;
           pf.vc = vcache + (size_t)(l + 1) * layer_stride;
+        }
+        if (M == 1 && fa::g_l2pf_lm > 0 && l >= lc.n_layer - fa::g_l2pf_lm) {  // the LM head's rows, in slices
+          const int nl = std::min(fa::g_l2pf_lm, lc.n_layer), j = l - (lc.n_layer - nl);
+          const int per = cdiv(lc.n_vocab, nl);
+          pf.lm_q = tok_embd.q; pf.lm_d = tok_embd.d;
+          pf.lm_row0 = j * per; pf.lm_rows = std::max(0, std::min(per, lc.n_vocab - j * per));
         }
         // a q8_0 weight-streaming layer launch (class 0, like C): algorithmic bytes = q|k|v + Wo weights + the K/V
         // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
@@ -1656,7 +1664,9 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* mm = getenv("FUNASR_L2PF_MAX_M");
       fa::g_l2pf_max_m = mm ? std::max(1, atoi(mm)) : 1;
       const char* k = getenv("FUNASR_L2PF_MASK");
-      fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
+      fa::g_l2pf_mask = k ? atoi(k) & 15 : 7;
+      const char* lm = getenv("FUNASR_L2PF_LM");
+      fa::g_l2pf_lm = lm ? std::max(0, atoi(lm)) : 0;
     }
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
