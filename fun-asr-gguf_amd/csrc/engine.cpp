@@ -1314,12 +1314,6 @@ struct Engine {
           pf.kc = kcache + (size_t)(l + 1) * layer_stride;
           pf.vc = vcache + (size_t)(l + 1) * layer_stride;
         }
-        if (M == 1 && fa::g_l2pf_lm > 0 && l >= lc.n_layer - fa::g_l2pf_lm) {  // the LM head's rows, in slices
-          const int nl = std::min(fa::g_l2pf_lm, lc.n_layer), j = l - (lc.n_layer - nl);
-          const int per = cdiv(lc.n_vocab, nl);
-          pf.lm_q = tok_embd.q; pf.lm_d = tok_embd.d;
-          pf.lm_row0 = j * per; pf.lm_rows = std::max(0, std::min(per, lc.n_vocab - j * per));
-        }
         // a q8_0 weight-streaming layer launch (class 0, like C): algorithmic bytes = q|k|v + Wo weights + the K/V
         // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
         hipEvent_t ev;
@@ -1664,9 +1658,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* mm = getenv("FUNASR_L2PF_MAX_M");
       fa::g_l2pf_max_m = mm ? std::max(1, atoi(mm)) : 1;
       const char* k = getenv("FUNASR_L2PF_MASK");
-      fa::g_l2pf_mask = k ? atoi(k) & 15 : 7;
-      const char* lm = getenv("FUNASR_L2PF_LM");
-      fa::g_l2pf_lm = lm ? std::max(0, atoi(lm)) : 0;
+      fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
     }
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;

@@ -215,11 +215,7 @@ struct L2Prefetch {
   const __half *qkv_d = nullptr, *o_d = nullptr;
   const __half *kc = nullptr, *vc = nullptr;
   int F = 0;
-  const int8_t* lm_q = nullptr;  // LM head rows [lm_row0, lm_row0 + lm_rows) ([V][1024] q8_0), split over the 8 XCDs
-  const __half* lm_d = nullptr;
-  int lm_row0 = 0, lm_rows = 0;
 };
-extern int g_l2pf_lm;      // the last this many layers' attention launches each prefetch 1 / this of the LM head
 extern int g_l2pf_blocks;  // L2 prefetch blocks per kv head in the two-launch attention launch (0 = off, <= 16)
 extern int g_l2pf_max_m;   // ... for decode batches up to this width
 extern int g_l2pf_delay;   // their start delay, ticks of the 100 MHz clock

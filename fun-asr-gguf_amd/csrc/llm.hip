@@ -2917,7 +2917,6 @@ int g_l2pf_blocks = 16;
 int g_l2pf_delay = 50;
 int g_l2pf_max_m = 1;
 int g_l2pf_mask = 7;
-int g_l2pf_lm = 0;
 
 // L2 prefetch blocks of the two-launch layer (the last z slab of k_attn_o<true>, after the M token slabs: block
 // (g, pb) with pb < pf_blocks <= ASPLIT; kv head g = blockIdx.x).
@@ -2945,7 +2944,6 @@ __device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb, i
   const L2Prefetch& p = a.pf;
   const int T = a.pf_blocks * AWV * 64, tid = pb * AWV * 64 + threadIdx.x;
   auto* lds = (__attribute__((address_space(3))) void*)&s_pf[threadIdx.x >> 6][0];
-  if (a.pf_mask & 8) g = (g + 1) & 7;  // A/B diagnostic: every XCD pulls its neighbour's bytes
   // the Qwen3-0.6B shape the fused layer requires (host: qkv_attn_o_fused); FR / DR: FF_ROWS / FD_ROWS of the FFN
   // launch (static_assert with their definitions below)
   constexpr int D = 128, E = 1024, F = 3072, H = 16, KV = 8, FR = 12, DR = 32, NBF = F / FR;
@@ -2980,17 +2978,6 @@ __device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb, i
         __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
       }
     }
-  }
-  if (p.lm_q) {  // a slice of the LM head's rows (row-major q8_0 + f16 scales), shared by the 8 XCDs' slabs
-    const int ta = pb * AWV * 64 + threadIdx.x, TA = T * 8;
-    const char* qb = (const char*)(p.lm_q + (int64_t)p.lm_row0 * E);
-    const int64_t UQ = (int64_t)p.lm_rows * E / 16;
-    for (int64_t u = (int64_t)ta * 8 + g; u < UQ; u += TA)
-      __builtin_amdgcn_global_load_lds((const void*)(qb + u * 16), lds, 16, 0, 0);
-    const char* db = (const char*)(p.lm_d + (int64_t)p.lm_row0 * (E / 32));
-    const int64_t UD = (int64_t)p.lm_rows * ER / 16;
-    for (int64_t u = (int64_t)ta * 8 + g; u < UD; u += TA)
-      __builtin_amdgcn_global_load_lds((const void*)(db + u * 16), lds, 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may land after the block's LDS is released
 }
