@@ -1302,18 +1302,18 @@ struct Engine {
       prof_sample = l == (lc.n_layer > 2 ? 1 : 0);  // as in llm_forward
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
-      // batch 1: extra blocks of the attention launch pull this layer's FFN weights and the next layer's attention
-      // weights / K/V rows into the L2 of the XCDs that will read them (llm.hip l2_prefetch)
-      fa::L2Prefetch pf;
-      pf.gq = w.gate.q; pf.gd = w.gate.d; pf.uq = w.up.q; pf.ud = w.up.d; pf.dq = w.down.q; pf.dd = w.down.d;
-      pf.F = F;
-      if (l + 1 < lc.n_layer) {
-        const LlmLayerW& wn = layers[l + 1];
-        pf.qkv_q = wn.qkv.q; pf.qkv_d = wn.qkv.d; pf.o_q = wn.o.q; pf.o_d = wn.o.d;
-        pf.kc = kcache + (size_t)(l + 1) * layer_stride;
-        pf.vc = vcache + (size_t)(l + 1) * layer_stride;
-      }
       if (use_fused == 1) {
+        // batch 1: extra blocks of the attention launch pull this layer's FFN weights and the next layer's attention
+        // weights / K/V rows into the L2 of the XCDs that will read them (llm.hip l2_prefetch)
+        fa::L2Prefetch pf;
+        pf.gq = w.gate.q; pf.gd = w.gate.d; pf.uq = w.up.q; pf.ud = w.up.d; pf.dq = w.down.q; pf.dd = w.down.d;
+        pf.F = F;
+        if (l + 1 < lc.n_layer) {
+          const LlmLayerW& wn = layers[l + 1];
+          pf.qkv_q = wn.qkv.q; pf.qkv_d = wn.qkv.d; pf.o_q = wn.o.q; pf.o_d = wn.o.d;
+          pf.kc = kcache + (size_t)(l + 1) * layer_stride;
+          pf.vc = vcache + (size_t)(l + 1) * layer_stride;
+        }
         // a q8_0 weight-streaming layer launch (class 0, like C): algorithmic bytes = q|k|v + Wo weights + the K/V
         // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
         hipEvent_t ev;
@@ -1344,7 +1344,7 @@ struct Engine {
         hipEvent_t ev;
         prof_begin(0, &ev);
         ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream,
-                  M, use_fused == 1 ? &pf : nullptr, d_tok_seq, d_tok_pos, seq_stride);
+                  M);
         prof_end(0, 3.0 * F * E * 34.0 / 32.0, 2.0 * 3.0 * M * F * E);
       }
     }
@@ -1659,8 +1659,6 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_l2pf_max_m = mm ? std::max(1, atoi(mm)) : 1;
       const char* k = getenv("FUNASR_L2PF_MASK");
       fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
-      const char* kc = getenv("FUNASR_L2PF_C");
-      fa::g_l2pf_c_blocks = kc ? std::max(0, atoi(kc)) : 0;
     }
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;

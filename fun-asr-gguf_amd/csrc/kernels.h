@@ -220,7 +220,6 @@ extern int g_l2pf_blocks;  // L2 prefetch blocks per kv head in the two-launch a
 extern int g_l2pf_max_m;   // ... for decode batches up to this width
 extern int g_l2pf_delay;   // their start delay, ticks of the 100 MHz clock
 extern int g_l2pf_mask;    // A/B: which byte sets they pull (1 FFN weights, 2 next attention weights, 4 next K/V)
-extern int g_l2pf_c_blocks;  // > 0: the FFN launch pulls the next attention bytes (2 | 4) with this many blocks per XCD
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
                   const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,
@@ -236,8 +235,7 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
 // M tokens (rows of x / xsum, slabs of the workspace); M = 1: the batch-1 layer
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
-               hipStream_t s, int M = 1, const L2Prefetch* pf = nullptr, const int* tok_seq = nullptr,
-               const int* tok_pos = nullptr, int64_t seq_stride = 0);
+               hipStream_t s, int M = 1);
 extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
 extern int g_gemm_bf3_256;    // bf16x3 GEMMs: 256x256 tiles when a launch has at least this many (0 = off)
 extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 4)

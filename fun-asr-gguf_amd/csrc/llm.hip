@@ -2833,15 +2833,6 @@ __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) 
 
 constexpr int FO_ROWS = 64;  // o-projection rows per split block (E / ASPLIT, E = 1024)
 
-// one launch's L2 prefetch slab (l2_prefetch): the byte sets, the token rows whose K/V it pulls, blocks per XCD
-struct PfLaunch {
-  L2Prefetch p;
-  const int* tok_pos;
-  const int* tok_seq;
-  int64_t seq_stride, head_stride;
-  int blocks, delay, mask;  // mask: 1 the FFN weights, 2 the next q|k|v / o weights, 4 the next K/V
-};
-
 struct AttnOArgs {
   const int* tok_seq;
   const int* tok_pos;
@@ -2873,7 +2864,8 @@ struct AttnOArgs {
   unsigned long long* gqkv;  // FA_QKV_GRANULE: [(H + 2 KV) D] 8-byte granules {value, tag} (zeroed once)
   int dbg_drop;        // test hook (fa_set_debug bit 1): block (0, 0) publishes no q|k|v granules -> fan-in timeout
   unsigned long long* gpart;  // FA_PART_GRANULE: [KV][ASPLIT][APART] split partials as granules {value, tag}
-  PfLaunch pf;         // l2_prefetch (pf.blocks > 0: the last z slab, pf.blocks blocks per kv head)
+  L2Prefetch pf;       // l2_prefetch (pf_blocks > 0: the last z slab, pf_blocks blocks per kv head)
+  int pf_blocks, pf_delay, pf_mask;  // pf_mask (A/B): 1 the FFN weights, 2 the next q|k|v / o weights, 4 the next K/V
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
@@ -2925,7 +2917,6 @@ int g_l2pf_blocks = 16;
 int g_l2pf_delay = 50;
 int g_l2pf_max_m = 1;
 int g_l2pf_mask = 7;
-int g_l2pf_c_blocks = 0;
 
 // L2 prefetch blocks of the two-launch layer (the last z slab of k_attn_o<true>, after the M token slabs: block
 // (g, pb) with pb < pf_blocks <= ASPLIT; kv head g = blockIdx.x).
@@ -2946,18 +2937,18 @@ __device__ __forceinline__ void pf_family(const void* base, int tid, int T, __at
   }
 }
 
-__device__ __forceinline__ void l2_prefetch(const PfLaunch& a, int g, int pb, int n_tok) {
+__device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb, int n_tok) {
   __shared__ __attribute__((aligned(16))) int4 s_pf[AWV][64];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.delay) __builtin_amdgcn_s_sleep(4);
-  const L2Prefetch& p = a.p;
-  const int T = a.blocks * AWV * 64, tid = pb * AWV * 64 + threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.pf_delay) __builtin_amdgcn_s_sleep(4);
+  const L2Prefetch& p = a.pf;
+  const int T = a.pf_blocks * AWV * 64, tid = pb * AWV * 64 + threadIdx.x;
   auto* lds = (__attribute__((address_space(3))) void*)&s_pf[threadIdx.x >> 6][0];
   // the Qwen3-0.6B shape the fused layer requires (host: qkv_attn_o_fused); FR / DR: FF_ROWS / FD_ROWS of the FFN
   // launch (static_assert with their definitions below)
   constexpr int D = 128, E = 1024, F = 3072, H = 16, KV = 8, FR = 12, DR = 32, NBF = F / FR;
   constexpr int ER = E / 32 * 2, FRB = F / 32 * 2;  // scale bytes per row of K = E / K = F
-  if (a.mask & 1) {  // the FFN launch (block b on XCD b % 8)
+  if (a.pf_mask & 1) {  // the FFN launch (block b on XCD b % 8)
     pf_family<NBF / 8, FR * E / 16, (int64_t)FR * 8 * E>(p.gq + (int64_t)FR * g * E, tid, T, lds);
     pf_family<NBF / 8, FR * E / 16, (int64_t)FR * 8 * E>(p.uq + (int64_t)FR * g * E, tid, T, lds);
     pf_family<NBF / 8, FR * ER / 16, (int64_t)FR * 8 * ER>((const char*)p.gd + (int64_t)FR * g * ER, tid, T, lds);
@@ -2966,7 +2957,7 @@ __device__ __forceinline__ void l2_prefetch(const PfLaunch& a, int g, int pb, in
     pf_family<E / DR / 8, DR * FRB / 16, (int64_t)DR * 8 * FRB>((const char*)p.dd + (int64_t)DR * g * FRB, tid, T, lds);
   }
   // the last layer (qkv_q == nullptr): the LM head comes next
-  if (p.qkv_q && (a.mask & 2)) {  // the next layer's attention launch (kv head g's 16 blocks on XCD g)
+  if (p.qkv_q && (a.pf_mask & 2)) {  // the next layer's attention launch (kv head g's 16 blocks on XCD g)
     const int rq = GQ * g * D, rk = (H + g) * D, rv = (H + KV + g) * D;
     pf_family<1, GQ * D * E / 16, 0>(p.qkv_q + (int64_t)rq * E, tid, T, lds);
     pf_family<1, D * E / 16, 0>(p.qkv_q + (int64_t)rk * E, tid, T, lds);
@@ -2977,7 +2968,7 @@ __device__ __forceinline__ void l2_prefetch(const PfLaunch& a, int g, int pb, in
     pf_family<E, GQ * D / 16, (int64_t)H * D>(p.o_q + GQ * D * g, tid, T, lds);
     pf_family<E, GQ * D / 32 * 2 / 16, (int64_t)H * D / 32 * 2>((const char*)p.o_d + GQ * D * g / 32 * 2, tid, T, lds);
   }
-  if (p.qkv_q && (a.mask & 4)) {  // ... and its K/V rows [0, pos] of kv head g
+  if (p.qkv_q && (a.pf_mask & 4)) {  // ... and its K/V rows [0, pos] of kv head g
     for (int m = 0; m < n_tok; ++m) {  // every token of the launch (its own sequence)
       const int pos = a.tok_pos[m], seq = a.tok_seq[m];
       const int64_t kvo = (int64_t)seq * a.seq_stride + (int64_t)g * a.head_stride;
@@ -3004,8 +2995,8 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   constexpr int D = 128, FS = ASPLIT;
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int g = blockIdx.x, sp = blockIdx.y, mt = blockIdx.z;
-  if (QKV && a0.pf.blocks > 0 && mt == (int)gridDim.z - 1) {  // the L2 prefetch slab (after the M token slabs)
-    if (sp < a0.pf.blocks) l2_prefetch(a0.pf, g, sp, mt);
+  if (QKV && a0.pf_blocks > 0 && mt == (int)gridDim.z - 1) {  // the L2 prefetch slab (after the M token slabs)
+    if (sp < a0.pf_blocks) l2_prefetch(a0, g, sp, mt);
     return;
   }
   AttnOArgs a = a0;
@@ -3337,8 +3328,10 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
     FA_REQUIRE(pf->F == 3072 && pf->gq && pf->uq && pf->dq && pf->gd && pf->ud && pf->dd &&
                    (!pf->qkv_q || (pf->qkv_d && pf->o_q && pf->o_d && pf->kc && pf->vc)),
                "qkv_attn_o_fused: L2 prefetch set");
-    a.pf = PfLaunch{*pf, tok_pos, tok_seq, seq_stride, seq_stride / KV, std::min(g_l2pf_blocks, ASPLIT), g_l2pf_delay,
-                    g_l2pf_c_blocks > 0 ? (g_l2pf_mask & 1) : g_l2pf_mask};
+    a.pf = *pf;
+    a.pf_blocks = std::min(g_l2pf_blocks, ASPLIT);
+    a.pf_delay = g_l2pf_delay;
+    a.pf_mask = g_l2pf_mask;
     nz += 1;
   }
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, nz), dim3(AWV * 64), 0, s, a);
@@ -3362,7 +3355,6 @@ struct FfnArgs {
   int* err;
   int E, F;
   const unsigned* epoch;  // the attention launch's fan-in counter of kv head 0: + ASPLIT per launch, never re-armed
-  PfLaunch pf;            // g_l2pf_c_blocks > 0 (batch 1): a trailing y slab pulls the next layer's attention bytes
 };
 // The group's act rows are handed over as data-tagged 8-byte granules {f32 value, tag} (one sc1 store each; tag = the
 // attention launch's epoch, new every layer and step), and each consumer polls the granules it needs until every tag
@@ -3382,10 +3374,6 @@ static_assert(FF_ROWS == 12 && FD_ROWS == 32 && FF_GROUP_BLOCKS == 32, "l2_prefe
 // and multiplied into the block's 32-row slice of the down projection. Same arithmetic for every CT.
 template <int CT>
 __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
-  if (f.pf.blocks > 0 && (int)blockIdx.y == (int)gridDim.y - 1) {  // the prefetch slab: block x on XCD x % 8
-    if ((int)blockIdx.x < 8 * f.pf.blocks) l2_prefetch(f.pf, blockIdx.x & 7, blockIdx.x >> 3, M);
-    return;
-  }
   constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
   const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
   const int m0 = blockIdx.y * CT, ct = min(CT, M - m0);
@@ -3568,24 +3556,17 @@ int g_ffn_pair_min_m = 4;  // decode batches from this width run the fused FFN w
 
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
-               hipStream_t s, int M, const L2Prefetch* pf, const int* tok_seq, const int* tok_pos, int64_t seq_stride) {
+               hipStream_t s, int M) {
   FA_REQUIRE(M >= 1 && M <= FUSED_MAX_M, "ffn_fused: 1 <= M <= FUSED_MAX_M");
   FA_REQUIRE(E == 1024 && F == FF_GROUP_ROWS * FUSED_PARTS && E == FD_ROWS * FF_GROUP_BLOCKS,
              "ffn_fused: Qwen3-0.6B FFN shape (E 1024, F 3072)");
   FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
   FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart,
             fw.cnt + FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.err, E, F, fw.cnt};
-  int ny = M >= g_ffn_pair_min_m ? cdiv(M, 2) : M;
-  if (pf && pf->qkv_q && M == 1 && g_l2pf_c_blocks > 0 && g_l2pf_blocks > 0) {
-    FA_REQUIRE(pf->qkv_d && pf->o_q && pf->o_d && pf->kc && pf->vc && 8 * g_l2pf_c_blocks <= F / FF_ROWS,
-               "ffn_fused: L2 prefetch set");
-    f.pf = PfLaunch{*pf, tok_pos, tok_seq, seq_stride, seq_stride / 8, g_l2pf_c_blocks, g_l2pf_delay, g_l2pf_mask & 6};
-    ny += 1;
-  }
   if (M >= g_ffn_pair_min_m)
-    hipLaunchKernelGGL(k_ffn_fused<2>, dim3(F / FF_ROWS, ny), dim3(256), 0, s, f, M);
+    hipLaunchKernelGGL(k_ffn_fused<2>, dim3(F / FF_ROWS, cdiv(M, 2)), dim3(256), 0, s, f, M);
   else
-    hipLaunchKernelGGL(k_ffn_fused<1>, dim3(F / FF_ROWS, ny), dim3(256), 0, s, f, M);
+    hipLaunchKernelGGL(k_ffn_fused<1>, dim3(F / FF_ROWS, M), dim3(256), 0, s, f, M);
 }
 
 }  // namespace fa
