@@ -611,6 +611,11 @@ def headline(args, world, dt, dt_prof, prof, stage):
                 per_launch=("q8_0 weight bytes (+ the two-launch layer's K/V rows)" if dom == 0 else
                             "q8_0 weight bytes" if dom == 4 else "algorithmic FLOPs"),
                 est_device_ms_per_step={names[c]: round(est_ms[c] / args.steps, 2) for c in prof})
+    if dom == 0 and roof.get("traffic"):
+        roof["traffic_note"] = ("FETCH_SIZE x 2 per decode-layer launch, graph path, newest profiles/*pmc_gemv*.json; "
+                                "with the prefetch slabs it counts the pulled bytes twice (the attention launch's pull "
+                                "for the next two launches and their own reads as seen under the profiler): HBM bytes "
+                                "per layer stay ~ the algorithmic 18.4 MB (DESIGN.md section 3)")
     # the encoder's MFMA classes (secondary: the clip's 705 GFLOP of f32 contractions) against the peak of the
     # arithmetic they run on: bf16x3 = three bf16 MFMA products per f32 product (2.5 PF/s / 3), or exact f32
     for c, key in ((1, "encoder_gemm"), (2, "encoder_attention")):
