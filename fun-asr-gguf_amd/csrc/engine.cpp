@@ -169,7 +169,9 @@ struct Engine {
   int graph_steps = 1;
   bool pf_row_local = false;  // the prefill forward being run is row-local (see llm_forward)
   int pf_rl_max = 1024;       // prompts longer than this prefill on the tiled forward, alone (FUNASR_PF_ROW_LOCAL_MAX)
-  int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after a fused fan-in timeout
+  int fused_retries = 0;     // chunks re-run on the fused layer after a fan-in timeout (exact: the same arithmetic)
+  int fused_recoveries = 0;  // chunks re-run on the 5-launch layer after the retry timed out too (not batch-exact)
+  int fused_fail_streak = 0; // consecutive chunks that needed the 5-launch layer; at kFusedGiveUp the engine keeps it
   int use_fused = 1;       // batch-1 layer: 1 two-launch (q|k|v + attention + o, FFN), 2 three-launch (q|k|v GEMV,
                            // attention + o, FFN), 0 the 5-launch layer every batch width uses (FUNASR_FUSED_DECODE)
   bool use_nrm = true;     // FUNASR_DECODE_NRM=0: batched decode keeps the k_prep_q8 launches (A/B)
@@ -183,9 +185,12 @@ struct Engine {
   // result gather over RCCL (fa_comm_*): this engine's communicator and its device staging buffers
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_world = 0;
-  int64_t* comm_sz = nullptr;  // [world]
+  int64_t* comm_sz = nullptr;  // [2 world]: the send slot + the gathered sizes (own allocation, reused across inits)
+  int comm_sz_n = 0;
   uint8_t* comm_buf = nullptr;  // send (cap) + receive (world x cap)
   int64_t comm_cap = 0;
+  // the communicator and its buffers (fa_comm_destroy; ~Engine for C-API users that never call it)
+  void comm_teardown();
 
   // profiling
   bool prof = false;
@@ -212,7 +217,13 @@ struct Engine {
     return (T*)p;
   }
   ~Engine() {
-    if (comm_buf) hipFree(comm_buf);
+    try {
+      comm_teardown();
+    } catch (...) {
+    }
+    if (comm_sz) hipFree(comm_sz);
+    if (hp_rowsrc) hipHostFree(hp_rowsrc);
+    if (ev_rowsrc) hipEventDestroy(ev_rowsrc);
     if (d_prow) hipFree(d_prow);
     for (auto& l : enc_lanes)
       if (l.s) hipStreamSynchronize(l.s);
@@ -404,6 +415,19 @@ struct Engine {
     r.N = N;
     r.K = K;
     r.row_set.assign(N, 0);
+  }
+  // an f32 write to (or unset of) elements [p, p + n) of a CTC-graph weight makes the int8 form of the rows it touches
+  // stale: those rows must be handed over again (fa_set_tensor_u8dq) before the int8 graph runs again
+  void u8_invalidate(const float* p, int64_t n) {
+    for (const float* w : ctc_regions) {
+      U8Region& r = u8w.at(w);
+      const int64_t lo = std::max<int64_t>(0, (p - w) / r.K), hi = std::min<int64_t>(r.N, (p + n - w + r.K - 1) / r.K);
+      for (int64_t i = lo; i < hi; ++i)
+        if (r.row_set[i]) {
+          r.row_set[i] = 0;
+          --r.n_set;
+        }
+    }
   }
   bool ctc_int8_active() const {
     if (!ctc_i8 || ctc_regions.empty()) return false;
@@ -1407,20 +1431,45 @@ struct Engine {
     FA_HIP(hipEventRecord(ev_gen, stream));
   }
 
-  // the landed chunk ran on the fused layer and a fan-in timed out: switch this engine to the 5-launch layer for good
-  // and decode the chunk again from the same host state (positions and input tokens were not advanced; the re-run
-  // overwrites the chunk's K/V rows before any step reads them, and its draws are keyed on the same (seed, seq, pos))
-  void recover_fused_chunk() {
-    log(3, "fused decode: an in-launch fan-in timed out (a group was not co-resident); re-running the chunk on the "
-           "5-launch layer and keeping it for this engine");
-    use_fused = 0;
-    debug_flags &= ~2;
+  // the landed chunk ran on the fused layer and a fan-in timed out (a group was not co-resident: another kernel or
+  // process held CUs). Decode the chunk again from the same host state (positions and input tokens were not advanced;
+  // a re-run overwrites the chunk's K/V rows before any step reads them, and its draws are keyed on the same (seed,
+  // seq, pos)): first on the fused layer again, which gives exactly the tokens an undisturbed chunk gives; only if that
+  // times out too, on the 5-launch layer for this chunk (agreeing to the q8_0 noise floor), and the next chunk probes
+  // the fused layer again. After kFusedGiveUp such chunks in a row the engine keeps the 5-launch layer.
+  static constexpr int kFusedGiveUp = 3;
+  void drop_step_graphs() {
     for (auto& g : step_graphs) FA_HIP(hipGraphExecDestroy(g.second));
-    step_graphs.clear();  // captured steps bake the layer structure in
-    ++fused_recoveries;
+    step_graphs.clear();  // captured steps bake the layer structure and the debug hook in
+  }
+  void rerun_chunk() {
     enqueue_steps(gen_seqs.data(), (int)gen_seqs.size(), gen_steps);
     FA_HIP(hipEventSynchronize(ev_gen));
+  }
+  void recover_fused_chunk() {
+    if ((debug_flags & 2) && !(debug_flags & 4)) {  // test hook: bit 1 withholds one hand-off once, bit 2 every time
+      debug_flags &= ~2;
+      drop_step_graphs();
+    }
+    ++fused_retries;
+    rerun_chunk();
+    if (!fused_error()) {
+      fused_fail_streak = 0;
+      log(2, "fused decode: an in-launch fan-in timed out; the chunk's re-run on the fused layer completed");
+      return;
+    }
+    ++fused_recoveries;
+    const bool give_up = ++fused_fail_streak >= kFusedGiveUp;
+    log(3, std::string("fused decode: the chunk's re-run timed out too; running it on the 5-launch layer") +
+               (give_up ? " and keeping that layer for this engine" : " (the next chunk probes the fused layer again)"));
+    const int fused_mode = use_fused;
+    use_fused = 0;
+    debug_flags &= ~6;
+    drop_step_graphs();
+    rerun_chunk();
     FA_REQUIRE(!fused_error(), "decode chunk re-run: error flag set on the 5-launch layer");
+    drop_step_graphs();
+    if (!give_up) use_fused = fused_mode;
   }
 
   // one prompt's prefill (fa_llm_prefill; also a long prompt of a row-local batch): row-local up to pf_rl_max rows (a
@@ -1445,12 +1494,29 @@ struct Engine {
       }
       return;
     }
-    std::vector<int32_t> c;
-    for (const auto& p : parts) c.insert(c.end(), src.codes + p.first, src.codes + p.first + p.second);
-    FA_REQUIRE((int64_t)c.size() <= pf_max, "prompt rows exceed the row capacity");
-    FA_HIP(hipMemcpyAsync(d_rowsrc, c.data(), c.size() * 4, hipMemcpyHostToDevice, stream));
-    fa::prompt_rows(d_prow, ad, last_tstride, d_rowsrc, (int)c.size(), E, lx, stream);
+    int64_t n = 0;
+    for (const auto& p : parts) n += p.second;
+    FA_REQUIRE(n <= pf_max, "prompt rows exceed the row capacity");
+    // the codes go through an engine-owned pinned buffer: the copy may still be queued when this call returns, so
+    // the source must outlive it (rewritten only after the event of its last copy)
+    if (!hp_rowsrc) {
+      FA_HIP(hipHostMalloc(reinterpret_cast<void**>(&hp_rowsrc), (size_t)std::max<int64_t>(pf_max, 1) * 4,
+                           hipHostMallocDefault));
+      FA_HIP(hipEventCreateWithFlags(&ev_rowsrc, hipEventDisableTiming));
+    } else {
+      FA_HIP(hipEventSynchronize(ev_rowsrc));
+    }
+    int64_t r = 0;
+    for (const auto& p : parts) {
+      std::memcpy(hp_rowsrc + r, src.codes + p.first, (size_t)p.second * 4);
+      r += p.second;
+    }
+    FA_HIP(hipMemcpyAsync(d_rowsrc, hp_rowsrc, (size_t)n * 4, hipMemcpyHostToDevice, stream));
+    FA_HIP(hipEventRecord(ev_rowsrc, stream));
+    fa::prompt_rows(d_prow, ad, last_tstride, d_rowsrc, (int)n, E, lx, stream);
   }
+  int32_t* hp_rowsrc = nullptr;  // pinned staging of the prompt row codes (load_prompt_rows)
+  hipEvent_t ev_rowsrc = nullptr;
 
   void prefill_one(int seq, const PromptSrc& src, int64_t off, int n_tokens, int32_t* tok_out, float* logits_out) {
     load_prompt_rows(src, {{off, n_tokens}});
@@ -1660,6 +1726,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* k = getenv("FUNASR_L2PF_MASK");
       fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
     }
+    if (const char* g = getenv("FUNASR_AB_FULL")) fa::g_ab_full_keys = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
@@ -1700,6 +1767,8 @@ int fa_weights_synthetic(fa_engine* h, uint32_t seed) {
   FA_API_BEGIN
   h->e->synthetic(seed);
   h->e->weights_changed();
+  for (auto& kv : h->e->slots)
+    if (kv.second.kind == 0) h->e->u8_invalidate(kv.second.f, kv.second.n);
   FA_API_END
 }
 
@@ -1711,6 +1780,7 @@ int fa_set_tensor_f32(fa_engine* h, const char* name, const float* host, int64_t
   if (s.kind == 0) {
     FA_HIP(hipMemcpyAsync(s.f, host, n * 4, hipMemcpyHostToDevice, e->stream));
     e->weights_changed();
+    e->u8_invalidate(s.f, s.n);
   } else {
     float* tmp = nullptr;
     FA_HIP(hipMalloc(&tmp, n * 4));
@@ -1768,7 +1838,10 @@ int fa_weights_mark_unset(fa_engine* h, const char* prefix) {
   FA_API_BEGIN
   const std::string p = prefix ? prefix : "";
   for (auto& kv : h->e->slots)
-    if (kv.first.compare(0, p.size(), p) == 0) kv.second.set = false;
+    if (kv.first.compare(0, p.size(), p) == 0) {
+      kv.second.set = false;
+      if (kv.second.kind == 0) h->e->u8_invalidate(kv.second.f, kv.second.n);
+    }
   FA_API_END
 }
 
@@ -2262,6 +2335,14 @@ int fa_llm_invariant_width(fa_engine* h, int32_t* out) {
   FA_API_END
 }
 
+int fa_llm_decode_recoveries(fa_engine* h, int32_t* retries, int32_t* fallbacks) {
+  FA_API_BEGIN
+  FA_REQUIRE(retries && fallbacks, "fa_llm_decode_recoveries: outputs");
+  *retries = h->e->fused_retries;
+  *fallbacks = h->e->fused_recoveries;
+  FA_API_END
+}
+
 int fa_llm_set_token(fa_engine* h, int32_t seq, int32_t token) {
   FA_API_BEGIN
   Engine* e = h->e;
@@ -2372,10 +2453,16 @@ int fa_comm_init(fa_engine* h, int32_t rank, int32_t world, const uint8_t* id) {
   FA_HIP(hipSetDevice(e->device));
   ncclUniqueId uid;
   std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+  if (e->comm_sz_n < 2 * world) {
+    if (e->comm_sz) FA_HIP(hipFree(e->comm_sz));
+    e->comm_sz = nullptr;
+    e->comm_sz_n = 0;
+    FA_HIP(hipMalloc(&e->comm_sz, (size_t)2 * world * sizeof(int64_t)));
+    e->comm_sz_n = 2 * world;
+  }
   FA_NCCL(rccl().comm_init_rank(&e->comm, world, uid, rank));
   e->comm_rank = rank;
   e->comm_world = world;
-  e->comm_sz = e->alloc<int64_t>(2 * world);
   FA_API_END
 }
 
@@ -2412,17 +2499,23 @@ int fa_comm_allgather_bytes(fa_engine* h, const uint8_t* data, int64_t n, int64_
   FA_API_END
 }
 
+void fa::Engine::comm_teardown() {
+  if (comm) {
+    FA_HIP(hipStreamSynchronize(stream));
+    const ncclComm_t c = comm;
+    comm = nullptr;
+    FA_NCCL(rccl().comm_destroy(c));
+  }
+  comm_rank = 0;
+  comm_world = 0;
+  if (comm_buf) FA_HIP(hipFree(comm_buf));
+  comm_buf = nullptr;
+  comm_cap = 0;
+}
+
 int fa_comm_destroy(fa_engine* h) {
   FA_API_BEGIN
-  Engine* e = h->e;
-  if (e->comm) {
-    FA_HIP(hipStreamSynchronize(e->stream));
-    FA_NCCL(rccl().comm_destroy(e->comm));
-    e->comm = nullptr;
-  }
-  if (e->comm_buf) FA_HIP(hipFree(e->comm_buf));
-  e->comm_buf = nullptr;
-  e->comm_cap = 0;
+  h->e->comm_teardown();
   FA_API_END
 }
 

@@ -23,7 +23,7 @@ EXPORTS = [
     "fa_weights_mark_unset", "fa_tensor_names", "fa_llm_set_token",
     "fa_llm_invariant_width", "fa_set_encode_mode", "fa_ctc_head", "fa_set_tensor_u8dq", "fa_set_ctc_int8",
     "fa_ctc_int8_active", "fa_comm_unique_id", "fa_comm_init", "fa_comm_allgather_sizes", "fa_comm_allgather_bytes",
-    "fa_comm_destroy", "fa_llm_prefill_rows", "fa_encode_generation",
+    "fa_comm_destroy", "fa_llm_prefill_rows", "fa_encode_generation", "fa_llm_decode_recoveries",
 ]
 
 
@@ -104,6 +104,7 @@ def load():
     lib.fa_llm_logits.argtypes = [P, I32, P]
     lib.fa_llm_set_token.argtypes = [P, I32, I32]
     lib.fa_llm_invariant_width.argtypes = [P, ctypes.c_void_p]
+    lib.fa_llm_decode_recoveries.argtypes = [P, P, P]
     lib.fa_llm_n_past.argtypes = [P, I32, P]
     lib.fa_profile_enable.argtypes = [P, I32]
     lib.fa_profile_read.argtypes = [P, I32, P, P, P, P]
@@ -464,6 +465,13 @@ class Engine:
         v = ctypes.c_int32()
         _check(self.lib.fa_llm_invariant_width(self.h, ctypes.byref(v)), "fa_llm_invariant_width")
         return v.value
+
+    def llm_decode_recoveries(self):
+        """(retries, fallbacks): decode chunks re-run on the fused layer after an in-launch timeout (results unchanged)
+        and chunks that ran on the 5-launch layer instead (noise-floor agreement only); fa_llm_decode_recoveries."""
+        r, f = ctypes.c_int32(), ctypes.c_int32()
+        _check(self.lib.fa_llm_decode_recoveries(self.h, ctypes.byref(r), ctypes.byref(f)), "fa_llm_decode_recoveries")
+        return r.value, f.value
 
     def llm_set_token(self, seq, token):
         """Feed `token` as the sequence's next generate input instead of its own last draw (teacher forcing)."""

@@ -89,6 +89,8 @@ class ContinuousBatcher:
         # single-sequence arithmetic: results are exactly the one-clip-at-a-time results, whatever the grouping
         alone = S <= invariant_width(eng)
         invariance_lost = False
+        rec = getattr(eng, "llm_decode_recoveries", None)
+        fallbacks0 = rec()[1] if rec else 0
         n_admit = n_encode_batches = 0
         t_enc = t_pre = t_wait = 0.0
         self.n_chunks = 0
@@ -98,15 +100,18 @@ class ContinuousBatcher:
         enc_cap = eng.max_batch if hasattr(eng, "max_batch") else S
 
         def check_width():
-            # the engine's invariant width can drop during the run (a fused fan-in timeout moves it to the 5-launch
-            # layer for good, fa_llm_invariant_width 6 -> 1): later batches are then no longer bit-identical to
-            # one-clip decoding. Re-read before every admission and decode chunk; say so once, in stats and a warning
+            # a fused fan-in timeout is re-run on the fused layer (exact); only when that times out too does the chunk
+            # run on the 5-launch layer (fa_llm_decode_recoveries counts it), and after three such chunks in a row the
+            # engine keeps that layer (fa_llm_invariant_width 6 -> 1). Either way results from there on are no longer
+            # bit-identical to one-clip decoding. Re-read before every admission and decode chunk; say so once, in
+            # stats and a warning
             nonlocal alone, invariance_lost
-            if alone and S > invariant_width(eng):
+            fell_back = bool(rec) and rec()[1] > fallbacks0
+            if alone and (S > invariant_width(eng) or fell_back):
                 alone, invariance_lost = False, True
-                warnings.warn(f"decode batches of {S} now exceed the engine's invariant width "
-                              f"({invariant_width(eng)}): results from here on agree with one-clip decoding to the "
-                              "q8_0 noise floor, not bit for bit", RuntimeWarning)
+                warnings.warn(f"decode batches of {S}: a decode chunk ran on the 5-launch layer (fused-layer timeouts; "
+                              f"invariant width now {invariant_width(eng)}): results from here on agree with one-clip "
+                              "decoding to the q8_0 noise floor, not bit for bit", RuntimeWarning)
 
         def encode_ahead(need):
             # clips are encoded ahead of their admission in encoder batches of the engine's full capacity (a padded

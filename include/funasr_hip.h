@@ -149,6 +149,9 @@ int fa_set_encoder_gemm(fa_engine* e, int32_t mode);
  * bit-identical to 1); 0 = the 5-launch layer (what wider batches always use). Same numerics contract (ggml q8_0),
  * different f32 summation order of the o / down projections between 0 and 1/2. */
 int fa_set_decode_fused(fa_engine* e, int32_t on);
+/* Test hooks: bit 0 taps the LFR rows of the next encode (fa_encode_tap); bit 1 makes one block of the fused attention
+ * launch withhold its q|k|v hand-off in the next decode chunk (a forced fan-in timeout, cleared by the recovery); bit 2
+ * with bit 1 keeps withholding it (the fused re-run times out too). */
 int fa_set_debug(fa_engine* e, int32_t flags);
 int fa_encode_tap(fa_engine* e, int32_t which, float* out, int64_t n);
 
@@ -206,6 +209,12 @@ int fa_llm_logits(fa_engine* e, int32_t seq, float* out);
  * width, each prefilled alone, produce exactly their single-sequence tokens. Wider batches agree to the q8_0 noise
  * floor. */
 int fa_llm_invariant_width(fa_engine* e, int32_t* out);
+/* Fused-layer timeout recoveries of this engine (llm.hip k_attn_o / k_ffn_fused bound every in-launch wait): *retries =
+ * decode chunks re-run on the fused layer after a fan-in timed out (same arithmetic: results unchanged); *fallbacks =
+ * chunks whose re-run timed out too and ran on the 5-launch layer (agreeing with single-sequence decoding to the q8_0
+ * noise floor, not bit for bit). Three fallbacks in a row keep the 5-launch layer (fa_llm_invariant_width drops to 1);
+ * otherwise the next chunk runs the fused layer again. No reference counterpart (llama.cpp has no in-launch waits). */
+int fa_llm_decode_recoveries(fa_engine* e, int32_t* retries, int32_t* fallbacks);
 /* Make `token` the input of the sequence's next generate step in place of the token it sampled last: the
  * caller-chosen token of the reference loop's llama_decode(batch{token, pos}) (decoder.py:91-98, llama.py:490-498),
  * used for teacher-forced parity runs. */

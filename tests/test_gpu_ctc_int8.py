@@ -99,3 +99,26 @@ def test_int8_ctc_batch_and_lanes_per_clip(i8):
         _check_ids(one["ctc_ids"][0], ref_ids, ref_lg, f"clip {b} single")
         ref_ids, ref_lg = oi8.ctc_ids_int8(out["enc"][b], W, Q, synth.ENC_FULL)
         _check_ids(out["ctc_ids"][b], ref_ids, ref_lg, f"clip {b} in the padded batch")
+
+
+def test_int8_ctc_invalidated_by_f32_writes(i8):
+    """An f32 write to a CTC weight (fa_set_tensor_f32) or an unset of it (fa_weights_mark_unset) makes that weight's
+    int8 form stale: the CTC head leaves the int8 graph (f32 again, bit for bit) until the weight is handed over as
+    int8 again (the head must not keep running the old int8 weights)."""
+    e, W, Q, ref_f32 = i8
+    g = np.load(os.path.join(GOLDEN, "encoder_full_10s.npz"))
+    int8_ids = e.ctc_head(g["enc"])
+    name = next(iter(Q))
+    try:
+        e.set_tensor(name + ".weight", W[name + ".weight"])
+        assert not e.ctc_int8_active()
+        assert np.array_equal(e.ctc_head(g["enc"]), ref_f32)
+        e.set_tensor_u8dq(name + ".weight", *Q[name])
+        assert e.ctc_int8_active()
+        e.mark_unset(name + ".weight")
+        assert not e.ctc_int8_active()
+    finally:
+        e.set_tensor(name + ".weight", W[name + ".weight"])
+        e.set_tensor_u8dq(name + ".weight", *Q[name])
+    assert e.ctc_int8_active()
+    assert np.array_equal(e.ctc_head(g["enc"]), int8_ids)

@@ -7,7 +7,8 @@ Oracles:
   * oracle/cref (C++/OpenMP restatement, pinned in tests/test_cref.py to those goldens and to the numpy oracle)
     for the decoder at full dims and for clips no golden holds (batch of 32, C4 segments);
   * oracle/encoder_fp16 (numpy) for the fp16 graph (configs[4]).
-Tolerances as test_gpu_parity.py: encoder fp32 max-abs/max <= 5e-4 and cosine >= 0.99999 (full depth); CTC ids
+Tolerances as test_gpu_parity.py: encoder fp32 max-abs/max <= 1e-4 and cosine >= 0.999999 at full depth (SURVEY §8(c),
+experience/03 ONNX_Export_Optimization_Experience.md:68-73; measured 1.6e-5 bf16x3, 1.7e-6 exact f32); CTC ids
 exact where the top-1/top-2 margin exceeds 1e-3; decoder teacher-forced logits cosine >= 0.9995 with equal argmax
 where the oracle's top-2 margin exceeds 0.25 (q8_0 activation rounding noise, tests/test_oracle_golden.py).
 """
@@ -23,7 +24,8 @@ from oracle import cref, ctc as octc, synth
 pytestmark = pytest.mark.gpu
 
 SR = 16000
-ENC_ATOL = 5e-4
+ENC_ATOL = 1e-4
+ENC_COS = 0.999999
 TIE_MARGIN = 0.25
 
 
@@ -79,9 +81,12 @@ def g60():
 
 
 def _check_encoder(out_enc, out_emb, out_ids, ref_enc, ref_emb, ref_ids, margin, tag):
-    assert _rel(out_enc, ref_enc) < ENC_ATOL and _cos(out_enc, ref_enc) > 0.99999, tag
+    e_enc, c_enc, e_emb, c_emb = _rel(out_enc, ref_enc), _cos(out_enc, ref_enc), None, None
     assert out_emb.shape == ref_emb.shape, tag
-    assert _rel(out_emb, ref_emb) < ENC_ATOL and _cos(out_emb, ref_emb) > 0.99999, tag
+    e_emb, c_emb = _rel(out_emb, ref_emb), _cos(out_emb, ref_emb)
+    print(f"{tag}: enc max-abs/max {e_enc:.2e} cos {c_enc:.8f}; adaptor max-abs/max {e_emb:.2e} cos {c_emb:.8f}")
+    assert e_enc < ENC_ATOL and c_enc > ENC_COS, tag
+    assert e_emb < ENC_ATOL and c_emb > ENC_COS, tag
     bad = (out_ids != ref_ids) & (margin > 1e-3)
     assert bad.sum() == 0, f"{tag}: {int(bad.sum())} non-tie CTC ids differ"
 
@@ -491,13 +496,15 @@ def test_continuous_batching_slot_reuse_equals_per_clip():
         api.cleanup()
 
 
-def test_llm_full_slot_reuse_above_width_bound(eng, g60):
+def test_llm_full_slot_reuse_above_width_bound(eng, cllm, g60):
     """Slot reuse above the invariant width (configs[2] shape): 40 ragged prompts on 32 slots. Slots 0-31 are prefilled
     as one batch; the first 8 clips stop after 8 steps, and their slots take clips 32-39 (one 8-prompt admission
     prefill while 24 sequences are mid-decode, slots reset and reused with their stale K/V rows still in the cache);
     then every slot decodes together, in admission order. 16 steps per clip, teacher-forced on each clip's single-stream
     tokens: the batch-32 bound of test_llm_full_batch32_vs_single_streams_bound (cosine >= 0.9995, equal argmax where
-    the single-stream top-2 margin exceeds 0.15)."""
+    the single-stream top-2 margin exceeds 0.15). The two clips on the first and last reused slot (32 on slot 0, 39 on
+    slot 7: the stale K/V rows of clips 0 and 7 still in their caches past the new prompts) are also checked
+    teacher-forced against the oracle (cref) fed the same tokens, not only against the GPU's own single-stream run."""
     adaptor = g60["adaptor"].astype(np.float32)
     base = _bench_prompts(eng, adaptor, 40)
     prompts = [p[:204 - 3 * (i % 7)] if i % 7 else p for i, p in enumerate(base)]  # ragged: 186-204 rows
@@ -512,10 +519,13 @@ def test_llm_full_slot_reuse_above_width_bound(eng, g60):
         slot_of[c], k_of[c] = c, 0
         order.append(c)
     worst = 1.0
+    kept = {32: [], 39: []}  # reused slots' logits per step, for the oracle check
 
     def check(c):
         nonlocal worst
         lg, ref = eng.llm_logits(slot_of[c]), single[c][1][k_of[c]]
+        if c in kept:
+            kept[c].append(lg)
         cs = _cos(lg, ref)
         worst = min(worst, cs)
         assert cs >= 0.9995, f"clip {c} step {k_of[c]}: cosine {cs}"
@@ -547,6 +557,12 @@ def test_llm_full_slot_reuse_above_width_bound(eng, g60):
             admitted = True
     assert admitted and all(k_of[c] == n_steps[c] for c in range(40))
     print(f"slot reuse above the width: worst cosine {worst:.6f}")
+    for c, lgs in kept.items():
+        assert len(lgs) == K + 1 and slot_of[c] in (0, 7)
+        toks = single[c][0]
+        _check_step(lgs[0], cllm.forward(prompts[c], 0))
+        for k in range(K):
+            _check_step(lgs[k + 1], cllm.forward(cllm.embed_tokens([toks[k]]), prompts[c].shape[0] + k))
 
 
 def test_long_prompt_prefilled_alone_in_row_local_batch(monkeypatch):
@@ -583,7 +599,8 @@ def test_prefill_rows_assembled_on_device_equal_host_prompts(eng):
     """fa_llm_prefill_rows (prompt rows assembled in HBM from the caller's prefix / suffix rows and the last encode's
     adaptor rows, core/decoder.PromptRows) against the reference's host concatenation (core/decoder.py:199) through
     fa_llm_prefill / fa_llm_prefill_batch: first tokens and last-row logits bit-identical for one prompt, a row-local
-    batch of 3 and a tiled batch of 8 (above the invariant width); a later encode invalidates the rows (loud failure,
+    batch of 3 (from a padded-batch encode and from independent-clip lanes, whose adaptor rows sit at another row
+    stride) and a tiled batch of 8 (above the invariant width); a later encode invalidates the rows (loud failure,
     and prefill_group falls back to the host rows)."""
     from fun_asr_gguf.core.decoder import PromptRows, prefill_group
     from fun_asr_gguf.synthetic import synth_audio
@@ -592,8 +609,8 @@ def test_prefill_rows_assembled_on_device_equal_host_prompts(eng):
     pre = [eng.embd_rows(rng.integers(0, 151933, 73).astype(np.int32)) for _ in range(2)]
     suf = eng.embd_rows(rng.integers(0, 151933, 5).astype(np.int32))
 
-    def run(n):
-        out = eng.encode(clips[:n])
+    def run(n, independent=False):
+        out = eng.encode(clips[:n], independent=independent)
         gen = out["enc_gen"]
         assert gen >= 0 and gen == eng.encode_generation()
         rows = [PromptRows(pre[b % 2], out["audio_embd"][b], suf, b, gen) for b in range(n)]
@@ -618,6 +635,7 @@ def test_prefill_rows_assembled_on_device_equal_host_prompts(eng):
 
     run(1)
     run(3)
+    run(3, independent=True)  # lane layout (the scheduler's front(independent=alone)): clip b's rows at b * tl_max
     rows = run(8)
     eng.encode(clips[:1])  # replaces the adaptor rows the PromptRows point at
     for s in range(8):

@@ -1,7 +1,8 @@
 """GPU parity: the HIP engine (through the C-ABI) against the CPU oracle and the reference goldens.
 
 Tolerances (written here, per SURVEY §8(c) / experience/03 ONNX_Export_Optimization_Experience.md:68-73):
-  encoder/adaptor fp32: max-abs <= ENC_ATOL_* relative to the tensor's max, cosine >= 0.99999
+  encoder/adaptor fp32: max-abs <= ENC_ATOL_* relative to the tensor's max, cosine >= 0.99999 (tiny configs), >= 0.999999
+  at full depth (ENC_ATOL_FULL)
   CTC ids: exact on frames whose top-1/top-2 logit margin exceeds 1e-3 (non-tie frames)
   decoder (q8_0 integer-dot numerics on both sides): logits cosine >= 0.9999, greedy ids equal
 """
@@ -16,7 +17,7 @@ from oracle import ctc as octc, encoder as oenc, frontend as ofe, q8 as oq8, qwe
 pytestmark = pytest.mark.gpu
 
 ENC_ATOL_TINY = 5e-5
-ENC_ATOL_FULL = 5e-4
+ENC_ATOL_FULL = 1e-4  # max-abs <= 1e-4 of the max, cosine >= 0.999999 at full depth
 
 
 def _cos(a, b):
@@ -371,7 +372,9 @@ def test_two_launch_layer_small_batches(llm_tiny_oracle, monkeypatch, M):
             if fed[:k + 1] == ([f0[i]] + [t0[j][i] for j in range(3)])[:k + 1]:
                 # M > 5: the 5-launch layer runs the MFMA GEMMs with producer-side quantisation (the same
                 # integers except at exact .5 ties), so it sits within the q8_0 noise floor of the fused layer
-                assert _cos(l1[k][i], l0[k][i]) > (0.99999 if M <= 5 else 0.9995)
+                # the fused layer attends unsplit (FUNASR_AB_FULL), the 5-launch one over key splits (M <= 5), or runs
+                # the MFMA GEMMs (M > 5): another f32 order either way, at the q8_0 noise floor
+                assert _cos(l1[k][i], l0[k][i]) > 0.9995
 
 
 @pytest.mark.slow
@@ -383,8 +386,8 @@ def test_encoder_full_10s_vs_reference_golden():
     out = eng.encode([g["audio"]], want_enc=True)
     eng.close()
     T = int(g["t_lfr_valid"])
-    assert _rel(out["enc"][0], g["enc"][:T]) < ENC_ATOL_FULL and _cos(out["enc"][0], g["enc"][:T]) > 0.99999
-    assert _rel(out["audio_embd"][0], g["adaptor"]) < ENC_ATOL_FULL
+    assert _rel(out["enc"][0], g["enc"][:T]) < ENC_ATOL_FULL and _cos(out["enc"][0], g["enc"][:T]) > 0.999999
+    assert _rel(out["audio_embd"][0], g["adaptor"]) < ENC_ATOL_FULL and _cos(out["audio_embd"][0], g["adaptor"]) > 0.999999
     nontie = g["ctc_margin"] > 1e-3
     assert ((out["ctc_ids"][0] != g["ctc_ids"]) & nontie).sum() == 0
 
@@ -419,11 +422,13 @@ def test_fused_decode_layer_vs_five_launch_layer(tiny_engine, llm_tiny_oracle):
     for k in range(8):
         if tf[:k + 1] != tu[:k + 1]:
             break  # a tie flipped the fed token: later steps are different sequences
-        assert _cos(lf[k], lu[k]) > 0.99999
+        # the fused launches attend unsplit up to FUNASR_AB_FULL keys, the 5-launch layer over 16 key splits: another
+        # f32 order, which q8_0 rounding of the o projection's input amplifies to the noise floor
+        assert _cos(lf[k], lu[k]) > 0.9995
         ref = m.forward(m.embed_tokens([tf[k]]), prompt.shape[0] + k)
         _check_step(lf[k], ref)
         s = np.sort(lu[k])
-        if s[-1] - s[-2] > 1e-3:
+        if s[-1] - s[-2] > TIE_MARGIN:
             assert tf[k + 1] == tu[k + 1]
 
 
@@ -577,6 +582,52 @@ def test_two_launch_layer_long_context():
         _check_step(l1[k], ref)
 
 
+def test_two_launch_layer_full_attention_switch(llm_tiny_oracle, monkeypatch):
+    """The fused attention launches' unsplit form (FUNASR_AB_FULL: every block of a kv head computes the head's whole
+    attention for pos + 1 <= the threshold, no split partials / fan-in / combine) switching to the key-split form
+    mid-chunk: the threshold sits 3 positions past the prompt, so one graph-replayed chunk of 8 steps runs both forms.
+    Two-launch and three-launch layers stay bit-identical; teacher-forced against the oracle; within f32 order of the
+    split-only run (FUNASR_AB_FULL=0)."""
+    from fun_asr_gguf import _native
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(19)
+    prompt = np.concatenate([m.embed_prompt(rng.integers(0, 4096, 30)),
+                             (rng.standard_normal((150, 1024)) * 0.5).astype(np.float32)], 0)
+    P = prompt.shape[0]
+    runs = {}
+    for full, mode in ((P + 3, 1), (P + 3, 2), (0, 1)):
+        monkeypatch.setenv("FUNASR_AB_FULL", str(full))
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=2), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            eng.set_decode_fused(mode)
+            eng.llm_reset(1)
+            toks = [eng.llm_prefill(1, prompt)]
+            toks += [int(t) for t in eng.llm_generate([1], 8)[0]]
+            lgs = []
+            for _ in range(4):  # eager single steps on the split form
+                toks.append(int(eng.llm_generate([1], 1)[0][0]))
+                lgs.append(eng.llm_logits(1))
+            runs[(full, mode)] = (toks, lgs)
+        finally:
+            eng.close()
+    (t2, l2), (t3, l3), (t0, l0) = runs[(P + 3, 1)], runs[(P + 3, 2)], runs[(0, 1)]
+    assert t2 == t3 and all(np.array_equal(a, b) for a, b in zip(l2, l3))
+    m.reset()
+    m.forward(prompt, 0)
+    for k in range(len(t2) - 1):
+        ref = m.forward(m.embed_tokens([t2[k]]), P + k)
+        if k >= 8:
+            _check_step(l2[k - 8], ref)
+            if t2[:k + 1] == t0[:k + 1]:
+                assert _cos(l2[k - 8], l0[k - 8]) > 0.9995  # the cached rows differ by f32 order: noise floor
+        else:
+            s = np.sort(ref)
+            if s[-1] - s[-2] > 0.25:
+                assert t2[k + 1] == int(np.argmax(ref)), k
+
+
 def test_two_launch_layer_l2_prefetch_bit_identical(monkeypatch):
     """The batch-1 attention launch's L2 prefetch blocks (FUNASR_L2PF, default 16 per kv head) only move lines into
     the L2 of the XCDs that read them next: tokens and logits of 48 greedy steps (graph-replayed chunk and single
@@ -670,36 +721,59 @@ def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
         assert got[q] == singles[q], q
 
 
-def test_fused_timeout_recovers_on_five_launch_layer():
+def test_fused_timeout_recovery_keeps_fused_layer():
     """A fan-in timeout in the fused decode layer (forced: fa_set_debug bit 1 makes one block withhold its q|k|v
-    hand-off; every wait is bounded at 10 ms) is not an error to the caller: fa_llm_generate_end re-runs the chunk on the
-    5-launch layer from the same positions and tokens, and the engine keeps that layer (invariant width drops to 1).
-    The tokens and logits equal a run on the 5-launch layer from the start."""
+    hand-off in the next chunk; every wait is bounded at 10 ms) is not an error to the caller: fa_llm_generate_end
+    re-runs the chunk on the fused layer from the same positions and tokens. The tokens and logits equal an undisturbed
+    run, and the invariant width stays 6 (DESIGN §3 decode step). With bit 2 too the re-run times out as well: that
+    chunk runs on the 5-launch layer (tokens and logits equal a 5-launch run of it), the next chunk is fused again, and
+    three such chunks in a row keep the 5-launch layer (width 1)."""
     from fun_asr_gguf import _native
     from oracle import qwen3 as oq
     cfg = dict(synth.LLM_TINY, n_ctx=256, max_seqs=2)
     m = oq.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=256)
     rng = np.random.default_rng(77)
     prompt = m.embed_prompt(rng.integers(0, 4096, 40))
-    runs = []
-    for forced in (True, False):
+
+    def run(debug=0, fused=1, chunks=1):
         eng = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)
-        eng.synthetic_weights(0)
-        if not forced:
-            eng.set_decode_fused(0)
-        eng.llm_reset(0)
-        first = eng.llm_prefill(0, prompt)
-        if forced:
-            assert eng.llm_invariant_width() > 1
-            eng.lib.fa_set_debug(eng.h, 2)
-        toks = [int(t) for t in eng.llm_generate([0], 3)[0]]
-        lg = eng.llm_logits(0)
-        more = [int(t) for t in eng.llm_generate([0], 2)[0]]
-        runs.append((first, toks, lg, more, eng.llm_invariant_width()))
-        eng.close()
-    (f1, t1, l1, m1, w1), (f0, t0, l0, m0, w0) = runs
-    assert w1 == 1 and f1 == f0 and t1 == t0 and m1 == m0
-    assert np.array_equal(l1, l0)
+        try:
+            eng.synthetic_weights(0)
+            eng.set_decode_fused(fused)
+            eng.llm_reset(0)
+            first = eng.llm_prefill(0, prompt)
+            toks = []
+            for c in range(chunks):
+                if debug:
+                    eng.lib.fa_set_debug(eng.h, debug)
+                toks += [int(t) for t in eng.llm_generate([0], 3)[0]]
+            lg = eng.llm_logits(0)
+            more = [int(t) for t in eng.llm_generate([0], 2)[0]]  # undisturbed chunk after the recovery
+            return first, toks, lg, more, eng.llm_invariant_width(), eng.llm_decode_recoveries()
+        finally:
+            eng.close()
+
+    f_ok, t_ok, l_ok, m_ok, w_ok, r_ok = run()
+    assert w_ok == 6 and r_ok == (0, 0)
+    f1, t1, l1, m1, w1, r1 = run(debug=2)
+    assert r1 == (1, 0) and w1 == 6, (r1, w1)
+    assert f1 == f_ok and t1 == t_ok and m1 == m_ok and np.array_equal(l1, l_ok)
+    # the re-run times out too: this chunk on the 5-launch layer, then the fused layer again
+    f2, t2, l2, m2, w2, r2 = run(debug=6)
+    assert r2 == (1, 1) and w2 == 6, (r2, w2)
+    e5 = _native.Engine(synth.ENC_TINY, cfg, max_batch=1, max_samples=16000)
+    try:
+        e5.synthetic_weights(0)
+        e5.set_decode_fused(0)
+        e5.llm_reset(0)
+        assert e5.llm_prefill(0, prompt) == f2
+        assert [int(t) for t in e5.llm_generate([0], 3)[0]] == t2
+        assert np.array_equal(e5.llm_logits(0), l2)
+    finally:
+        e5.close()
+    # three fallbacks in a row: the engine keeps the 5-launch layer
+    *_, w3, r3 = run(debug=6, chunks=3)
+    assert r3 == (3, 3) and w3 == 1, (r3, w3)
 
 
 def test_llm_prefill_batch_row_local_exact(llm_tiny_oracle):
