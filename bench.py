@@ -499,7 +499,7 @@ def main():
         step()
     m.engine.synchronize()
     dt_prof = time.perf_counter() - tp
-    prof = {c: m.engine.profile_read(c) for c in range(5)}
+    prof = {c: m.engine.profile_read(c) for c in range(7)}
     m.engine.profile_enable(False)
     step1_ms = graph_step_ms(m.engine, 1)
     barrier()
@@ -606,17 +606,27 @@ def headline(args, world, dt, dt_prof, prof, stage):
     audio_s = CLIP_S * args.steps * world
     value = audio_s / dt
     ms_step = dt / args.steps * 1e3
-    # dominant kernel class by estimated device time: decoder layer classes are timed on one layer only (layer 1:
-    # identical shapes in all layers, L2-warm weights from the prefetch slabs as in every layer but 0), so their
-    # sampled ms stand for n_layer x as much device time
+    # dominant kernel class by estimated device time: decoder layer classes are timed on layers 0 and 1 only
+    # (identical shapes in all layers): layer 1 (L2-warm weights from the prefetch slabs, as in every layer but 0)
+    # stands for layers 1 .. n_layer - 1, layer 0 is its own class (5); prefill forwards are class 6
     bf3 = os.environ.get("FUNASR_ENC_GEMM", "bf16x3") != "f32"
     enc_peak = BF16X3_PEAK_TFS if bf3 else FP32_MFMA_PEAK_TFS
     names = {0: "q8_0 GEMV/GEMM (decoder layers)",
              1: "bf16x3 MFMA GEMM (f32 encoder)" if bf3 else "f32 MFMA GEMM (encoder)",
              2: "bf16x3 MFMA attention (f32 encoder)" if bf3 else "f32 MFMA attention (encoder)",
-             3: "decode attention", 4: "q8_0 LM head GEMV + argmax"}
+             3: "decode attention", 4: "q8_0 LM head GEMV + argmax", 6: "prefill layer launches (sampled layers)"}
     n_layer = 28 if args.model == "full" else 2
-    weight = {0: n_layer, 1: 1, 2: 1, 3: n_layer, 4: 1}
+    prof = dict(prof)
+    l0 = prof.pop(5)
+    if n_layer > 2 and l0["launches"]:  # decode layers: layer 0 + (n_layer - 1) x layer 1 (class 0 holds layer 1)
+        p0 = prof[0]
+        prof[0] = {k: p0[k] * (n_layer - 1) + l0[k] for k in ("ms", "bytes", "flops", "launches")}
+        layer_note = {"layer0_avg_launch_us": round(l0["ms"] * 1e3 / l0["launches"], 2),
+                      "layer1_avg_launch_us": round(p0["ms"] * 1e3 / max(1, p0["launches"]), 2)}
+        weight = {0: 1, 1: 1, 2: 1, 3: n_layer, 4: 1, 6: n_layer / 2}
+    else:
+        layer_note = {}
+        weight = {0: n_layer, 1: 1, 2: 1, 3: n_layer, 4: 1, 6: n_layer}
     est_ms = {c: prof[c]["ms"] * weight[c] for c in prof}
     dom = max(prof, key=lambda c: est_ms[c])
     p = prof[dom]
@@ -629,7 +639,9 @@ def headline(args, world, dt, dt_prof, prof, stage):
         ach = p["flops"] / max(1, p["launches"]) / avg_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(enc_peak, 1), "unit": "TFLOP/s",
                 "frac": round(ach / enc_peak, 4), "traffic": None}
-    roof.update(kernel=names[dom], avg_launch_us=round(avg_s * 1e6, 2), launches_timed=p["launches"],
+    if dom == 0:
+        roof.update(layer_note)
+    roof.update(kernel=names[dom], avg_launch_us=round(avg_s * 1e6, 2), launches_timed=round(p["launches"]),
                 per_launch=("q8_0 weight bytes (+ the two-launch layer's K/V rows)" if dom == 0 else
                             "q8_0 weight bytes" if dom == 4 else "algorithmic FLOPs"),
                 est_device_ms_per_step={names[c]: round(est_ms[c] / args.steps, 2) for c in prof})

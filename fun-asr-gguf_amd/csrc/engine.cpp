@@ -197,7 +197,7 @@ struct Engine {
   struct ProfCls {
     double ms = 0, bytes = 0, flops = 0;
     int64_t launches = 0;
-  } pcls[5];
+  } pcls[7];
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   struct Pending {
     int cls;
@@ -248,7 +248,9 @@ struct Engine {
   }
 
   // ---- profiling helpers: bracket launches of class `cls` with events on the engine stream
-  bool prof_sample = true;  // decode layers > 0 are not bracketed (keeps the eager host ahead of the GPU)
+  bool prof_sample = true;  // decode layers > 1 are not bracketed (keeps the eager host ahead of the GPU)
+  bool prof_layer0 = false;  // layer 0's decoder launches go to class 5 (its weights arrive without prefetch)
+  bool prof_prefill = false; // prefill forwards' layer launches go to class 6 (not the decode classes)
   int prof_pos = 0;         // position of the profiled eager batch-1 decode step
   void prof_begin(int cls, hipEvent_t* a) {
     if (!prof || !prof_sample) return;
@@ -268,6 +270,7 @@ struct Engine {
     if (!prof || !prof_sample) return;
     hipEvent_t a = ev_pool[ev_next].first, b = ev_pool[ev_next].second;
     FA_HIP(hipEventRecord(b, stream));
+    if (cls == 0 || cls == 3) cls = prof_prefill ? 6 : prof_layer0 ? 5 : cls;
     pending.push_back({cls, a, b, bytes, flops});
     ev_next++;
   }
@@ -1201,9 +1204,12 @@ struct Engine {
     }
     for (int l = 0; l < (fused ? 0 : lc.n_layer); ++l) {
       const LlmLayerW& w = layers[l];
-      // sampled timing: one layer's launches stand for every layer (identical shapes); layer 1, not 0: from layer 1 on
-      // the weights arrive L2-warm from the previous launches' prefetch slabs, and layer 0 also carries the first slabs
-      prof_sample = l == (lc.n_layer > 2 ? 1 : 0);
+      // sampled timing: layer 1's launches stand for layers 1 .. n_layer - 1 (identical shapes; from layer 1 on the
+      // weights arrive L2-warm from the previous launches' prefetch slabs); layer 0, which also carries the first
+      // slabs, is timed as its own class (5); prefill forwards go to class 6
+      prof_sample = l <= (lc.n_layer > 2 ? 1 : 0);
+      prof_layer0 = l == 0 && lc.n_layer > 2;
+      prof_prefill = !decode;
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       GemvArgs a{};
@@ -1279,6 +1285,7 @@ struct Engine {
       gemv(dn, F, 1);
     }
     prof_sample = true;
+    prof_layer0 = prof_prefill = false;
     // lm_head (tied token_embd) with fused argmax partials: all rows (decode), the last row (prefill) or each
     // sequence's last row (prefill batch)
     const int n_rows = decode ? M : n_last > 0 ? n_last : 1;
@@ -1323,7 +1330,8 @@ struct Engine {
     const int QKV = (H + 2 * KV) * D;
     for (int l = 0; l < lc.n_layer; ++l) {
       const LlmLayerW& w = layers[l];
-      prof_sample = l == (lc.n_layer > 2 ? 1 : 0);  // as in llm_forward
+      prof_sample = l <= (lc.n_layer > 2 ? 1 : 0);
+      prof_layer0 = l == 0 && lc.n_layer > 2;  // as in llm_forward
       __half* kc = kcache + (size_t)l * layer_stride;
       __half* vc = vcache + (size_t)l * layer_stride;
       if (use_fused == 1) {
@@ -1373,6 +1381,7 @@ struct Engine {
       }
     }
     prof_sample = true;
+    prof_layer0 = false;
     if (M > 1) return;
     GemvArgs h{};
     h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
@@ -1726,7 +1735,6 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* k = getenv("FUNASR_L2PF_MASK");
       fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
     }
-    if (const char* g = getenv("FUNASR_AB_FULL")) fa::g_ab_full_keys = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_PF_ROW_LOCAL_MAX")) e->pf_rl_max = std::max(1, atoi(g));
     if (const char* g = getenv("FUNASR_F16_ATTN")) fa::g_attn_f16_mfma = atoi(g) != 0;
     // batched decode attention: one 16-wave block per (token, kv head) once there are 256 of them (a CU each):
@@ -2385,7 +2393,7 @@ int fa_profile_enable(fa_engine* h, int32_t on) {
 int fa_profile_read(fa_engine* h, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops) {
   FA_API_BEGIN
   Engine* e = h->e;
-  FA_REQUIRE(cls >= 0 && cls < 5, "class");
+  FA_REQUIRE(cls >= 0 && cls < 7, "class");
   e->prof_collect();
   if (ms) *ms = e->pcls[cls].ms;
   if (launches) *launches = e->pcls[cls].launches;

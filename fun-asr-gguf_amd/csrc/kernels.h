@@ -220,8 +220,6 @@ extern int g_l2pf_blocks;  // L2 prefetch blocks per kv head in the two-launch a
 extern int g_l2pf_max_m;   // ... for decode batches up to this width
 extern int g_l2pf_delay;   // their start delay, ticks of the 100 MHz clock
 extern int g_l2pf_mask;    // A/B: which byte sets they pull (1 FFN weights, 2 next attention weights, 4 next K/V)
-extern int g_ab_full_keys;  // fused attention launches: every block computes its kv head's whole attention (no key splits,
-                            // no fan-in) for positions with pos + 1 <= this (0 = never)
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
                   __half* kc, __half* vc, int H, int KV, const int* tok_seq, const int* tok_pos, int64_t seq_stride,
                   const int8_t* wo_q, const __half* wo_d, int E, const AttnWork& wk, const FusedDecodeWork& fw,

@@ -1673,8 +1673,7 @@ constexpr int AKV_PRE = 4;
 template <int NI, int AW, bool PIPE, bool PRE = false>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
-                                          bool store_kv, int pos, float eps, float scale, const AttnQIn& qi,
-                                          __half* __restrict__ kd,
+                                          int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
                                           float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
                                           const int4* pk = nullptr, const int4* pv = nullptr) {
@@ -1705,12 +1704,10 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
       norm_rope(qi.kx0, qi.kx1, qi.kw0, qi.kw1, eps, qi.c, qi.sn, y0, y1);
       const __half k0h = __float2half_rn(y0), k1h = __float2half_rn(y1);
       const __half v0h = __float2half_rn(qi.v0), v1h = __float2half_rn(qi.v1);
-      if (store_kv) {
-        kd[lane] = k0h;
-        kd[lane + 64] = k1h;
-        vd[lane] = v0h;
-        vd[lane + 64] = v1h;
-      }
+      kd[lane] = k0h;
+      kd[lane + 64] = k1h;
+      vd[lane] = v0h;
+      vd[lane + 64] = v1h;
       s_kn[lane] = __half2float(k0h);
       s_kn[lane + 64] = __half2float(k1h);
       s_vn[lane] = __half2float(v0h);
@@ -1857,7 +1854,7 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
                                                  const float* __restrict__ rcos, const float* __restrict__ rsin, float eps,
                                                  float scale, int& n_active_out, int& j, int& d0, float& M, float& L,
                                                  float4& o, const AttnQIn* pre = nullptr, const int4* pk = nullptr,
-                                                 const int4* pv = nullptr, bool store_fresh = true) {
+                                                 const int4* pv = nullptr) {
   static_assert(!PRE || LEAN, "attn_split_merge: preloaded K/V with lean passes only (NI <= 4)");
   constexpr int D = 128;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1927,16 +1924,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     __half* vd = vb + (int64_t)pos * D;
     const int ni = (ge - g0 + NW - 1) / NW;
     if (ni <= 1)
-      attn_wave<1, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, store_fresh, pos, eps, scale, qi,
+      attn_wave<1, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 2)
-      attn_wave<2, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, store_fresh, pos, eps, scale, qi,
+      attn_wave<2, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else if (ni <= 4 || LEAN)
-      attn_wave<4, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, store_fresh, pos, eps, scale, qi,
+      attn_wave<4, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
                                  kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
     else
-      attn_wave<8, NW, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, store_fresh, pos, eps, scale, qi, kd, vd,
+      attn_wave<8, NW, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
   }
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
@@ -2869,7 +2866,6 @@ struct AttnOArgs {
   unsigned long long* gpart;  // FA_PART_GRANULE: [KV][ASPLIT][APART] split partials as granules {value, tag}
   L2Prefetch pf;       // l2_prefetch (pf_blocks > 0: the last z slab, pf_blocks blocks per kv head)
   int pf_blocks, pf_delay, pf_mask;  // pf_mask (A/B): 1 the FFN weights, 2 the next q|k|v / o weights, 4 the next K/V
-  int full_keys;       // positions with pos + 1 <= full_keys take the unsplit (full-attention) form, see k_attn_o
 };
 // FA_QKV_GRANULE = 1: the q|k|v rows go from the 16 producing blocks of a kv head to the same 16 blocks as
 // data-tagged granules (tag = this launch's epoch), polled by every consumer thread for its 2 rows and staged in LDS:
@@ -2918,7 +2914,6 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
 }
 
 int g_l2pf_blocks = 16;
-int g_ab_full_keys = 1024;  // fused attention launches: unsplit (full-attention) form up to this many keys (0 = never)
 int g_l2pf_delay = 50;
 int g_l2pf_max_m = 1;
 int g_l2pf_mask = 7;
@@ -3082,10 +3077,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   int pos = a.tok_pos[0];
   const int seq = a.tok_seq[0];
   asm volatile("" : "+s"(pos) : "s"(seq));
-  // full-attention form (kernel-uniform: pos is the launch's token position): every block of kv head g computes head
-  // g's whole attention over keys [0, pos] itself, from the XCD's L2 (the 16 blocks of a head share one XCD, where the
-  // previous layer's prefetch slab pulled the K/V rows), so no split partials, no ticket fan-in and no combine hop.
-  const bool full = pos + 1 <= a.full_keys;
   STAMP(0);
   int4 kpre[AKV_PRE], vpre[AKV_PRE];  // FA_KV_EARLY: the wave's first-pass K/V
   // this block's o slice: rows [FO_ROWS sp, +FO_ROWS), columns [GQ D g, +GQ D); thread -> row tr, 2 q8_0 blocks tq
@@ -3118,7 +3109,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       *reinterpret_cast<float4*>(a.xsum + threadIdx.x * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
     norm_quant_block_regs<4>(xv, xw, true, a.eps, 1024, s_xq, s_xd, s_red);
     __syncthreads();
-    if (FA_KV_EARLY == 1 && !full) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
+    if (FA_KV_EARLY == 1) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
     STAMP(12);
     // ---- the wave's QR rows (compute_group<1, 1, 0>'s arithmetic), published as two 16-B sc1 stores
     const int4 xq = *reinterpret_cast<const int4*>(s_xq + lane * 16);
@@ -3142,7 +3133,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
         __hip_atomic_store(a.gqkv + qrow0 + QR * wave + lane, ((unsigned long long)ep_qkv << 32) | __float_as_uint(yv),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (FA_KV_EARLY == 2 && !full) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
+    if (FA_KV_EARLY == 2) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
     STAMP(13);
     // thread t: head g's local rows 2t, 2t + 1 (q head GQ g, q head GQ g + 1, k head g, v head g; 128 each)
     __shared__ float s_qkv[(GQ + 2) * D];
@@ -3202,23 +3193,11 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
   // QKV: lean passes (at most 4 groups per wave pass, no next-pass prefetch): the GEMV and the preloads need the
   // registers; identical arithmetic to k_attn_o<false> up to 4 groups per wave (n_past < 16 x 4 x 4 x 4 = 1024)
   constexpr bool PRE = QKV && FA_KV_EARLY != 0;
-  float4 r;
-  if (full) {
-    // one split over all keys, 8-group passes with the next pass's K/V in flight (the same instantiation in the two- and
-    // three-launch layers: bit-identical); the block of split 0 stores the fresh K/V row, the others use it from LDS
-    attn_split_merge<1, 0, false>(g, 0, 0, pos, seq, 1, a.H, a.KV, a.seq_stride, a.head_stride, a.kc, a.vc, a.qkv,
-                                  a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0, M, L, o, &qpre, nullptr,
-                                  nullptr, sp == 0);
-    // the launch counter (the epoch source of the granule hand-offs): one ticket per block, as the fan-in adds them;
-    // nobody waits on it (QKV: every block of head g read it before its q|k|v granules, all of which this block has seen)
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.cnt + g * CNT_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);  // wave 0 (the single-split normalisation of k_attn_block)
-    STAMP(10);
-  } else {
   const bool active = attn_split_merge<1, QKV ? 1 : 0, PRE>(g, sp, 0, pos, seq, FS, a.H, a.KV, a.seq_stride,
                                                             a.head_stride, a.kc, a.vc, a.qkv, a.qn, a.kn, a.rcos,
                                                             a.rsin, a.eps, a.scale, n_active, j, d0, M, L, o, &qpre,
                                                             kpre, vpre);
+  float4 r;
   if (QKV && FA_PART_GRANULE) {
     // publish this split's partial as granules tagged with the launch's epoch; poll the n_active splits' granules
     // this lane folds (wave w: splits [4 w, 4 w + 4); head lane >> 5, dims [4 (lane & 31), +4) and the 4 (m, l))
@@ -3287,7 +3266,6 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     // every split combines the n_active partials (combine_splits, as the last arriver of k_attn_block does)
     r = combine_splits(rs, n_active, wave, lane);
   }
-  }
   __shared__ __attribute__((aligned(16))) int8_t s_aq[GQ * D];
   __shared__ float s_ad[GQ * D / 32];
   if (wave == 0) {
@@ -3325,7 +3303,6 @@ void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps,
   FA_REQUIRE(wk.partials && fw.opart && fw.cnt && fw.err, "attn_o_fused: workspace");
   AttnOArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
               1.0f / sqrtf(128.0f), wo_q, wo_d, E, fw.opart, fw.cnt, wk.partials, fw.err};
-  a.full_keys = g_ab_full_keys;
   hipLaunchKernelGGL(k_attn_o<false>, dim3(KV, ASPLIT), dim3(AWV * 64), 0, s, a);
 }
 
@@ -3346,7 +3323,6 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
               fw.cnt + 2 * FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.gqkv, dbg_drop, fw.gpart};
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   FA_REQUIRE(!FA_PART_GRANULE || fw.gpart, "qkv_attn_o_fused: partial granule workspace");
-  a.full_keys = g_ab_full_keys;
   int nz = M;
   if (pf && M <= g_l2pf_max_m && g_l2pf_blocks > 0) {
     FA_REQUIRE(pf->F == 3072 && pf->gq && pf->uq && pf->dq && pf->gd && pf->ud && pf->dd &&

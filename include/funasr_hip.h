@@ -257,8 +257,11 @@ int fa_fuzzy_substring_distance(const int32_t* main_codes, int32_t m, const int3
 /* ---- timing hooks for bench.py roofline (HIP events on the engine's stream) */
 /* Enable per-kernel-class event timing; fa_profile_read returns accumulated ms and launch counts for
  * class ids: 0 q8 GEMV/GEMM of the decoder layers, 1 f32 GEMM (encoder), 2 encoder attention,
- * 3 decoder attention, 4 LM head. Classes 0 and 3 are sampled on layer 0 only (identical shapes in every
- * layer): multiply their ms by n_layer for the device time of all layers. */
+ * 3 decoder attention, 4 LM head, 5 layer 0's decoder launches (classes 0 and 3 of layer 0), 6 prefill forwards'
+ * layer launches (sampled layers only). Classes 0 and 3
+ * are sampled on layer 1 only (identical shapes in every layer; from layer 1 on the weights arrive L2-warm from
+ * the previous launches' prefetch slabs, layer 0's do not): the device time of all layers is class 5 +
+ * (n_layer - 1) x (classes 0 + 3). */
 int fa_profile_enable(fa_engine* e, int32_t on);
 int fa_profile_read(fa_engine* e, int32_t cls, double* ms, int64_t* launches, double* bytes, double* flops);
 int fa_synchronize(fa_engine* e);

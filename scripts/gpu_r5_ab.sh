@@ -10,5 +10,5 @@ if [ -n "${AB_TESTS}" ]; then
   # assertion failures (1) still allow the timing runs; anything else (a fault, an abort, a timeout) ends the call
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi
-timeout -k 10 400 python -u scripts/prof_decode_ab.py ${AB_STEPS:-256} ${AB_SETTINGS:-FUNASR_AB_FULL=0 FUNASR_AB_FULL=1024} \
+timeout -k 10 400 python -u scripts/prof_decode_ab.py ${AB_STEPS:-256} ${AB_SETTINGS:--} \
   2>&1 | tee gpurun_out/ab.log
