@@ -1205,9 +1205,12 @@ struct QTile {
   static constexpr int BYTES = 2 * STAGE;
 };
 
+// The weight scales stay raw fp16 bits in registers until qt_store: converted right after the load (where hipcc put
+// the conversion), each k-step began with a vmcnt wait for the NEXT stage's loads, serialising a global round trip with
+// every stage's MFMAs.
 template <int EPI>
 __device__ __forceinline__ void qt_load(const GemvArgs& a, int K, int o0, int t0, int kb, int t, i32x4_t (&rw)[QTile<EPI>::NM][2],
-                                        i32x4_t (&rx)[2], float (&rdw)[QTile<EPI>::NM], float& rdx) {
+                                        i32x4_t (&rx)[2], unsigned short (&rdw)[QTile<EPI>::NM], float& rdx) {
   const int nb = K >> 5;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -1223,13 +1226,13 @@ __device__ __forceinline__ void qt_load(const GemvArgs& a, int K, int o0, int t0
   const int row = t >> 1, blk = t & 1;
 #pragma unroll
   for (int m = 0; m < QTile<EPI>::NM; ++m)
-    rdw[m] = __half2float((m ? a.wd2 : a.wd)[(int64_t)min(o0 + row, a.O - 1) * nb + kb + blk]);
+    rdw[m] = __half_as_ushort((m ? a.wd2 : a.wd)[(int64_t)min(o0 + row, a.O - 1) * nb + kb + blk]);
   rdx = a.xd[(int64_t)min(t0 + row, a.M - 1) * nb + kb + blk];
 }
 
 template <int EPI>
 __device__ __forceinline__ void qt_store(uint8_t* st, int t, const i32x4_t (&rw)[QTile<EPI>::NM][2], const i32x4_t (&rx)[2],
-                                         const float (&rdw)[QTile<EPI>::NM], float rdx) {
+                                         const unsigned short (&rdw0)[QTile<EPI>::NM], float rdx) {
   using T = QTile<EPI>;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -1241,7 +1244,11 @@ __device__ __forceinline__ void qt_store(uint8_t* st, int t, const i32x4_t (&rw)
   float* sc = reinterpret_cast<float*>(st + (T::NM + 1) * T::W);  // [m (weights) | NM (tokens)][blk][128]
   const int row = t >> 1, blk = t & 1;
 #pragma unroll
-  for (int m = 0; m < T::NM; ++m) sc[(m * 2 + blk) * 128 + row] = rdw[m];
+  for (int m = 0; m < T::NM; ++m) {
+    unsigned short raw = rdw0[m];
+    asm volatile("" : "+v"(raw)::"memory");  // convert here, after the stage's compute, not at the load
+    sc[(m * 2 + blk) * 128 + row] = __half2float(__ushort_as_half(raw));
+  }
   sc[(T::NM * 2 + blk) * 128 + row] = rdx;
 }
 
@@ -1263,7 +1270,8 @@ __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[m][i][j] = f32x16{};
   i32x4_t rw[NM][2], rx[2];
-  float rdw[NM], rdx;
+  unsigned short rdw[NM];
+  float rdx;
   const int nk = K / 64;
   qt_load<EPI>(a, K, o0, t0, 0, t, rw, rx, rdw, rdx);
   qt_store<EPI>(qsm, t, rw, rx, rdw, rdx);
@@ -1296,20 +1304,22 @@ __global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
         for (int i = 0; i < 2; ++i) {
           const int rb = wr * 64 + i * 32;
           const i32x4_t aw = *reinterpret_cast<const i32x4_t*>(st + m * T::W + (rb + r) * QT_LD + 32 * j + 16 * h);
-          float4 dw4[4];  // this lane's 16 rows: (reg & 3) + 8 (reg >> 2) + 4 h
+          f32x16 dwv;  // this lane's 16 row scales: rows (reg & 3) + 8 (reg >> 2) + 4 h
 #pragma unroll
-          for (int g = 0; g < 4; ++g)
-            dw4[g] = *reinterpret_cast<const float4*>(sc + (m * 2 + j) * 128 + rb + 8 * g + 4 * h);
+          for (int g = 0; g < 4; ++g) {
+            const float4 d4 = *reinterpret_cast<const float4*>(sc + (m * 2 + j) * 128 + rb + 8 * g + 4 * h);
+            dwv[4 * g + 0] = d4.x;
+            dwv[4 * g + 1] = d4.y;
+            dwv[4 * g + 2] = d4.z;
+            dwv[4 * g + 3] = d4.w;
+          }
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
             const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(aw, bx[jj], zero, 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              acc[m][i][jj][4 * g + 0] += (float)D[4 * g + 0] * (dw4[g].x * dx[jj]);
-              acc[m][i][jj][4 * g + 1] += (float)D[4 * g + 1] * (dw4[g].y * dx[jj]);
-              acc[m][i][jj][4 * g + 2] += (float)D[4 * g + 2] * (dw4[g].z * dx[jj]);
-              acc[m][i][jj][4 * g + 3] += (float)D[4 * g + 3] * (dw4[g].w * dx[jj]);
-            }
+            // acc += f32(dot) * (f32(d_w) * d_x), one rounding per product and per fused add as before, on 16-wide
+            // vectors: v_pk_mul_f32 / v_pk_fma_f32 (two values per instruction; hipcc packed the EPI 0 / 1 forms by
+            // itself but not the SwiGLU one)
+            acc[m][i][jj] = __builtin_elementwise_fma(__builtin_convertvector(D, f32x16), dwv * dx[jj], acc[m][i][jj]);
           }
           __builtin_amdgcn_sched_barrier(0);  // one (matrix, row tile) at a time: two MFMA results live, not eight
         }

@@ -25,5 +25,8 @@ for r in range(reps + 1):
     eng.llm_prefill_batch(list(range(B)), prompts, temperature=0.0)
     eng.synchronize()
     if r:
-        print(f"prefill batch {B} x {T} rows: {(time.perf_counter() - t) * 1e3:.2f} ms")
+        print(f"prefill batch {B} x {T} rows: {(time.perf_counter() - t) * 1e3:.2f} ms", flush=True)
+import hashlib  # noqa: E402
+h = hashlib.sha256(b"".join(eng.llm_logits(s).tobytes() for s in sorted({0, B // 2, B - 1}))).hexdigest()[:16]
+print(f"logits hash (sequences 0, {B // 2}, {B - 1}): {h}")
 eng.close()
