@@ -167,6 +167,10 @@ struct Engine {
   // Measured (graph-replayed, full model): 1 / 8 / 32 steps per graph -> batch 1 0.489 / 0.499 / 0.525 ms per step,
   // batch 32 1.223 / 1.239 / 1.358 ms: one step per graph replay stays the default
   int graph_steps = 1;
+  // profiler experiment hook (FUNASR_STEP_MASK, default all): which launches a batch-1 fused decode step enqueues --
+  // bit 0 the attention launches (AB), 1 the FFN launches (C), 2 the LM head, 3 the sampler. Steps with bits cleared
+  // compute garbage; only for bisecting which graph node rocprofv3's kernel trace rejects (scripts/gpu_r5_graphprof.sh)
+  int step_mask = 15;
   bool pf_row_local = false;  // the prefill forward being run is row-local (see llm_forward)
   int pf_rl_max = 1024;       // prompts longer than this prefill on the tiled forward, alone (FUNASR_PF_ROW_LOCAL_MAX)
   int fused_retries = 0;     // chunks re-run on the fused layer after a fan-in timeout (exact: the same arithmetic)
@@ -1350,6 +1354,7 @@ struct Engine {
         // rows of positions [0, pos] of every kv head (fp16 K and V: 2 x KV x D x 2 B per position)
         hipEvent_t ev;
         prof_begin(0, &ev);
+        if (step_mask & 1)
         qkv_attn_o_fused(l == 0 ? lx : fdw.xmid, l == 0 ? nullptr : fdw.dpart, lx, w.attn_norm, w.qkv.q, w.qkv.d, lqkv,
                          w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, H, KV, d_tok_seq, d_tok_pos, seq_stride,
                          w.o.q, w.o.d, E, attn_wk, fdw, stream, M, (debug_flags & 2) ? 1 : 0, &pf);
@@ -1375,8 +1380,9 @@ struct Engine {
       {
         hipEvent_t ev;
         prof_begin(0, &ev);
-        ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream,
-                  M);
+        if (step_mask & 2)
+          ffn_fused(lx, w.ffn_norm, lc.rms_eps, w.gate.q, w.gate.d, w.up.q, w.up.d, w.down.q, w.down.d, E, F, fdw, stream,
+                    M);
         prof_end(0, 3.0 * F * E * 34.0 / 32.0, 2.0 * 3.0 * M * F * E);
       }
     }
@@ -1390,7 +1396,7 @@ struct Engine {
     h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, 1);
     chunk_cur = lm_head_chunk(lc.n_vocab, 1);
     h.x = fdw.xmid; h.ldx = E; h.norm_w = out_norm; h.psum = fdw.dpart;
-    gemv(h, E, 3);
+    if (step_mask & 4) gemv(h, E, 3);
   }
 
   // a fused-decode fan-in timeout (a group not co-resident: another kernel held CUs) leaves the chunk's outputs
@@ -1567,7 +1573,7 @@ struct Engine {
     // embedded by fa_llm_generate before the steps)
     EmbedNext en;
     en.qs = tok_embd.q; en.d = tok_embd.d; en.E = lc.n_embd; en.x = lx; en.tok_pos = d_tok_pos;
-    sample(n, d_tok_seq, d_tok_pos, d_step, d_tok_cur, d_tok_hist, &en);
+    if (step_mask & 8) sample(n, d_tok_seq, d_tok_pos, d_step, d_tok_cur, d_tok_hist, &en);
   }
 
   // hipGraph of one decode step (all per-step state, the sampler parameters included, lives in device memory;
@@ -1695,6 +1701,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       const char* g = getenv("FUNASR_LM_HEAD_MT6");
       fa::g_lm_head_mt6 = g ? atoi(g) != 0 : 1;
     }
+    if (const char* g = getenv("FUNASR_STEP_MASK")) e->step_mask = atoi(g) & 15;
     if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));

@@ -3,11 +3,15 @@
 #   FETCH_SIZE of the bench's decode launches with the batch-1 prefetch slabs OFF (the HBM bytes the layer launches
 #   need: the slabs' pulls would otherwise be counted as well as the consumers' reads) and ON, and TCC hit / miss per
 #   decode launch with the slabs on and off (does C hit the L2 lines AB's slab pulled?).
-# STEPS: which parts to run (default "tests bench pmc"); every GPU step has its own time limit and the chain stops at
+# STEPS: which parts to run (default "abw tests bench"; "pmc" separately); every GPU step has its own time limit and the chain stops at
 # the first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-STEPS=${STEPS:-"tests bench pmc"}
+STEPS=${STEPS:-"abw tests bench"}
+if [[ " $STEPS " == *" abw "* ]]; then  # batch-32 graph-replayed decode step: lean VALU vs one-round-trip MFMA attention
+  AB_M=32 timeout -k 10 300 python -u scripts/prof_decode_ab.py 128 FUNASR_ATTN_MFMA=0 FUNASR_ATTN_MFMA=1 \
+    FUNASR_ATTN_MFMA=0 FUNASR_ATTN_MFMA=1 2>&1 | tee gpurun_out/ab_wide.log || exit 1
+fi
 if [[ " $STEPS " == *" tests "* ]]; then
   timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }

@@ -294,6 +294,39 @@ def test_llm_batch20_lean_attention_chunked_combine(llm_tiny_oracle):
     eng.close()
 
 
+def test_llm_batch32_wide_attention_long_contexts():
+    """M = 32 decode: the wide attention launch (one 16-wave block per (token, kv head), no key splits) over contexts of
+    3 .. 651 keys in one launch. Rows checked teacher-forced against the oracle run of each sequence alone, over two
+    steps."""
+    from fun_asr_gguf import _native
+    m = oqw.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=700)
+    rng = np.random.default_rng(32)
+    lens = [int(n) for n in rng.integers(3, 300, 32)]
+    lens[0], lens[1], lens[2], lens[3] = 510, 515, 600, 650
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in lens]
+    eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=700, max_seqs=32), max_batch=1, max_samples=16000)
+    try:
+        eng.synthetic_weights(0)
+        toks = []
+        for s_, p in enumerate(prompts):
+            eng.llm_reset(s_)
+            toks.append(eng.llm_prefill(s_, p))
+        steps, lgs = [], []
+        for k in range(2):
+            steps.append(eng.llm_generate(list(range(32)), 1)[:, 0])
+            lgs.append({s_: eng.llm_logits(s_) for s_ in (0, 1, 2, 3, 7, 19, 31)})
+    finally:
+        eng.close()
+    for s_ in (0, 1, 2, 3, 7, 19, 31):
+        m.reset()
+        m.forward(prompts[s_], 0)
+        fed = [toks[s_], int(steps[0][s_])]
+        for k in range(2):
+            ref = m.forward(m.embed_tokens([fed[k]]), lens[s_] + k)
+            _check_step(lgs[k][s_], ref)
+            assert int(steps[k][s_]) == int(np.argmax(lgs[k][s_]))
+
+
 def test_llm_continuous_batch_equals_single(tiny_engine, llm_tiny_oracle):
     """A sequence decoded inside a batch gives the tokens it gives alone on the same layer structure: the two-launch
     fused layer (a batch of 3 runs one grid slab per token; the batch-1 run completes the residual in the LM head's
