@@ -138,15 +138,32 @@ def pmc_mfma_busy(mode):
 
 
 def pmc_traffic():
-    """Per-launch HBM bytes of the decode GEMV class from the committed PMC pass (scripts/pmc_traffic.py,
-    rocprofv3 --pmc FETCH_SIZE with the gfx950 x2 correction), or None when no summary is present."""
+    """Per-launch HBM bytes of the decode-layer class from the committed PMC pass (scripts/pmc_traffic.py, rocprofv3
+    --pmc FETCH_SIZE with the gfx950 x2 correction) taken with the batch-1 L2 prefetch slabs OFF (newest
+    profiles/*pmc_gemv*slabs_off*.json, else the newest *pmc_gemv*.json): with the slabs on, the attention launch's
+    pulls for the next two launches are counted in it while the consumers' reads are counted again (the counter pass
+    brackets every dispatch, so the pulled lines do not survive to the consumer: its L2 hit rate is the same with and
+    without the slabs, profiles/r05_pmc_l2hit_slabs_*.json). Returns (bytes, source, extra) or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gemv*.json")))
+    prof = os.path.join(ROOT, "profiles")
+    files = sorted(glob.glob(os.path.join(prof, "*pmc_gemv*slabs_off*.json"))) or \
+        sorted(glob.glob(os.path.join(prof, "*pmc_gemv*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
-        return round(d["decode_layer_gemv_mean"]["traffic_bytes"])
+        m = d["decode_layer_gemv_mean"]
+        extra = {"traffic_over_weight_bytes": round(m["traffic_bytes"] / m["algorithmic_bytes"], 3)}
+        on = sorted(glob.glob(os.path.join(prof, "*pmc_gemv*slabs_on*.json")))
+        if on:
+            extra["traffic_slabs_on"] = round(json.load(open(on[-1]))["decode_layer_gemv_mean"]["traffic_bytes"])
+        for tag in ("off", "on"):
+            hf = sorted(glob.glob(os.path.join(prof, f"*pmc_l2hit*slabs_{tag}*.json")))
+            if hf:
+                h = json.load(open(hf[-1]))
+                extra[f"l2_hit_rate_slabs_{tag}"] = {k: round(v["hit_rate"], 3) for k, v in h.items()
+                                                      if isinstance(v, dict) and "hit_rate" in v}
+        return round(m["traffic_bytes"]), "profiles/" + os.path.basename(files[-1]), extra
     except Exception:
         return None
 
@@ -634,7 +651,12 @@ def headline(args, world, dt, dt_prof, prof, stage):
     if dom in (0, 4):
         ach = p["bytes"] / max(1, p["launches"]) / avg_s / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic() if dom == 0 else None}
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+        pt = pmc_traffic() if dom == 0 else None
+        if pt:
+            roof["traffic"] = pt[0]
+            roof["traffic_source"] = pt[1]
+            roof.update(pt[2])
     else:
         ach = p["flops"] / max(1, p["launches"]) / avg_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(enc_peak, 1), "unit": "TFLOP/s",
@@ -646,10 +668,12 @@ def headline(args, world, dt, dt_prof, prof, stage):
                             "q8_0 weight bytes" if dom == 4 else "algorithmic FLOPs"),
                 est_device_ms_per_step={names[c]: round(est_ms[c] / args.steps, 2) for c in prof})
     if dom == 0 and roof.get("traffic"):
-        roof["traffic_note"] = ("FETCH_SIZE x 2 per decode-layer launch, graph path, newest profiles/*pmc_gemv*.json; "
-                                "with the prefetch slabs it counts the pulled bytes twice (the attention launch's pull "
-                                "for the next two launches and their own reads as seen under the profiler): HBM bytes "
-                                "per layer stay ~ the algorithmic 18.4 MB (DESIGN.md section 3)")
+        roof["traffic_note"] = ("FETCH_SIZE x 2 per decode-layer launch (mean of the attention and FFN launches), graph "
+                                "path, batch-1 L2 prefetch slabs off: the HBM bytes the launches need (weights, K/V rows, "
+                                "activations). With the slabs on the counter pass also counts the attention launch's "
+                                "pulls for the next two launches (traffic_slabs_on), which the bracketed dispatches of "
+                                "a counter pass do not keep for the consumers (same FFN-launch L2 hit rate either way); "
+                                "DESIGN.md section 3")
     # the encoder's MFMA classes (secondary: the clip's 705 GFLOP of f32 contractions) against the peak of the
     # arithmetic they run on: bf16x3 = three bf16 MFMA products per f32 product (2.5 PF/s / 3), or exact f32
     for c, key in ((1, "encoder_gemm"), (2, "encoder_attention")):

@@ -72,13 +72,28 @@ __device__ __forceinline__ void attn_store_tile(float* lds, int stage, const f4v
   }
 }
 
+// the output row as f32, or (op.hi != nullptr: bf16x3 encoder, output consumed only by the out-projection GEMM) as
+// its bf16 hi / lo planes at the same element offsets: hi = bf16_rn(v), lo = bf16_rn(v - hi), the split the GEMM's
+// staging would apply to the f32 row (bit-identical products)
+__device__ __forceinline__ void store_o4(const float4 v, float* __restrict__ O, const APlanesD& op, int64_t off) {
+  if (!op.hi) {
+    *reinterpret_cast<float4*>(O + off) = v;
+    return;
+  }
+  bf16x4_t h, l;
+  split_bf16x4(v, h, l);
+  *reinterpret_cast<bf16x4_t*>(op.hi + off) = h;
+  *reinterpret_cast<bf16x4_t*>(op.lo + off) = l;
+}
+
 // The block's epilogue, shared by the exact-f32 and the bf16x3 kernels: O^T (d on registers, q on lanes) -> LDS [q][d]
 // for row-contiguous stores; with key splits, publish (m, l, O) and let the last split merge.
 template <int D>
 __device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m_run, float l_run, float* lds,
                                               float* __restrict__ O, int64_t ldo, int64_t row_base, int head, int q0,
                                               int qt, int n_qt, int clip, int t_stride, int KS, int ks, int r16,
-                                              float* __restrict__ part, int* __restrict__ cnt, int lds_bytes) {
+                                              float* __restrict__ part, int* __restrict__ cnt, int lds_bytes,
+                                              APlanesD op = {}) {
   using L = AttnLds<D>;
   constexpr int NDT = D / 32;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -108,7 +123,7 @@ __device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m
         float4 v = *reinterpret_cast<const float4*>(so + q * L::OS + 4 * d4);
         v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
         if (r16) v = round_f16x4(v);
-        *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+        store_o4(v, O, op, (row_base + q0 + q) * ldo + head * D + 4 * d4);
       }
     }
     return;
@@ -171,7 +186,7 @@ __device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m
     const float inv = 1.0f / s_l[q];
     float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
     if (r16) v = round_f16x4(v);
-    *reinterpret_cast<float4*>(O + (row_base + q0 + q) * ldo + head * D + 4 * d4) = v;
+    store_o4(v, O, op, (row_base + q0 + q) * ldo + head * D + 4 * d4);
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -390,7 +405,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
                                                   const int* __restrict__ lens, float scale, int KS,
-                                                  float* __restrict__ part, int* __restrict__ cnt) {
+                                                  float* __restrict__ part, int* __restrict__ cnt, APlanesD op) {
   using L = AttnLds3<D>;
   constexpr int NDT = D / 32;
   constexpr int NKS = D / 16;  // k-steps of the S product
@@ -574,7 +589,7 @@ __global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, c
     __syncthreads();
   }
   attn_epilogue<D>(o, m_run, l_run, lds, O, ldo, row_base, head, q0, qt, n_qt, clip, t_stride, KS, ks, P == 1 ? 1 : 0,
-                   part, cnt, L::BYTES);
+                   part, cnt, L::BYTES, op);
 }
 
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
@@ -584,7 +599,7 @@ int g_attn_wab = 0;               // k_attn_bf3 write-after-barrier staging (S =
 template <int D, int P>
 static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const float* K, const float* V, int64_t ldq,
                             int64_t ldk, int64_t ldv, float* O, int64_t ldo, int t_stride, const int* lens, float scale,
-                            int KS, const AttnF32Work& wk) {
+                            int KS, const AttnF32Work& wk, APlanesD op = {}) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_attn_bf3<D, P, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<D>::BYTES);
@@ -593,10 +608,10 @@ static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const floa
   }
   if (g_attn_wab)
     hipLaunchKernelGGL((k_attn_bf3<D, P, 1>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, wk.part, wk.cnt, op);
   else
     hipLaunchKernelGGL((k_attn_bf3<D, P, 0>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, wk.part, wk.cnt, op);
 }
 
 int attn_f32_splits(int batch, int t_stride, int n_heads) {
@@ -610,7 +625,9 @@ int attn_f32_splits(int batch, int t_stride, int n_heads) {
 
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s, int r16, int bf3) {
+              const AttnF32Work& wk, hipStream_t s, int r16, int bf3, APlanes op) {
+  FA_REQUIRE(!op.hi || (bf3 && !r16), "attn_f32: bf16 output planes need the bf16x3 mode");
+  const APlanesD opd{reinterpret_cast<__bf16*>(op.hi), reinterpret_cast<__bf16*>(op.lo)};
   const int KS = attn_f32_splits(batch, t_stride, n_heads);
   FA_REQUIRE(KS >= 1 && KS <= 8, "attn_f32: 1-8 key splits (16 measured slower: 60 vs 39 us at T = 1001)");
   const int n_tiles = cdiv(t_stride, AQ) * n_heads * batch;
@@ -634,8 +651,8 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
   }
   if (bf3 && !r16) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
-    if (head_dim == 128) launch_attn_bf3<128, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
-    else launch_attn_bf3<64, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
+    if (head_dim == 128) launch_attn_bf3<128, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk, opd);
+    else launch_attn_bf3<64, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk, opd);
     return;
   }
   if (head_dim == 128) {

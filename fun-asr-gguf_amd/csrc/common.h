@@ -108,6 +108,23 @@ __device__ __forceinline__ void st_sc1_f4(f32x4_t v, __amdgpu_buffer_rsrc_t rs, 
 }
 
 // (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).
+// bf16x3 encoder activations handed between kernels as their two bf16 planes (APlanes in kernels.h): hi = bf16_rn(v),
+// lo = bf16_rn(v - hi), exactly the split the bf16x3 GEMM's staging applies to an f32 A row
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+struct APlanesD {
+  __bf16* hi = nullptr;
+  __bf16* lo = nullptr;
+};
+__device__ __forceinline__ void split_bf16x4(const float4 v, bf16x4_t& h, bf16x4_t& l) {
+  h = bf16x4_t{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  l = bf16x4_t{(__bf16)(v.x - (float)h[0]), (__bf16)(v.y - (float)h[1]), (__bf16)(v.z - (float)h[2]),
+               (__bf16)(v.w - (float)h[3])};
+}
+__device__ __forceinline__ void split_bf16(const float v, __bf16& h, __bf16& l) {
+  h = (__bf16)v;
+  l = (__bf16)(v - (float)h);
+}
+
 __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i) || (v != v)) {
     v = v2;

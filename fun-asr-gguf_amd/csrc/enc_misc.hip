@@ -94,7 +94,7 @@ void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, cons
 template <int PER>
 __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
                             const float* __restrict__ w, const float* __restrict__ bb, int rows, int D, float eps,
-                            const int* __restrict__ lens, int t_stride, int r16) {
+                            const int* __restrict__ lens, int t_stride, int r16, APlanesD yp) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -135,32 +135,44 @@ __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __r
     int b = row / t_stride, t = row - b * t_stride;
     mk = t < lens[b] ? 1.0f : 0.0f;
   }
-  float* yr = y + (int64_t)row * ldy;
+  const int64_t yo = (int64_t)row * ldy;
   if (vec) {
 #pragma unroll
     for (int i = 0; i < PER; i += 4) {
       const int c = lane * PER + i;
       const float4 wv = *reinterpret_cast<const float4*>(w + c), bv = *reinterpret_cast<const float4*>(bb + c);
-      *reinterpret_cast<float4*>(yr + c) = make_float4(r16e((v[i] - mean) * rstd * wv.x + bv.x, r16) * mk,
-                                                       r16e((v[i + 1] - mean) * rstd * wv.y + bv.y, r16) * mk,
-                                                       r16e((v[i + 2] - mean) * rstd * wv.z + bv.z, r16) * mk,
-                                                       r16e((v[i + 3] - mean) * rstd * wv.w + bv.w, r16) * mk);
+      const float4 o = make_float4(r16e((v[i] - mean) * rstd * wv.x + bv.x, r16) * mk,
+                                   r16e((v[i + 1] - mean) * rstd * wv.y + bv.y, r16) * mk,
+                                   r16e((v[i + 2] - mean) * rstd * wv.z + bv.z, r16) * mk,
+                                   r16e((v[i + 3] - mean) * rstd * wv.w + bv.w, r16) * mk);
+      if (yp.hi) {  // bf16x3 consumer only: the planes its staging would form from these f32 values
+        bf16x4_t h, l;
+        split_bf16x4(o, h, l);
+        *reinterpret_cast<bf16x4_t*>(yp.hi + yo + c) = h;
+        *reinterpret_cast<bf16x4_t*>(yp.lo + yo + c) = l;
+      } else {
+        *reinterpret_cast<float4*>(y + yo + c) = o;
+      }
     }
   } else {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int c = lane + i * 64;
-      if (c < D) yr[c] = r16e((v[i] - mean) * rstd * w[c] + bb[c], r16) * mk;
+      if (c >= D) continue;
+      const float o = r16e((v[i] - mean) * rstd * w[c] + bb[c], r16) * mk;
+      if (yp.hi) split_bf16(o, yp.hi[yo + c], yp.lo[yo + c]);
+      else y[yo + c] = o;
     }
   }
 }
 
 void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
-               float eps, const int* lens, int t_stride, hipStream_t s, int r16) {
+               float eps, const int* lens, int t_stride, hipStream_t s, int r16, APlanes yp) {
   dim3 grid(cdiv(rows, 4));
-  if (D <= 512) hipLaunchKernelGGL(k_layernorm<8>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
-  else if (D <= 640) hipLaunchKernelGGL(k_layernorm<10>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
-  else if (D <= 1024) hipLaunchKernelGGL(k_layernorm<16>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16);
+  const APlanesD yd{reinterpret_cast<__bf16*>(yp.hi), reinterpret_cast<__bf16*>(yp.lo)};
+  if (D <= 512) hipLaunchKernelGGL(k_layernorm<8>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16, yd);
+  else if (D <= 640) hipLaunchKernelGGL(k_layernorm<10>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16, yd);
+  else if (D <= 1024) hipLaunchKernelGGL(k_layernorm<16>, grid, dim3(256), 0, s, x, ldx, y, ldy, w, b, rows, D, eps, lens, t_stride, r16, yd);
   else FA_REQUIRE(false, "layernorm: D > 1024");
 }
 

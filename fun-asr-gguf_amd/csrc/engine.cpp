@@ -878,36 +878,53 @@ struct Engine {
   // ---------------------------------------------------------------------------------------------
   // encoder forward (batch, device pcm)
   void enc_lin(const float* A, int64_t lda, const float* W, const float* b, float* C, int64_t ldc, int M, int N, int K,
-               int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0) {
+               int relu = 0, const float* add1 = nullptr, int64_t ld1 = 0, const float* add2 = nullptr, int64_t ld2 = 0,
+               APlanes ap = {}, APlanes cp = {}) {
     hipEvent_t ev;
     prof_begin(1, &ev);
-    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W), &enc_gemm_wk, WB(W));
+    gemm_linear(A, lda, W, K, b, C, ldc, M, N, K, relu, add1, ld1, add2, ld2, stream, W16(W), &enc_gemm_wk, WB(W), ap,
+                cp);
     prof_end(1, 0, 2.0 * M * N * K);
+  }
+
+  // bf16x3 encoder: the SANM blocks' GEMM inputs (LN1, attention, LN2 and ffn1 outputs, each read only by one bf16x3
+  // GEMM) travel as bf16 hi / lo planes, written by their producers instead of f32 (FUNASR_ENC_PLANES=0: f32, A/B).
+  // Same split as the GEMM staging applies to an f32 row: bit-identical products. The planes of a [rows][ld] tensor
+  // live in the f32 buffer it replaces: hi at its start, lo rows * ld elements later (4 B per element either way).
+  bool enc_planes = true;
+  bool planes_on() const { return enc_planes && !enc_fp16 && enc_gemm; }
+  static APlanes planes_in(float* buf, int rows, int ld) {
+    uint16_t* hi = reinterpret_cast<uint16_t*>(buf);
+    return APlanes{hi, hi + (size_t)rows * ld};
   }
 
   void sanm(const EncBlockW& w, int rows, int ts, const int* lens, bool first) {
     const int d = ec.d_model;
     const float* xin = first ? hbuf : xa;  // block0 input = PE'd LFR features (hbuf holds them)
     float* x = xa;
+    const bool pl = planes_on() && WB(w.qkv_w).hi && WB(w.out_w).hi && WB(w.w1).hi && WB(w.w2).hi;
+    const APlanes p_ln1 = pl ? planes_in(att, rows, w.d_in) : APlanes{}, p_att = pl ? planes_in(att, rows, d) : APlanes{};
+    const APlanes p_ffn = pl ? planes_in(ffn, rows, ec.d_ffn) : APlanes{};
     // LN1
-    layernorm(first ? xin : x, w.d_in, att, w.d_in, w.ln1_w, w.ln1_b, rows, w.d_in, 1e-5f, nullptr, ts, stream, r16());
-    enc_lin(att, w.d_in, w.qkv_w, w.qkv_b, qkv, 3 * d, rows, 3 * d, w.d_in);
+    layernorm(first ? xin : x, w.d_in, att, w.d_in, w.ln1_w, w.ln1_b, rows, w.d_in, 1e-5f, nullptr, ts, stream, r16(),
+              p_ln1);
+    enc_lin(att, w.d_in, w.qkv_w, w.qkv_b, qkv, 3 * d, rows, 3 * d, w.d_in, 0, nullptr, 0, nullptr, 0, p_ln1);
     fsmn(qkv + 2 * d, 3 * d, w.fsmn_w, mem, d, rows, d, ec.fsmn_k, lens, ts, stream, r16());
     {
       hipEvent_t ev;
       prof_begin(2, &ev);
       attn_f32(qkv, qkv + d, qkv + 2 * d, 3 * d, 3 * d, 3 * d, att, d, rows / ts, ts, ec.n_heads, d / ec.n_heads, lens,
-               enc_attn_wk, stream, r16(), bf3_attn());
+               enc_attn_wk, stream, r16(), bf3_attn(), p_att);
       prof_end(2, 0, 4.0 * rows * (double)ts * d);
     }
     if (first) {
-      enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, nullptr, 0, mem, d);
+      enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, nullptr, 0, mem, d, p_att);
       return;
     }
-    enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, x, d, mem, d);
-    layernorm(x, d, hbuf, d, w.ln2_w, w.ln2_b, rows, d, 1e-5f, nullptr, ts, stream, r16());
-    enc_lin(hbuf, d, w.w1, w.b1, ffn, ec.d_ffn, rows, ec.d_ffn, d, 1);
-    enc_lin(ffn, ec.d_ffn, w.w2, w.b2, x, d, rows, d, ec.d_ffn, 0, x, d);
+    enc_lin(att, d, w.out_w, w.out_b, x, d, rows, d, d, 0, x, d, mem, d, p_att);
+    layernorm(x, d, hbuf, d, w.ln2_w, w.ln2_b, rows, d, 1e-5f, nullptr, ts, stream, r16(), p_att);
+    enc_lin(hbuf, d, w.w1, w.b1, ffn, ec.d_ffn, rows, ec.d_ffn, d, 1, nullptr, 0, nullptr, 0, p_att, p_ffn);
+    enc_lin(ffn, ec.d_ffn, w.w2, w.b2, x, d, rows, d, ec.d_ffn, 0, x, d, nullptr, 0, p_ffn);
   }
 
   // CorrectTransformerAdaptor: out [rows][d_out] in `out`; uses hbuf/qkv/att/ffn as scratch
@@ -1717,6 +1734,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_BF3_KW4")) fa::g_gemm_bf3_kw4 = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_F16_DEEP")) fa::g_gemm_f16_deep = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_256_S")) fa::g_gemm_bf3_256_s = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_BF3_DMA")) fa::g_gemm_bf3_dma = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_WAB")) fa::g_attn_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_T_WAB")) fa::g_gemm_t_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;
@@ -1749,6 +1767,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_attn_wide = 256;
     if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation

@@ -50,6 +50,30 @@ struct ALoadPlain {
   }
 };
 
+// bf16x3 A operand already split by its producer (APlanes): 8 k of one plane per 16-B load, lda % 8 == 0, K % 8 == 0
+struct ALoadPlanes {
+  const uint16_t* hi;
+  const uint16_t* lo;
+  int64_t lda;
+  __device__ __forceinline__ void load8(int row, int k, int M, int K, uint4& h, uint4& l) const {
+    if (row >= M || k >= K) {
+      h = l = make_uint4(0, 0, 0, 0);
+      return;
+    }
+    const int64_t o = (int64_t)row * lda + k;
+    h = *reinterpret_cast<const uint4*>(hi + o);
+    l = *reinterpret_cast<const uint4*>(lo + o);
+  }
+};
+template <class AL>
+struct IsPlanes {
+  static constexpr bool value = false;
+};
+template <>
+struct IsPlanes<ALoadPlanes> {
+  static constexpr bool value = true;
+};
+
 // STFT framing (model_definition.py:255 F.pad + conv1d stride 160): row = clip*t_stride + t reads
 // xp[clip][160 t + k] from the 200/200 zero-padded, pre-emphasised signal.
 struct ALoadFrames {
@@ -126,6 +150,8 @@ struct EpiLinear {
   int64_t ld2;
   int relu;
   int r16;            // fp16 mode: Gemm (+bias) output, then each Add, rounded to fp16
+  __bf16* ph = nullptr;  // bf16x3 consumer only (ffn1 -> ffn2): C written as its hi / lo planes (ldc) instead of f32
+  __bf16* pl = nullptr;
   __device__ __forceinline__ void finish(int, int, int, int, float*) const {}  // after every apply of the block
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
@@ -140,7 +166,8 @@ struct EpiLinear {
         if (relu) v = fmaxf(v, 0.f);
         if (add2) v = r16v(v + add2[(int64_t)row * ld2 + col], r16);
         if (add1) v = r16v(add1[(int64_t)row * ld1 + col] + v, r16);
-        C[(int64_t)row * ldc + col] = v;
+        if (ph) split_bf16(v, ph[(int64_t)row * ldc + col], pl[(int64_t)row * ldc + col]);
+        else C[(int64_t)row * ldc + col] = v;
       }
     }
   }
@@ -732,10 +759,23 @@ __device__ __forceinline__ void load_b3(const AL& al, const typename PrecB<P>::E
                                         uint4 (&rh)[TileB3<WM, WN, KB, P>::NB], uint4 (&rl)[TileB3<WM, WN, KB, P>::NB],
                                         int t) {
   using T = TileB3<WM, WN, KB, P>;
+  if constexpr (IsPlanes<AL>::value) {  // ra[0, NA/2): hi chunks, ra[NA/2, NA): lo chunks (8 k each)
+    static_assert(P == 3 && T::NA % 2 == 0, "A planes: bf16x3 only");
+    constexpr int NC = T::NA / 2;
 #pragma unroll
-  for (int i = 0; i < T::NA; ++i) {
-    const int idx = t + i * 256;
-    ra[i] = al.load4(m0 + idx / T::R4, k0 + 4 * (idx % T::R4), M, K);
+    for (int i = 0; i < NC; ++i) {
+      const int idx = t + i * 256;
+      uint4 h, l;
+      al.load8(m0 + idx / T::R8, k0 + 8 * (idx % T::R8), M, K, h, l);
+      ra[i] = __builtin_bit_cast(float4, h);
+      ra[NC + i] = __builtin_bit_cast(float4, l);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < T::NA; ++i) {
+      const int idx = t + i * 256;
+      ra[i] = al.load4(m0 + idx / T::R4, k0 + 4 * (idx % T::R4), M, K);
+    }
   }
 #pragma unroll
   for (int i = 0; i < T::NB; ++i) {
@@ -748,13 +788,23 @@ __device__ __forceinline__ void load_b3(const AL& al, const typename PrecB<P>::E
   }
 }
 
-template <int WM, int WN, int KB, int P>
+template <int WM, int WN, int KB, int P, bool AP = false>
 __device__ __forceinline__ void store_b3(typename PrecB<P>::E* st, const float4 (&ra)[TileB3<WM, WN, KB, P>::NA],
                                          const uint4 (&rh)[TileB3<WM, WN, KB, P>::NB],
                                          const uint4 (&rl)[TileB3<WM, WN, KB, P>::NB], int t) {
   using T = TileB3<WM, WN, KB, P>;
   typedef typename PrecB<P>::E E;
   typedef typename PrecB<P>::V4 V4;
+  if constexpr (AP) {  // A planes (load_b3): whole 16-B chunks per plane, as W
+    constexpr int NC = T::NA / 2;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int idx = t + i * 256;
+      const int o = (idx / T::R8) * T::LDK + 8 * (idx % T::R8);
+      *reinterpret_cast<float4*>(st + o) = ra[i];
+      *reinterpret_cast<float4*>(st + T::PA + o) = ra[NC + i];
+    }
+  } else
 #pragma unroll
   for (int i = 0; i < T::NA; ++i) {
     const int idx = t + i * 256;
@@ -808,7 +858,7 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
   uint4 rh[T::NB], rl[T::NB];
   const int kq = K / KW, kb0 = grp * kq, ke = kb0 + kq;  // host: K % (KW * KB) == 0 when KW > 1
   load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0, M, N, ke, ra, rh, rl, t);
-  store_b3<WM, WN, KB, P>(sh, ra, rh, rl, t);
+  store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh, ra, rh, rl, t);
   __syncthreads();
   const int nk = (kq + KB - 1) / KB;
   auto compute = [&](const E* stage) {
@@ -839,7 +889,7 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
       if (kt + 1 < nk)
         load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 1) * KB, M, N, ke, ra, rh, rl, t);
       compute(sh + cur * T::STAGE);
-      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
       __syncthreads();
     }
   } else if constexpr (PF == 3) {
@@ -848,7 +898,7 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
     if (nk > 1) load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + KB, M, N, ke, ra, rh, rl, t);
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh + (cur ^ 1) * T::STAGE, ra, rh, rl, t);
       if (kt + 2 < nk)
         load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 2) * KB, M, N, ke, ra, rh, rl, t);
       compute(sh + cur * T::STAGE);
@@ -863,13 +913,13 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
     if (nk > 2) load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + 2 * KB, M, N, ke, rb, rhb, rlb, t);
     for (int kt = 0; kt < nk; kt += 2) {
       compute(sh);  // step kt (stage 0)
-      if (kt + 1 < nk) store_b3<WM, WN, KB, P>(sh + T::STAGE, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh + T::STAGE, ra, rh, rl, t);
       if (kt + 3 < nk)
         load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 3) * KB, M, N, ke, ra, rh, rl, t);
       __syncthreads();
       if (kt + 1 >= nk) break;
       compute(sh + T::STAGE);  // step kt + 1 (stage 1)
-      if (kt + 2 < nk) store_b3<WM, WN, KB, P>(sh, rb, rhb, rlb, t);
+      if (kt + 2 < nk) store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh, rb, rhb, rlb, t);
       if (kt + 4 < nk)
         load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0 + (kt + 4) * KB, M, N, ke, rb, rhb, rlb, t);
       __syncthreads();
@@ -961,10 +1011,23 @@ __device__ __forceinline__ void load_b3b(const AL& al, const typename PrecB<P>::
                                          int M, int N, int K, float4 (&ra)[B3B_NA], uint4 (&rh)[B3B_NB],
                                          uint4 (&rl)[B3B_NB], int t) {
   constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
+  if constexpr (IsPlanes<AL>::value) {  // as load_b3
+    static_assert(P == 3 && B3B_NA % 2 == 0, "A planes: bf16x3 only");
+    constexpr int NC = B3B_NA / 2;
 #pragma unroll
-  for (int i = 0; i < B3B_NA; ++i) {
-    const int idx = t + i * B3B_T;
-    ra[i] = al.load4(m0 + idx / R4, k0 + 4 * (idx % R4), M, K);
+    for (int i = 0; i < NC; ++i) {
+      const int idx = t + i * B3B_T;
+      uint4 h, l;
+      al.load8(m0 + idx / R8, k0 + 8 * (idx % R8), M, K, h, l);
+      ra[i] = __builtin_bit_cast(float4, h);
+      ra[NC + i] = __builtin_bit_cast(float4, l);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < B3B_NA; ++i) {
+      const int idx = t + i * B3B_T;
+      ra[i] = al.load4(m0 + idx / R4, k0 + 4 * (idx % R4), M, K);
+    }
   }
 #pragma unroll
   for (int i = 0; i < B3B_NB; ++i) {
@@ -977,12 +1040,22 @@ __device__ __forceinline__ void load_b3b(const AL& al, const typename PrecB<P>::
   }
 }
 
-template <int P>
+template <int P, bool AP = false>
 __device__ __forceinline__ void store_b3b(typename PrecB<P>::E* st, const float4 (&ra)[B3B_NA], const uint4 (&rh)[B3B_NB],
                                           const uint4 (&rl)[B3B_NB], int t) {
   constexpr int R4 = B3B_KB / 4, R8 = B3B_KB / 8;
   typedef typename PrecB<P>::E E;
   typedef typename PrecB<P>::V4 V4;
+  if constexpr (AP) {  // A planes: whole 16-B chunks per plane
+    constexpr int NC = B3B_NA / 2;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int idx = t + i * B3B_T;
+      const int o = (idx / R8) * B3B_LDK + 8 * (idx % R8);
+      *reinterpret_cast<float4*>(st + o) = ra[i];
+      *reinterpret_cast<float4*>(st + B3B_PA + o) = ra[NC + i];
+    }
+  } else
 #pragma unroll
   for (int i = 0; i < B3B_NA; ++i) {
     const int idx = t + i * B3B_T;
@@ -1031,14 +1104,14 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
   float4 ra[B3B_NA];
   uint4 rh[B3B_NB], rl[B3B_NB];
   load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, 0, M, N, K, ra, rh, rl, t);
-  store_b3b<P>(sh, ra, rh, rl, t);
+  store_b3b<P, IsPlanes<AL>::value>(sh, ra, rh, rl, t);
   const int nk = (K + B3B_KB - 1) / B3B_KB;
   if (S == 1 && nk > 1) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, B3B_KB, M, N, K, ra, rh, rl, t);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if constexpr (S == 1) {
-      if (kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
+      if (kt + 1 < nk) store_b3b<P, IsPlanes<AL>::value>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
       if (kt + 2 < nk) load_b3b<AL, P>(al, Wh, Wl, ldw, m0, n0, (kt + 2) * B3B_KB, M, N, K, ra, rh, rl, t);
     }
 #if B3B_VARIANT != 3
@@ -1050,7 +1123,7 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
 #pragma unroll
     for (int kk = 0; kk < B3B_KB / 16; ++kk) {
 #if B3B_VARIANT == 2
-      if (kk == 1 && kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
+      if (kk == 1 && kt + 1 < nk) store_b3b<P, IsPlanes<AL>::value>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
 #endif
       V8 ah[WM], alo[WM], bh[WN], blo[WN];
 #pragma unroll
@@ -1082,7 +1155,7 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
 #endif
     }
 #if B3B_VARIANT != 2 && B3B_VARIANT != 3
-    if (S == 0 && kt + 1 < nk) store_b3b<P>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
+    if (S == 0 && kt + 1 < nk) store_b3b<P, IsPlanes<AL>::value>(sh + (cur ^ 1) * STAGE, ra, rh, rl, t);
 #endif
     __syncthreads();
   }
@@ -1108,10 +1181,128 @@ static void launch_gemm_b3_256_s(const AL& al, const WSplit& w, int64_t ldw, int
                      reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
 }
 
+// ---- 256x256 bf16x3 tile with both operands as bf16 planes (A from its producer's APlanes), staged by LDS-DMA
+// (global_load_lds_dwordx4) into a ring of G_NB 16-deep K-tiles, three K-tiles in flight across each barrier: the
+// wait that retires tile kt is a counted `s_waitcnt vmcnt` (4 DMA instructions per wave per K-tile) and the barrier a
+// raw s_barrier, so later tiles' DMA stays in flight (cdna_hip_programming.md §5 "Pipelining across barriers"). No
+// staging registers, no ds_writes, no A split. Per buffer: 4 planes [Ah][Al][Wh][Wl] of 256 rows x 32 B; a DMA
+// wave-instruction fills 32 rows (1 KiB, lane-linear), so the bank swizzle (16-B chunk ^= (row >> 3) & 1, which
+// puts every 16-lane group of a fragment read on 16 distinct 16-B slots) is applied to the per-lane SOURCE address
+// and undone on the read (§5.4 rule 21). Rows past M / N load row M-1 / N-1 (their products land only in
+// accumulator rows / columns the epilogue never stores). Same wave tiling, per-element MFMA order (lo.hi, hi.lo,
+// hi.hi per 16 of k, k ascending) and epilogue as k_gemm_bf3_256: bit-identical outputs.
+int g_gemm_bf3_dma = 1;  // 1: planes-A 256x256 launches on k_gemm_bf3_256d (FUNASR_BF3_DMA; 0 = register staging)
+constexpr int G_KB = 16, G_NB = 4;
+constexpr int G_PLANE = 256 * G_KB;  // bf16 per plane per buffer (8 KiB)
+constexpr int G_BUF = 4 * G_PLANE;   // one K-tile: [Ah][Al][Wh][Wl]
+constexpr size_t G_LDS = std::max<size_t>((size_t)G_NB * G_BUF * 2, (4096 + 8 * 32 * 33) * 4);  // >= EpiArgmax256
+
+template <class EPI>
+__global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256d(ALoadPlanes al, const __bf16* __restrict__ Wh,
+                                                             const __bf16* __restrict__ Wl, int64_t ldw, int M, int N,
+                                                             int K, EPI epi) {
+  constexpr int WM = 4, WN = 2;
+  extern __shared__ float smem[];  // the ring; the epilogue reuses it
+  int tm, tn;
+  if (!xcd_tile((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, tm, tn)) return;
+  const int m0 = tm * B3B_BM, n0 = tn * B3B_BN;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int r = lane & 31, h = lane >> 5;
+  __bf16* ring = reinterpret_cast<__bf16*>(smem);
+  // DMA: wave w fills plane w >> 1 (0 Ah, 1 Al, 2 Wh, 3 Wl), 32-row chunks c = 4 (w & 1) + i, i < 4; lane s -> row
+  // 32 c + (s >> 1), source chunk (s & 1) ^ ((s >> 4) & 1) (= the swizzle of that row)
+  const int pl = wave >> 1;
+  const int koff = 8 * ((lane & 1) ^ ((lane >> 4) & 1));
+  const __bf16* src[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 32 * (4 * (wave & 1) + i) + (lane >> 1);
+    if (pl < 2) {
+      const int gr = min(m0 + row, M - 1);
+      src[i] = reinterpret_cast<const __bf16*>(pl == 0 ? al.hi : al.lo) + (int64_t)gr * al.lda + koff;
+    } else {
+      const int gr = min(n0 + row, N - 1);
+      src[i] = (pl == 2 ? Wh : Wl) + (int64_t)gr * ldw + koff;
+    }
+  }
+  const int ldsw = pl * G_PLANE + 32 * G_KB * 4 * (wave & 1);  // this wave's first chunk in a buffer (elements)
+  auto issue = [&](int kt) {
+    __bf16* d = ring + (kt % G_NB) * G_BUF + ldsw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * G_KB),
+                                       (__attribute__((address_space(3))) void*)(d + i * 32 * G_KB), 16, 0, 0);
+  };
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  const int nk = K / G_KB;  // host: K % 16 == 0
+  // fragment read offsets (elements): row * 16 + 8 * (h ^ swizzle(row)); rows of a sub-tile differ from r by
+  // multiples of 32, so the swizzle bit is (r >> 3) & 1 for all of them
+  const int fo = r * G_KB + 8 * (h ^ ((r >> 3) & 1));
+  const int fa = (wr * 32 * WM) * G_KB + fo, fb = 2 * G_PLANE + (wc * 32 * WN) * G_KB + fo;
+  for (int s = 0; s < G_NB - 1 && s < nk; ++s) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire this wave's DMA of tile kt (tiles kt + 1, kt + 2 may stay in flight), then the barrier makes every
+    // wave's part visible and frees buffer (kt - 1) % G_NB (read in step kt - 1 by all waves) for tile kt + 3
+    const int ahead = min(G_NB - 2, nk - 1 - kt);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + G_NB - 1 < nk) issue(kt + G_NB - 1);
+    const __bf16* b = ring + (kt % G_NB) * G_BUF;
+    bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(b + fb + 32 * j * G_KB);
+      blo[j] = *reinterpret_cast<const bf16x8*>(b + fb + G_PLANE + 32 * j * G_KB);
+    }
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(b + fa + 32 * i * G_KB);
+      alo[i] = *reinterpret_cast<const bf16x8*>(b + fa + G_PLANE + 32 * i * G_KB);
+    }
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) mma_step<3>(acc[i][j], ah[i], alo[i], bh[j], blo[j]);
+  }
+  __syncthreads();  // every wave's last fragment reads done before an epilogue reuses the LDS (no DMA in flight)
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+  epi.finish(m0, n0, M, N, smem);
+}
+
+template <class EPI>
+static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t ldw, int M, int N, int K,
+                                const EPI& epi, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256d<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)G_LDS));
+    attr = true;
+  }
+  const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
+  hipLaunchKernelGGL((k_gemm_bf3_256d<EPI>), grid, dim3(B3B_T), G_LDS, s, al, reinterpret_cast<const __bf16*>(w.hi),
+                     reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+}
+
 template <class AL, class EPI, int P = 3>
 static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                                hipStream_t s) {
   FA_REQUIRE(K % 8 == 0 && ldw % 8 == 0, "gemm_bf3_256: K and ldw must be multiples of 8");
+  if constexpr (IsPlanes<AL>::value && P == 3) {
+    if (g_gemm_bf3_dma && K % G_KB == 0 && M > 0 && N > 0) {
+      launch_gemm_b3_256d<EPI>(al, w, ldw, M, N, K, epi, s);
+      return;
+    }
+  }
   if (g_gemm_bf3_256_s) launch_gemm_b3_256_s<AL, EPI, P, 1>(al, w, ldw, M, N, K, epi, s);
   else launch_gemm_b3_256_s<AL, EPI, P, 0>(al, w, ldw, M, N, K, epi, s);
 }
@@ -1187,9 +1378,19 @@ void launch_split_bf16(const float* w, uint16_t* hi, uint16_t* lo, int64_t n, hi
 
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16, const GemmF32Work* wk, WSplit wb) {
+                 hipStream_t s, const __half* W16, const GemmF32Work* wk, WSplit wb, APlanes ap, APlanes cp) {
   ALoadPlain al{A, lda};
   EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
+  if (ap.hi || cp.hi) FA_REQUIRE(wb.hi && !W16, "gemm_linear: bf16 activation planes need the bf16x3 mode");
+  if (cp.hi) {
+    epi.ph = reinterpret_cast<__bf16*>(cp.hi);
+    epi.pl = reinterpret_cast<__bf16*>(cp.lo);
+  }
+  if (ap.hi) {
+    FA_REQUIRE(lda % 8 == 0 && K % 8 == 0, "gemm_linear: A planes need lda % 8 == 0 and K % 8 == 0");
+    run_gemm_b3(ALoadPlanes{ap.hi, ap.lo, lda}, wb, ldw, M, N, K, epi, s);
+    return;
+  }
   if (W16 && g_gemm_f16_b3) run_gemm_b3<ALoadPlain, EpiLinear, 1>(al, WSplit{reinterpret_cast<const uint16_t*>(W16)}, ldw, M, N, K, epi, s);
   else if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
   else if (wb.hi) run_gemm_b3(al, wb, ldw, M, N, K, epi, s);

@@ -39,6 +39,7 @@ extern int g_gemm_f32_wab;  // exact-f32 GEMM tiles: 1 = write-after-barrier sta
 extern int g_gemm_t_wab;  // k_gemm_q8_t: 1 = write-after-barrier staging
 extern int g_attn_wab;  // k_attn_bf3: 1 = write-after-barrier K/V staging
 extern int g_gemm_bf3_256_s;  // 256x256 tile: 1 = write-after-barrier staging
+extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gemm_bf3_256d; default 1)
 extern int g_gemm_f16_deep;  // fp16 one-clip GEMMs on 128-deep stages (default 1)
 extern int g_gemm_bf3_kw4;  // 1: four K groups per block for few-tile K >= 2048 shapes (FUNASR_BF3_KW4)
 extern int g_gemm_bf3_mid;  // 1: 128x64 tiles for one clip's 256-1024-tile GEMM shapes (A/B, default 0)
@@ -48,11 +49,19 @@ struct WSplit {
   const uint16_t* lo = nullptr;
 };
 void launch_split_bf16(const float* w, uint16_t* hi, uint16_t* lo, int64_t n, hipStream_t s);
+// the same split of an f32 ACTIVATION, written by its producer (layernorm, encoder attention, ffn1 epilogue) in place of
+// the f32 tensor when only a bf16x3 GEMM reads it: element (row, col) at hi / lo + row * ld + col, ld = the f32 tensor's
+// row stride (raw bf16 bits)
+struct APlanes {
+  uint16_t* hi = nullptr;
+  uint16_t* lo = nullptr;
+};
 // W16 != nullptr: fp16 mode (C5) on the f16 MFMA kernel with the fp16 weight copy W16, every op output rounded to fp16;
 // else wb.hi != nullptr: f32 mode on the bf16x3 split kernel; else the exact-f32 MFMA kernel
 void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias, float* C, int64_t ldc,
                  int M, int N, int K, int relu, const float* add1, int64_t ld1, const float* add2, int64_t ld2,
-                 hipStream_t s, const __half* W16 = nullptr, const GemmF32Work* wk = nullptr, WSplit wb = {});
+                 hipStream_t s, const __half* W16 = nullptr, const GemmF32Work* wk = nullptr, WSplit wb = {},
+                 APlanes ap = {}, APlanes cp = {});  // ap.hi: A read from planes (lda); cp.hi: C written as planes (ldc)
 void gemm_stft_power(const float* xp, int64_t xp_stride, int t_stride, int M, const float* basis, float* power,
                      int64_t ldp, hipStream_t s, int r16 = 0);
 void gemm_mel_log(const float* power, int64_t ldp, const float* fbank, int64_t ldf, float* mel, int M, int n_mels,
@@ -99,7 +108,8 @@ constexpr int64_t ATTN_F32_COUNTERS = 512;
 int attn_f32_splits(int batch, int t_stride, int n_heads);
 void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64_t ldk, int64_t ldv, float* O,
               int64_t ldo, int batch, int t_stride, int n_heads, int head_dim, const int* lens,
-              const AttnF32Work& wk, hipStream_t s, int r16 = 0, int bf3 = 0);  // bf3: bf16x3 split MFMA products
+              const AttnF32Work& wk, hipStream_t s, int r16 = 0, int bf3 = 0,  // bf3: bf16x3 split MFMA products
+              APlanes op = {});  // op.hi (bf3 only): O written as bf16 planes (ldo) instead of f32
 
 // enc_misc.hip
 void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_samples, int batch, float* partial,
@@ -107,7 +117,8 @@ void frontend_preemph(const float* pcm, int64_t stride, const int64_t* d_n_sampl
 void frontend_lfr(const float* mel, int mel_stride, const int* t_mel_valid, const int* t_lfr_valid, const float* pe,
                   float* x, int batch, int t_stride, int n_mels, int lfr_m, int lfr_n, hipStream_t s, int r16 = 0);
 void layernorm(const float* x, int64_t ldx, float* y, int64_t ldy, const float* w, const float* b, int rows, int D,
-               float eps, const int* lens, int t_stride, hipStream_t s, int r16 = 0);
+               float eps, const int* lens, int t_stride, hipStream_t s, int r16 = 0,
+               APlanes yp = {});  // yp.hi: y written as bf16 planes (ldy) instead of f32
 void fsmn(const float* v, int64_t ldv, const float* w, float* out, int64_t ldo, int rows, int C, int ksize,
           const int* lens, int t_stride, hipStream_t s, int r16 = 0);
 void ctc_collapse(const int* ids, int64_t ids_stride, const int* lens, int batch, int blank, int* out_ids,

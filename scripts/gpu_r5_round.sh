@@ -31,13 +31,15 @@ if [[ " $STEPS " == *" pmc "* ]]; then
     d=gpurun_out/pmc_fetch_pf$pf
     FUNASR_L2PF=$pf timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $d -o run -- $B > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
     f=$(find $d -name "*results.db" | head -1)
-    python3 scripts/pmc_traffic.py $f gpurun_out/pmc_gemv_pf$pf.json > /dev/null && echo "fetch pf$pf ok"
+    python3 scripts/pmc_traffic.py $f gpurun_out/pmc_gemv_pf$pf.json > gpurun_out/pmc_gemv_pf$pf.txt && echo "fetch pf$pf ok"
+    rm -rf $d
   done
   for pf in 0 16; do
     d=gpurun_out/pmc_hit_pf$pf
     FUNASR_L2PF=$pf AB_REPS=1 timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d $d -o run -- \
       python3 -u scripts/prof_decode_ab.py 32 - > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
     f=$(find $d -name "*results.db" | head -1)
-    python3 scripts/pmc_l2hit.py $f gpurun_out/pmc_l2hit_pf$pf.json "FUNASR_L2PF=$pf" > /dev/null && echo "l2hit pf$pf ok"
+    python3 scripts/pmc_l2hit.py $f gpurun_out/pmc_l2hit_pf$pf.json "FUNASR_L2PF=$pf" > gpurun_out/pmc_l2hit_pf$pf.txt && echo "l2hit pf$pf ok"
+    rm -rf $d
   done
 fi

@@ -676,3 +676,31 @@ def test_write_after_barrier_gemm_staging_bit_identical(monkeypatch):
         assert np.array_equal(outs[0]["enc"][b], outs[1]["enc"][b]), f"clip {b}: encoder rows"
         assert np.array_equal(outs[0]["audio_embd"][b], outs[1]["audio_embd"][b]), f"clip {b}: adaptor rows"
         assert np.array_equal(outs[0]["ctc_ids"][b], outs[1]["ctc_ids"][b]), f"clip {b}: CTC ids"
+
+
+def test_encoder_activation_planes_bit_identical(monkeypatch):
+    """bf16x3 encoder: the SANM blocks' GEMM inputs written as bf16 hi / lo planes by their producers (layernorm, the
+    attention epilogue, the ffn1 epilogue; FUNASR_ENC_PLANES=1, the default) instead of f32 rows split by the GEMM's
+    staging. The split is the same, so every product is: a batch of eight 60 s clips (the 256x256 tile) and one 60 s
+    clip (the few-tile shapes) encode bit-identically with FUNASR_ENC_PLANES=0, with the 256x256 tile's planes staged
+    by LDS-DMA (k_gemm_bf3_256d, FUNASR_BF3_DMA=1, the default) and by registers (=0)."""
+    from fun_asr_gguf import _native
+    from fun_asr_gguf.synthetic import synth_audio
+    clips = [synth_audio(SR * 60, 400 + i) for i in range(8)]
+    outs = []
+    for planes, dma in (("0", "1"), ("1", "1"), ("1", "0")):
+        monkeypatch.setenv("FUNASR_ENC_PLANES", planes)
+        monkeypatch.setenv("FUNASR_BF3_DMA", dma)
+        e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=8,
+                           max_samples=SR * 62)
+        try:
+            e.synthetic_weights(0)
+            outs.append((e.encode(clips, want_enc=True), e.encode(clips[3:4], want_enc=True)))
+        finally:
+            e.close()
+    for v in (1, 2):
+        for k in range(2):
+            for b in range(len(outs[0][k]["enc"])):
+                assert np.array_equal(outs[0][k]["enc"][b], outs[v][k]["enc"][b]), f"mode {v} call {k} clip {b}: encoder"
+                assert np.array_equal(outs[0][k]["audio_embd"][b], outs[v][k]["audio_embd"][b]), f"mode {v} {k} {b}"
+                assert np.array_equal(outs[0][k]["ctc_ids"][b], outs[v][k]["ctc_ids"][b]), f"mode {v} {k} {b}: CTC ids"
