@@ -137,21 +137,32 @@ __global__ void k_layernorm(const float* __restrict__ x, int64_t ldx, float* __r
   }
   const int64_t yo = (int64_t)row * ldy;
   if (vec) {
+    float4 o[PER / 4];
 #pragma unroll
     for (int i = 0; i < PER; i += 4) {
       const int c = lane * PER + i;
       const float4 wv = *reinterpret_cast<const float4*>(w + c), bv = *reinterpret_cast<const float4*>(bb + c);
-      const float4 o = make_float4(r16e((v[i] - mean) * rstd * wv.x + bv.x, r16) * mk,
-                                   r16e((v[i + 1] - mean) * rstd * wv.y + bv.y, r16) * mk,
-                                   r16e((v[i + 2] - mean) * rstd * wv.z + bv.z, r16) * mk,
-                                   r16e((v[i + 3] - mean) * rstd * wv.w + bv.w, r16) * mk);
-      if (yp.hi) {  // bf16x3 consumer only: the planes its staging would form from these f32 values
-        bf16x4_t h, l;
-        split_bf16x4(o, h, l);
-        *reinterpret_cast<bf16x4_t*>(yp.hi + yo + c) = h;
-        *reinterpret_cast<bf16x4_t*>(yp.lo + yo + c) = l;
-      } else {
-        *reinterpret_cast<float4*>(y + yo + c) = o;
+      o[i / 4] = make_float4(r16e((v[i] - mean) * rstd * wv.x + bv.x, r16) * mk,
+                             r16e((v[i + 1] - mean) * rstd * wv.y + bv.y, r16) * mk,
+                             r16e((v[i + 2] - mean) * rstd * wv.z + bv.z, r16) * mk,
+                             r16e((v[i + 3] - mean) * rstd * wv.w + bv.w, r16) * mk);
+      if (!yp.hi) *reinterpret_cast<float4*>(y + yo + c) = o[i / 4];
+    }
+    if (yp.hi) {  // bf16x3 consumer only: the planes its staging would form from these f32 values, 16 B per store
+      typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int i = 0; i < PER; i += 8) {
+        bf16x4_t h0, l0, h1, l1;
+        split_bf16x4(o[i / 4], h0, l0);
+        if (i + 4 < PER) split_bf16x4(o[i / 4 + 1], h1, l1);
+        const int c = lane * PER + i;
+        if (i + 8 <= PER) {
+          *reinterpret_cast<bf16x8_t*>(yp.hi + yo + c) = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+          *reinterpret_cast<bf16x8_t*>(yp.lo + yo + c) = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+          *reinterpret_cast<bf16x4_t*>(yp.hi + yo + c) = h0;
+          *reinterpret_cast<bf16x4_t*>(yp.lo + yo + c) = l0;
+        }
       }
     }
   } else {

@@ -1735,6 +1735,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_F16_DEEP")) fa::g_gemm_f16_deep = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_256_S")) fa::g_gemm_bf3_256_s = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_DMA")) fa::g_gemm_bf3_dma = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_BF3_PERSIST")) fa::g_gemm_bf3_persist = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_WAB")) fa::g_attn_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_T_WAB")) fa::g_gemm_t_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_F32_WAB")) fa::g_gemm_f32_wab = atoi(g) != 0;

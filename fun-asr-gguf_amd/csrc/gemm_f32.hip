@@ -381,13 +381,29 @@ struct EpiArgmax256 {
 // contiguous run of tile ids, and ids run through bands of 4 M-tiles (all N-tiles of a band, M fastest), so an XCD's
 // blocks share a few A row bands and W column bands in its L2 instead of every XCD streaming all of A and W.
 // Placement only decides speed; every tile is computed exactly once either way. false: padding block (no tile).
+__device__ __forceinline__ void xcd_tile_of(int t, int nbx, int nby, int& tm, int& tn) {
+  const int g = t / (4 * nbx), fm = 4 * g, gs = min(4, nby - fm), r = t - g * 4 * nbx;
+  tm = fm + r % gs;
+  tn = r / gs;
+}
 __device__ __forceinline__ bool xcd_tile(int nbx, int nby, int& tm, int& tn) {
   const int T = nbx * nby, per = (T + 7) >> 3, b = blockIdx.x;
   const int t = (b & 7) * per + (b >> 3);
   if (t >= T) return false;
-  const int g = t / (4 * nbx), fm = 4 * g, gs = min(4, nby - fm), r = t - g * 4 * nbx;
-  tm = fm + r % gs;
-  tn = r / gs;
+  xcd_tile_of(t, nbx, nby, tm, tn);
+  return true;
+}
+// Persistent form (gridDim.x a multiple of 8, at most one block per CU): block b's it-th tile is local index
+// (b >> 3) + it * gridDim.x / 8 of XCD b % 8's contiguous run, so every tile is computed exactly once, on the XCD the
+// one-block-per-tile grid would have used, and a block's epilogue stores stay in flight while its next tile's loads
+// are issued. false: no tile left for this block.
+__device__ __forceinline__ bool xcd_tile_it(int nbx, int nby, int it, bool persist, int& tm, int& tn) {
+  if (!persist) return it == 0 && xcd_tile(nbx, nby, tm, tn);
+  const int T = nbx * nby, per = (T + 7) >> 3, b = blockIdx.x;
+  const int li = (b >> 3) + it * ((int)gridDim.x >> 3);
+  const int t = (b & 7) * per + li;
+  if (li >= per || t >= T) return false;
+  xcd_tile_of(t, nbx, nby, tm, tn);
   return true;
 }
 inline dim3 xcd_grid(int nbx, int nby, int ks = 1) { return dim3(((nbx * nby + 7) >> 3) << 3, 1, ks); }
@@ -1080,7 +1096,7 @@ __device__ __forceinline__ void store_b3b(typename PrecB<P>::E* st, const float4
 // S = 1: write-after-barrier staging (cdna_hip_programming.md T14): step kt first stores the registers holding tile
 // kt + 1 (loaded a whole step earlier) into the free stage, re-issues the loads of tile kt + 2 into the same registers,
 // then computes tile kt; S = 0 loads tile kt + 1 at the top of step kt and stores it after the compute. Same MFMA order.
-template <class AL, class EPI, int P = 3, int S = 0>
+template <class AL, class EPI, int P = 3, int S = 0, bool PER = false>
 __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename PrecB<P>::E* __restrict__ Wh,
                                                             const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw,
                                                             int M, int N, int K, EPI epi) {
@@ -1089,8 +1105,10 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
   typedef typename PrecB<P>::E E;
   typedef typename PrecB<P>::V8 V8;
   extern __shared__ float smem[];  // 2 stages; the epilogue reuses it
+  for (int it = 0; it < (PER ? 0x7fffffff : 1); ++it) {
   int tm, tn;
-  if (!xcd_tile((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, tm, tn)) return;
+  if (!xcd_tile_it((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, it, PER, tm, tn)) return;
+  if (PER && it) __syncthreads();  // the previous tile's epilogue may have used the LDS
   const int m0 = tm * B3B_BM, n0 = tn * B3B_BN;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int wr = wave >> 2, wc = wave & 3;
@@ -1164,7 +1182,22 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
 #pragma unroll
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
   epi.finish(m0, n0, M, N, smem);
+  }
 }
+
+int g_gemm_bf3_persist = 0;  // 256x256 tiles: persistent blocks, one per CU (FUNASR_BF3_PERSIST; A/B)
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    FA_HIP(hipGetDevice(&dev));
+    FA_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    n = std::max(8, n & ~7);
+  }
+  return n;
+}
+// persistent grid: one block per CU (a multiple of 8), never more blocks than the one-block-per-tile grid
+static dim3 persist_grid(const dim3& g) { return dim3(std::min<unsigned>(g.x, (unsigned)cu_count()), 1, 1); }
 
 template <class AL, class EPI, int P, int S>
 static void launch_gemm_b3_256_s(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
@@ -1174,11 +1207,17 @@ static void launch_gemm_b3_256_s(const AL& al, const WSplit& w, int64_t ldw, int
   if (!attr) {
     FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI, P, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)B3BT<P>::LDS));
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256<AL, EPI, P, S, true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)B3BT<P>::LDS));
     attr = true;
   }
   const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
-  hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P, S>), grid, dim3(B3B_T), B3BT<P>::LDS, s, al,
-                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
+  if (g_gemm_bf3_persist)
+    hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P, S, true>), persist_grid(grid), dim3(B3B_T), B3BT<P>::LDS, s, al,
+                       reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
+  else
+    hipLaunchKernelGGL((k_gemm_bf3_256<AL, EPI, P, S>), grid, dim3(B3B_T), B3BT<P>::LDS, s, al,
+                       reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
 }
 
 // ---- 256x256 bf16x3 tile with both operands as bf16 planes (A from its producer's APlanes), staged by LDS-DMA
@@ -1197,14 +1236,16 @@ constexpr int G_PLANE = 256 * G_KB;  // bf16 per plane per buffer (8 KiB)
 constexpr int G_BUF = 4 * G_PLANE;   // one K-tile: [Ah][Al][Wh][Wl]
 constexpr size_t G_LDS = std::max<size_t>((size_t)G_NB * G_BUF * 2, (4096 + 8 * 32 * 33) * 4);  // >= EpiArgmax256
 
-template <class EPI>
+template <class EPI, bool PER = false>
 __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256d(ALoadPlanes al, const __bf16* __restrict__ Wh,
                                                              const __bf16* __restrict__ Wl, int64_t ldw, int M, int N,
                                                              int K, EPI epi) {
   constexpr int WM = 4, WN = 2;
   extern __shared__ float smem[];  // the ring; the epilogue reuses it
+  for (int it = 0; it < (PER ? 0x7fffffff : 1); ++it) {
   int tm, tn;
-  if (!xcd_tile((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, tm, tn)) return;
+  if (!xcd_tile_it((N + B3B_BN - 1) / B3B_BN, (M + B3B_BM - 1) / B3B_BM, it, PER, tm, tn)) return;
+  if (PER && it) __syncthreads();  // the previous tile's epilogue may have used the LDS (no DMA in flight)
   const int m0 = tm * B3B_BM, n0 = tn * B3B_BN;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int wr = wave >> 2, wc = wave & 3;
@@ -1277,6 +1318,7 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256d(ALoadPlanes al, cons
 #pragma unroll
     for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
   epi.finish(m0, n0, M, N, smem);
+  }
 }
 
 template <class EPI>
@@ -1286,11 +1328,17 @@ static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t 
   if (!attr) {
     FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256d<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)G_LDS));
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_256d<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)G_LDS));
     attr = true;
   }
   const dim3 grid = xcd_grid(cdiv(N, B3B_BN), cdiv(M, B3B_BM));
-  hipLaunchKernelGGL((k_gemm_bf3_256d<EPI>), grid, dim3(B3B_T), G_LDS, s, al, reinterpret_cast<const __bf16*>(w.hi),
-                     reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+  if (g_gemm_bf3_persist)
+    hipLaunchKernelGGL((k_gemm_bf3_256d<EPI, true>), persist_grid(grid), dim3(B3B_T), G_LDS, s, al,
+                       reinterpret_cast<const __bf16*>(w.hi), reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
+  else
+    hipLaunchKernelGGL((k_gemm_bf3_256d<EPI>), grid, dim3(B3B_T), G_LDS, s, al, reinterpret_cast<const __bf16*>(w.hi),
+                       reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
 template <class AL, class EPI, int P = 3>

@@ -39,6 +39,7 @@ extern int g_gemm_f32_wab;  // exact-f32 GEMM tiles: 1 = write-after-barrier sta
 extern int g_gemm_t_wab;  // k_gemm_q8_t: 1 = write-after-barrier staging
 extern int g_attn_wab;  // k_attn_bf3: 1 = write-after-barrier K/V staging
 extern int g_gemm_bf3_256_s;  // 256x256 tile: 1 = write-after-barrier staging
+extern int g_gemm_bf3_persist;  // 256x256 tiles as persistent blocks, one per CU (A/B, default 0)
 extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gemm_bf3_256d; default 1)
 extern int g_gemm_f16_deep;  // fp16 one-clip GEMMs on 128-deep stages (default 1)
 extern int g_gemm_bf3_kw4;  // 1: four K groups per block for few-tile K >= 2048 shapes (FUNASR_BF3_KW4)

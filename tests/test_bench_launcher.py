@@ -72,3 +72,18 @@ def test_bench_module_imports_no_torch():
     r = subprocess.run([sys.executable, "-c", f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
                         "print('torch' in sys.modules)"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "False", r.stderr
+
+
+def test_roofline_traffic_from_the_slabs_off_counter_pass():
+    """roofline.traffic is FETCH_SIZE x 2 per decode-layer launch from the committed slabs-off pass, with the slabs-on
+    traffic and the per-launch L2 hit rates of both passes beside it (profiles/r05_pmc_*)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    got = bench.pmc_traffic()
+    assert got is not None
+    traffic, src, extra = got
+    assert "slabs_off" in src
+    d = json.load(open(os.path.join(ROOT, src)))["decode_layer_gemv_mean"]
+    assert traffic == round(d["traffic_bytes"]) and 1.0 < extra["traffic_over_weight_bytes"] < 1.3
+    assert extra["traffic_slabs_on"] > traffic
+    assert set(extra["l2_hit_rate_slabs_off"]) == set(extra["l2_hit_rate_slabs_on"]) == {"k_attn_o<true>", "k_ffn_fused<1>"}

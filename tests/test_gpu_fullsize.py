@@ -688,9 +688,11 @@ def test_encoder_activation_planes_bit_identical(monkeypatch):
     from fun_asr_gguf.synthetic import synth_audio
     clips = [synth_audio(SR * 60, 400 + i) for i in range(8)]
     outs = []
-    for planes, dma in (("0", "1"), ("1", "1"), ("1", "0")):
+    modes = (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1"), ("1", "1", "1"), ("1", "0", "1"))
+    for planes, dma, persist in modes:  # ..., and as persistent blocks (FUNASR_BF3_PERSIST=1)
         monkeypatch.setenv("FUNASR_ENC_PLANES", planes)
         monkeypatch.setenv("FUNASR_BF3_DMA", dma)
+        monkeypatch.setenv("FUNASR_BF3_PERSIST", persist)
         e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=8,
                            max_samples=SR * 62)
         try:
@@ -698,7 +700,7 @@ def test_encoder_activation_planes_bit_identical(monkeypatch):
             outs.append((e.encode(clips, want_enc=True), e.encode(clips[3:4], want_enc=True)))
         finally:
             e.close()
-    for v in (1, 2):
+    for v in range(1, len(modes)):
         for k in range(2):
             for b in range(len(outs[0][k]["enc"])):
                 assert np.array_equal(outs[0][k]["enc"][b], outs[v][k]["enc"][b]), f"mode {v} call {k} clip {b}: encoder"
