@@ -156,6 +156,28 @@ struct EpiLinear {
   __device__ __forceinline__ void apply(const f32x16& acc, int row0, int col0, int M, int N, float* lds) const {
     int lane = threadIdx.x & 63;
     int col = col0 + (lane & 31);
+    if (ph) {  // planes (host: N even): lane pairs swap values so the even lane stores the hi pair, the odd the lo pair
+      const bool cin = col < N;
+      const float b = bias && cin ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const bool in = cin && row < M;
+        float v = acc[r] + b;
+        if (relu) v = fmaxf(v, 0.f);
+        if (add2 && in) v = v + add2[(int64_t)row * ld2 + col];
+        if (add1 && in) v = add1[(int64_t)row * ld1 + col] + v;
+        __bf16 h, l;
+        split_bf16(v, h, l);
+        const float mine = __uint_as_float(((uint32_t)__builtin_bit_cast(unsigned short, l) << 16) | __builtin_bit_cast(unsigned short, h));
+        const uint32_t other = __float_as_uint(__shfl_xor(mine, 1, 64));  // the neighbour column's (hi, lo)
+        const uint32_t me = __float_as_uint(mine);
+        // even lane: (hi[col], hi[col + 1]); odd lane: (lo[col - 1], lo[col])
+        const uint32_t word = (lane & 1) ? ((other >> 16) | (me & 0xffff0000u)) : ((me & 0xffffu) | (other << 16));
+        if (in) *reinterpret_cast<uint32_t*>((lane & 1) ? pl + (int64_t)row * ldc + col - 1 : ph + (int64_t)row * ldc + col) = word;
+      }
+      return;
+    }
     if (col >= N) return;
     float b = bias ? r16v(bias[col], r16) : 0.f;
 #pragma unroll
@@ -166,8 +188,7 @@ struct EpiLinear {
         if (relu) v = fmaxf(v, 0.f);
         if (add2) v = r16v(v + add2[(int64_t)row * ld2 + col], r16);
         if (add1) v = r16v(add1[(int64_t)row * ld1 + col] + v, r16);
-        if (ph) split_bf16(v, ph[(int64_t)row * ldc + col], pl[(int64_t)row * ldc + col]);
-        else C[(int64_t)row * ldc + col] = v;
+        C[(int64_t)row * ldc + col] = v;
       }
     }
   }
@@ -1431,6 +1452,7 @@ void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const
   EpiLinear epi{C, ldc, bias, add1, ld1, add2, ld2, relu, W16 ? 1 : 0};
   if (ap.hi || cp.hi) FA_REQUIRE(wb.hi && !W16, "gemm_linear: bf16 activation planes need the bf16x3 mode");
   if (cp.hi) {
+    FA_REQUIRE(N % 2 == 0 && ldc % 2 == 0, "gemm_linear: C planes need even N and ldc");
     epi.ph = reinterpret_cast<__bf16*>(cp.hi);
     epi.pl = reinterpret_cast<__bf16*>(cp.lo);
   }

@@ -24,6 +24,13 @@ import json; d=json.loads(open('gpurun_out/bench.json').read().strip().splitline
 print('C2', d['value'], d['stage_ms'], 'step1', d.get('decode_step_ms_graph')); print('roof', d['roofline']['frac'], d['roofline']['avg_launch_us'])
 print('C3', d['c3']['value'], d['c3'].get('stage_ms'), 'step32', d['c3'].get('decode_step_ms_graph')); print('C4', d['c4']['value'], 'C5', d['c5']['value'], 'c5_long', d['c5_long']['value'])"
 fi
+if [[ " $STEPS " == *" trace "* ]]; then  # per-kernel device time of the bench workload, graph-replayed decode
+  d=gpurun_out/prof
+  DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run -- python3 bench.py \
+    --steps 3 --warmup 1 --no-cpu-baseline --c3-varlen 0 > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+  python3 scripts/prof_summary.py $(find $d -name "*results.db" | head -1) 45 > gpurun_out/prof_summary.txt; rm -rf $d
+  echo "trace ok"
+fi
 if [[ " $STEPS " == *" pmc "* ]]; then
   export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
   B="python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --c3-batch 0 --c3-varlen 0 --no-c4"
