@@ -182,6 +182,9 @@ struct Engine {
   float* d_ssp = nullptr;  // batched decode: per-token sum-of-squares partials [max_seqs][32] of the residual stream
   AttnF32Work enc_attn_wk;
   GemmF32Work enc_gemm_wk;
+  unsigned* gd_cnt = nullptr;  // gemv_gu_down hand-off counters
+  // batched decode: gate|up + down in one launch with a per-K-split hand-off (FUNASR_GU_DOWN; 0 = two launches, A/B)
+  bool use_gu_down = false;  // measured: batch-32 step 1.216-1.218 vs 1.2085-1.209 ms (profiles/r05_exp_gu_down.txt)
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
   int* gk_cnt = nullptr;
   int64_t gk_part_n = 0, gk_cnt_n = 0;
@@ -832,6 +835,8 @@ struct Engine {
     gk_cnt_n = 1024;                             // tiles of a split-K launch
     gk_part_n = (int64_t)1024 * 2 * 1024;        // tiles x splits x (1 or 2 matrices) x 32 x 32 partial floats
     gk_cnt = alloc<int>(gk_cnt_n * CNT_LINE);
+    gd_cnt = alloc<unsigned>(64 * CNT_LINE);  // gate|up -> down hand-off counters (re-armed in-launch)
+    FA_HIP(hipMemset(gd_cnt, 0, 64 * CNT_LINE * sizeof(unsigned)));
     FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * CNT_LINE * sizeof(int)));
     gk_part = alloc<float>(gk_part_n);
     n_past.assign(lc.max_seqs, 0);
@@ -891,8 +896,14 @@ struct Engine {
   // GEMM) travel as bf16 hi / lo planes, written by their producers instead of f32 (FUNASR_ENC_PLANES=0: f32, A/B).
   // Same split as the GEMM staging applies to an f32 row: bit-identical products. The planes of a [rows][ld] tensor
   // live in the f32 buffer it replaces: hi at its start, lo rows * ld elements later (4 B per element either way).
-  bool enc_planes = true;
-  bool planes_on() const { return enc_planes && !enc_fp16 && enc_gemm; }
+  // Measured (profiles/r05_exp_enc_planes_ab.txt): one 60 s clip 11.3-11.5 -> 11.0-11.2 ms, but batch 32 103.7-104.3 ->
+  // 105.8-106.2 ms (the 256x256 tile reads A as two half-line streams instead of one), so planes are used while no
+  // GEMM of the call takes the 256x256 tile (below enc_planes_max_rows rows; FUNASR_ENC_PLANES=2: always)
+  int enc_planes = 1;
+  int enc_planes_max_rows = 6000;
+  bool planes_on(int rows) const {
+    return !enc_fp16 && enc_gemm && (enc_planes == 2 || (enc_planes == 1 && rows < enc_planes_max_rows));
+  }
   static APlanes planes_in(float* buf, int rows, int ld) {
     uint16_t* hi = reinterpret_cast<uint16_t*>(buf);
     return APlanes{hi, hi + (size_t)rows * ld};
@@ -902,7 +913,7 @@ struct Engine {
     const int d = ec.d_model;
     const float* xin = first ? hbuf : xa;  // block0 input = PE'd LFR features (hbuf holds them)
     float* x = xa;
-    const bool pl = planes_on() && WB(w.qkv_w).hi && WB(w.out_w).hi && WB(w.w1).hi && WB(w.w2).hi;
+    const bool pl = planes_on(rows) && WB(w.qkv_w).hi && WB(w.out_w).hi && WB(w.w1).hi && WB(w.w2).hi;
     const APlanes p_ln1 = pl ? planes_in(att, rows, w.d_in) : APlanes{}, p_att = pl ? planes_in(att, rows, d) : APlanes{};
     const APlanes p_ffn = pl ? planes_in(ffn, rows, ec.d_ffn) : APlanes{};
     // LN1
@@ -1290,7 +1301,6 @@ struct Engine {
         g.qout = lxq2; g.dout = lxd2;  // SwiGLU epilogue quantises act for the down GEMM (no prep launch)
       }
       set_pf(g, 2, w.down, nullptr, E, F);
-      gemv(g, E, 2);
       // x += Wdown . act
       GemvArgs dn{};
       dn.M = M; dn.eps = lc.rms_eps; dn.wq = w.down.q; dn.wd = w.down.d; dn.O = E; dn.rpw = gemv_rows_per_wave(E);
@@ -1303,7 +1313,10 @@ struct Engine {
         dn.qn_w = l + 1 < lc.n_layer ? layers[l + 1].attn_norm : out_norm;
       }
       if (l + 1 < lc.n_layer) set_pf(dn, 4, layers[l + 1].qkv, nullptr, QKV, E);
-      gemv(dn, F, 1);
+      if (!(nrm && decode && use_gu_down && gemv_gu_down(g, dn))) {
+        gemv(g, E, 2);
+        gemv(dn, F, 1);
+      }
     }
     prof_sample = true;
     prof_layer0 = prof_prefill = false;
@@ -1610,6 +1623,21 @@ struct Engine {
     return step_graphs[key] = ex;
   }
 
+  // gate|up + down in one launch (batched decode, FUNASR_GU_DOWN); false: shape not covered
+  bool gemv_gu_down(const GemvArgs& g0, const GemvArgs& d0) {
+    GemvArgs g = g0;
+    g.kpart = gk_part;
+    g.kpart_n = gk_part_n;
+    g.kcnt = gk_cnt;
+    g.kcnt_n = gk_cnt_n;
+    hipEvent_t ev;
+    prof_begin(0, &ev);
+    const bool ok = fa::gemm_q8_gu_down(g, d0, gd_cnt, fdw.err, stream);
+    const double F = lc.n_ff, E = lc.n_embd;
+    prof_end(0, ok ? 3.0 * F * E * 34.0 / 32.0 : 0.0, ok ? 2.0 * 3.0 * g.M * F * E : 0.0);
+    return ok;
+  }
+
   void gemv(const GemvArgs& a0, int K, int epi) {
     GemvArgs a = a0;
     a.kpart = gk_part;
@@ -1768,9 +1796,10 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_attn_wide = 256;
     if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
-    if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_GU_DOWN")) e->use_gu_down = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
       fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;
@@ -2344,6 +2373,15 @@ int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
   const int n_seqs = (int)e->gen_seqs.size(), n_steps = e->gen_steps;
   e->prof_collect();
   if (n_seqs <= fa::FUSED_MAX_M && e->fused_error()) e->recover_fused_chunk();
+  else if (n_seqs > fa::FUSED_MAX_M && e->use_gu_down && e->fused_error()) {
+    // a gate|up -> down hand-off timed out (not expected: the producers are dispatched first): two launches from now on
+    fa::log(3, "batched decode: the gate|up -> down hand-off timed out; re-running the chunk with two launches");
+    e->use_gu_down = false;
+    ++e->fused_recoveries;  // counted with the chunks re-run on another layer form (fa_llm_decode_recoveries)
+    e->drop_step_graphs();
+    e->rerun_chunk();
+    FA_REQUIRE(!e->fused_error(), "decode chunk re-run: error flag set with the two-launch FFN");
+  }
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {
     const int q = e->gen_seqs[i];

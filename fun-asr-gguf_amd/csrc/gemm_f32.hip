@@ -1206,7 +1206,8 @@ __global__ __launch_bounds__(B3B_T, 1) void k_gemm_bf3_256(AL al, const typename
   }
 }
 
-int g_gemm_bf3_persist = 0;  // 256x256 tiles: persistent blocks, one per CU (FUNASR_BF3_PERSIST; A/B)
+int g_gemm_bf3_persist = 0;  // 256x256 tiles: persistent blocks, one per CU (FUNASR_BF3_PERSIST; A/B: batch-32 encode
+                             // 105.1-105.9 vs 103.7-104.3 ms on f32 rows, no change on planes)
 static int cu_count() {
   static int n = 0;
   if (!n) {
@@ -1251,7 +1252,8 @@ static void launch_gemm_b3_256_s(const AL& al, const WSplit& w, int64_t ldw, int
 // and undone on the read (§5.4 rule 21). Rows past M / N load row M-1 / N-1 (their products land only in
 // accumulator rows / columns the epilogue never stores). Same wave tiling, per-element MFMA order (lo.hi, hi.lo,
 // hi.hi per 16 of k, k ascending) and epilogue as k_gemm_bf3_256: bit-identical outputs.
-int g_gemm_bf3_dma = 1;  // 1: planes-A 256x256 launches on k_gemm_bf3_256d (FUNASR_BF3_DMA; 0 = register staging)
+int g_gemm_bf3_dma = 0;  // 1: planes-A 256x256 launches on k_gemm_bf3_256d (FUNASR_BF3_DMA; A/B: batch-32 encode
+                         // with planes 109.4 vs 105.8-106.2 ms on register staging, profiles/r05_exp_enc_planes_ab.txt)
 constexpr int G_KB = 16, G_NB = 4;
 constexpr int G_PLANE = 256 * G_KB;  // bf16 per plane per buffer (8 KiB)
 constexpr int G_BUF = 4 * G_PLANE;   // one K-tile: [Ah][Al][Wh][Wl]

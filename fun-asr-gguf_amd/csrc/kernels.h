@@ -163,6 +163,10 @@ int gemv_rows_per_wave(int O);
 // argmax partials per token written by the lm_head launch for M tokens (GEMV for gemv_small(M), MFMA GEMM above)
 int lm_head_parts(int O, int M);
 int gemm_k_splits(int O, int M, int K, int epi);  // K splits of the split-K GEMM form for this shape
+// batched decode (M <= 32, producer-normalised inputs): gate|up + SwiGLU and the down projection in one launch with a
+// group-local hand-off per down K split; cnt = 64 zeroed counter lines (re-armed in-launch), err = timeout flag.
+// false: shape not covered (the caller runs the two launches)
+bool gemm_q8_gu_down(const GemvArgs& g, const GemvArgs& d, unsigned* cnt, int* err, hipStream_t s);
 extern int g_attn_lean;    // -1 auto, 0/1 force the 128-VGPR attention variant (A/B)
 extern int g_attn_blocks;  // attention key-split target (blocks per launch), 1024 by default
 extern int g_attn_wide;    // decode launches with >= this many (token, kv head) pairs: 16-wave blocks, no splits

@@ -603,6 +603,7 @@ __device__ __forceinline__ void load_scales(const __half* p, uint32_t (&d)[NBW /
 // SwiGLU epilogue's q8_0 rows: the tile's 32 rows of a token are one q8_0 block of the down projection's input,
 // quantised exactly as norm_quant_row does (no prep launch). s_act = tile [token][row]; threads 0..63: token
 // t & 31, rows [16 (t >> 5), +16)
+template <bool SC1 = false>
 __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const GemvArgs& a, int t0, int o0) {
   if (threadIdx.x >= 64) return;
   const int tk = threadIdx.x & 31, hh = threadIdx.x >> 5;
@@ -623,8 +624,18 @@ __device__ __forceinline__ void swiglu_tile_q8(const float (*s_act)[33], const G
     pk[j] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
   }
   if (t0 + tk < a.M) {
-    *reinterpret_cast<int4*>(a.qout + (int64_t)(t0 + tk) * a.ldo + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
-    if (hh == 0) a.dout[(int64_t)(t0 + tk) * (a.ldo / 32) + o0 / 32] = __half2float(__float2half_rn(d));
+    if constexpr (SC1) {  // consumed inside this launch (k_gemm_q8_gu_down): write-through stores, drained by the caller
+      const __amdgpu_buffer_rsrc_t rq = buf_rsrc(a.qout, a.M * (int)a.ldo);
+      const __amdgpu_buffer_rsrc_t rd = buf_rsrc(a.dout, a.M * (int)(a.ldo / 32) * 4);
+      st_sc1_f4(__builtin_bit_cast(f32x4_t, i32x4v_t{pk[0], pk[1], pk[2], pk[3]}), rq,
+                (int)((t0 + tk) * a.ldo + o0 + 16 * hh));
+      if (hh == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__half2float(__float2half_rn(d))), rd,
+                                              (int)(((t0 + tk) * (a.ldo / 32) + o0 / 32) * 4), 0, CPOL_SC1);
+    } else {
+      *reinterpret_cast<int4*>(a.qout + (int64_t)(t0 + tk) * a.ldo + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+      if (hh == 0) a.dout[(int64_t)(t0 + tk) * (a.ldo / 32) + o0 / 32] = __half2float(__float2half_rn(d));
+    }
   }
 }
 
@@ -649,11 +660,11 @@ int g_gemm_pf_delay = 50;
 // rows [32 x, +32) for x = g + 8 i in full (every K split of a tile shares its XCD). After pf_delay ticks (this launch's
 // own weights have landed) the prefetch blocks on XCD g pull those rows and their scales into g's L2 with LDS-DMA
 // loads into a scratch slot, drained before the block ends. Only lines move; no result changes.
-__device__ __forceinline__ void gemm_l2_prefetch(const GemvArgs& a, int KS) {
+// idx: this block's index among the launch's n_pf prefetch blocks (n_pf % 8 == 0; placement: linear block id % 8 ==
+// idx % 8, i.e. the launch's compute blocks before them come in multiples of 8)
+__device__ __forceinline__ void gemm_l2_prefetch(const GemvArgs& a, int idx, int n_pf) {
   __shared__ __attribute__((aligned(16))) int4 s_pf[4][64];
-  const int nxy = gridDim.x * gridDim.y;
-  const int idx = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (blockIdx.z - KS));  // host: nxy % 8 == 0
-  const int g = idx & 7, pb = idx >> 3, P = nxy * (gridDim.z - KS) / 8;
+  const int g = idx & 7, pb = idx >> 3, P = n_pf / 8;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)a.pf_delay) __builtin_amdgcn_s_sleep(4);
   auto* lds = (__attribute__((address_space(3))) void*)&s_pf[threadIdx.x >> 6][0];
@@ -673,18 +684,48 @@ __device__ __forceinline__ void gemm_l2_prefetch(const GemvArgs& a, int KS) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA write may land after the block's LDS is released
 }
 
-template <int EPI, int NBW, int KSM, bool NRM = false>
-__global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
-  if ((int)blockIdx.z >= KS) {  // L2 prefetch slabs (host: only with a.pf_q set)
-    gemm_l2_prefetch(a, KS);
-    return;
+// Every in-launch wait is bounded by time, not spin count: SPIN_TICKS of the 100 MHz reference clock (10 ms) from
+// the first poll (checked every 16 polls). A group that is not co-resident (another kernel holding CUs) then costs a
+// few ms per wait instead of seconds; the timed-out block sets *err and falls through, and fa_llm_generate_end re-runs
+// the chunk on the 5-launch layer (engine.cpp, recover_fused_chunk).
+constexpr uint64_t SPIN_TICKS = 1000000;
+struct SpinDeadline {
+  uint64_t t0 = 0;
+  unsigned n = 0;
+  __device__ __forceinline__ bool expired() {
+    if ((++n & 15) != 1) return false;
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (n == 1) {
+      t0 = t;
+      return false;
+    }
+    return t - t0 > SPIN_TICKS;
   }
+};
+
+// In-launch fusion of two split-K GEMMs of the batched-decode chain (k_gemm_q8_gu_down): ROLE 1 = a SwiGLU producer
+// whose combining block publishes its act tile (sc1 stores, drained) and counts it on arr[tile / tiles_per_split]; ROLE 2
+// = a consumer (down projection, K split s = its act columns [32 tiles_per_split s, +32 tiles_per_split)) that issues
+// its weight rows and scales first, waits for its split's tiles, then reads the act rows with sc1 loads. The consumer
+// blocks of a split count themselves past the wait on dep[s]; the last one re-arms both counters for the next launch
+// (every producer of this launch has counted by then, and the next launch starts after this one ends).
+struct SkFuse {
+  unsigned* arr = nullptr;
+  unsigned* dep = nullptr;
+  int tiles_per_split = 0;
+  int consumers = 0;
+  int* err = nullptr;
+};
+
+template <int EPI, int NBW, int KSM, bool NRM, int ROLE>
+__device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx, int by, int bz, int gdx,
+                                        int8_t* s_ab_mem, const SkFuse& fz) {
   constexpr int WPM = EPI == 2 ? 2 : 4;  // waves per weight matrix
   constexpr int NS = EPI == 2 ? 2 : 1;
   static_assert(!NRM || EPI != 1, "k_gemm_q8_sk: NRM inputs feed q|k|v, gate|up and the LM head");
   const int nb = K >> 5;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int o0 = blockIdx.x * 32, t0 = blockIdx.y * 32, ks = blockIdx.z;
+  const int o0 = bx * 32, t0 = by * 32, ks = bz;
   const bool upw = EPI == 2 && wave >= 2;
   const int bw0 = (ks * WPM + (EPI == 2 ? (wave & 1) : wave)) * NBW;  // host: nb == KS * WPM * NBW
   const int8_t* wq = upw ? a.wq2 : a.wq;
@@ -701,22 +742,58 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   // the fragments are rebuilt through LDS below (16 B per lane from 32 rows per instruction ran the LM head at a third
   // of the coalesced rate)
   constexpr int RB = NBW * 32, LPR = RB / 16, RPI = 64 / LPR, SLD = RB + 16;
-  __shared__ __attribute__((aligned(16))) int8_t s_ab[4][2][32 * SLD];
+  int8_t(&s_ab)[4][2][32 * SLD] = *reinterpret_cast<int8_t(*)[4][2][32 * SLD]>(s_ab_mem);
+  uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
+  float2 dx2[NBW / 2];
   {
     const int rr = lane / LPR, off = bw0 * 32 + 16 * (lane % LPR);
+    if constexpr (ROLE == 2) {
+      // consumer: weight rows and scales first (they do not depend on the producers), then the wait, then the act
+      // rows of this split with sc1 loads (written by other workgroups of this launch, any XCD)
 #pragma unroll
-    for (int i = 0; i < NBW; ++i) {
-      A[i] = *reinterpret_cast<const i32x4_t*>(wq + (int64_t)min(o0 + RPI * i + rr, a.O - 1) * K + off);
-      B[i] = *reinterpret_cast<const i32x4_t*>(a.xq + (int64_t)min(t0 + RPI * i + rr, a.M - 1) * K + off);
+      for (int i = 0; i < NBW; ++i)
+        A[i] = *reinterpret_cast<const i32x4_t*>(wq + (int64_t)min(o0 + RPI * i + rr, a.O - 1) * K + off);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg)
+        load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
+      if (threadIdx.x == 0) {
+        SpinDeadline dl;
+        while ((int)__hip_atomic_load(fz.arr + ks * CNT_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               fz.tiles_per_split) {
+          __builtin_amdgcn_s_sleep(1);
+          if (dl.expired()) {
+            __hip_atomic_store(fz.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        if (__hip_atomic_fetch_add(fz.dep + ks * CNT_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (unsigned)fz.consumers - 1) {
+          __hip_atomic_store(fz.arr + ks * CNT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(fz.dep + ks * CNT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rx = buf_rsrc(a.xq, a.M * K);
+      const __amdgpu_buffer_rsrc_t rd = buf_rsrc(a.xd, a.M * nb * 4);
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+        B[i] = __builtin_bit_cast(i32x4_t, ld_sc1_f4(rx, (min(t0 + RPI * i + rr, a.M - 1) * K + off)));
+#pragma unroll
+      for (int q = 0; q < NBW / 2; ++q)
+        dx2[q] = make_float2(ld_sc1_f1(rd, (t_b * nb + bw0 + 2 * q) * 4), ld_sc1_f1(rd, (t_b * nb + bw0 + 2 * q + 1) * 4));
+    } else {
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        A[i] = *reinterpret_cast<const i32x4_t*>(wq + (int64_t)min(o0 + RPI * i + rr, a.O - 1) * K + off);
+        B[i] = *reinterpret_cast<const i32x4_t*>(a.xq + (int64_t)min(t0 + RPI * i + rr, a.M - 1) * K + off);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg)
+        load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
+#pragma unroll
+      for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + bw0 + 2 * q);
     }
   }
-  uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg)
-    load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
-  float2 dx2[NBW / 2];
-#pragma unroll
-  for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + bw0 + 2 * q);
   if constexpr (NRM) {
     float ss = 0.f;  // the producer's 32 tile partials in tile order
 #pragma unroll
@@ -796,7 +873,7 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
   }
   if (KSM > 1 && KS > 1) {
     typedef float f4v __attribute__((ext_vector_type(4)));
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile = by * gdx + bx;
     float* base = a.kpart + (int64_t)tile * KS * (NS * 1024);
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, KS * NS * 1024 * 4);
     st_sc1_f4(f4v{y[0], y[1], y[2], y[3]}, rs, (ks * NS * 1024 + threadIdx.x * 4) * 4);
@@ -872,8 +949,8 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
     if (tok < a.M) {
       *reinterpret_cast<int32_t*>(a.qout + (int64_t)tok * 1024 + o0 + rb) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
       if (threadIdx.x < 32) {
-        a.dout[(int64_t)tok * 32 + blockIdx.x] = d;
-        a.ssp_out[(int64_t)tok * 32 + blockIdx.x] = ((s_ssq[0][col] + s_ssq[1][col]) + s_ssq[2][col]) + s_ssq[3][col];
+        a.dout[(int64_t)tok * 32 + bx] = d;
+        a.ssp_out[(int64_t)tok * 32 + bx] = ((s_ssq[0][col] + s_ssq[1][col]) + s_ssq[2][col]) + s_ssq[3][col];
       }
     }
   }
@@ -883,17 +960,35 @@ __global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
       for (int rr = 0; rr < 32; ++rr) argmax_combine(bv, bi, s_act[threadIdx.x][rr], o0 + rr);
-      a.pval[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bv;
-      a.pidx[(int64_t)(t0 + threadIdx.x) * a.n_part + blockIdx.x] = bi;
+      a.pval[(int64_t)(t0 + threadIdx.x) * a.n_part + bx] = bv;
+      a.pidx[(int64_t)(t0 + threadIdx.x) * a.n_part + bx] = bi;
     }
   }
   if (EPI == 2 && a.qout) {
     __syncthreads();
-    swiglu_tile_q8(s_act, a, t0, o0);
+    swiglu_tile_q8<ROLE == 1>(s_act, a, t0, o0);
+    if (ROLE == 1 && threadIdx.x < 64) {  // publish: the tile's sc1 stores drained, then counted for its down split
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(fz.arr + (bx / fz.tiles_per_split) * CNT_LINE, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   KSTAMP(5);
 }
 #undef SRED
+
+template <int EPI, int NBW, int KSM, bool NRM = false>
+__global__ __launch_bounds__(256) void k_gemm_q8_sk(GemvArgs a, int K, int KS) {
+  if ((int)blockIdx.z >= KS) {  // L2 prefetch slabs (host: only with a.pf_q set)
+    const int nxy = gridDim.x * gridDim.y;  // host: nxy % 8 == 0
+    gemm_l2_prefetch(a, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * (blockIdx.z - KS)), nxy * (gridDim.z - KS));
+    return;
+  }
+  constexpr int SLD = NBW * 32 + 16;
+  __shared__ __attribute__((aligned(16))) int8_t s_ab[4 * 2 * 32 * SLD];
+  sk_tile<EPI, NBW, KSM, NRM, 0>(a, K, KS, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, s_ab, SkFuse{});
+}
 
 // Batched LM head (5-32 tokens, K = 1024, the 151936 vocabulary rows): the split-K block kernel's tile arithmetic
 // (4 waves x 8 q8_0 blocks of K, fixed-order wave sum, argmax partial per 32-row tile) in a persistent loop over
@@ -1537,6 +1632,67 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     SK(3, 8, 1)
 #undef SK
     default: FA_REQUIRE(false, "gemm_q8: split-K shape not instantiated");
+  }
+}
+
+// ---- gate|up + down of a batched-decode layer in ONE launch (FUNASR_GU_DOWN): the SwiGLU split-K blocks first (lower
+// block ids, so all of them are dispatched before any consumer can hold a CU), then the down projection's split-K
+// blocks, each waiting only for the 96 / KSd act tiles of its own K split (a group-local hand-off, SkFuse), then the
+// down GEMM's L2 prefetch slabs (the next layer's q|k|v rows). The down blocks' weight rows are in flight while the
+// SwiGLU blocks run, and one kernel boundary per layer disappears. Same per-tile arithmetic and split order as the
+// two launches: bit-identical outputs.
+template <int NBWG, int KSMG, int NBWD, int KSMD>
+__global__ __launch_bounds__(256) void k_gemm_q8_gu_down(GemvArgs g, GemvArgs d, int KSg, int KSd, SkFuse fz, int n_pf) {
+  constexpr int SLDG = NBWG * 32 + 16, SLDD = NBWD * 32 + 16;
+  __shared__ __attribute__((aligned(16))) int8_t s_ab[4 * 2 * 32 * (SLDG > SLDD ? SLDG : SLDD)];
+  const int b = blockIdx.x, tg = g.O >> 5, td = d.O >> 5;  // one 32-token tile (M <= 32)
+  const int ng = tg * KSg, nd = td * KSd;
+  if (b < ng) {
+    sk_tile<2, NBWG, KSMG, true, 1>(g, 1024, KSg, b % tg, 0, b / tg, tg, s_ab, fz);
+  } else if (b < ng + nd) {
+    const int c = b - ng;
+    sk_tile<1, NBWD, KSMD, false, 2>(d, 3072, KSd, c % td, 0, c / td, td, s_ab, fz);
+  } else {
+    gemm_l2_prefetch(d, b - ng - nd, n_pf);
+  }
+}
+
+bool gemm_q8_gu_down(const GemvArgs& g0, const GemvArgs& d0, unsigned* cnt, int* err, hipStream_t s) {
+  // shapes: Qwen3-0.6B at M <= 32 (E 1024, F 3072), producer-normalised gate|up input, down with K = F
+  if (g0.M > 32 || g0.M != d0.M || g0.O != 3072 || d0.O != 1024 || !g0.ssp || !g0.qout || d0.ssp || !g0.kpart ||
+      !g0.kcnt)
+    return false;
+  int nbwg, ksg, nbwd, ksd;
+  gemm_sk_shape(g0.O, g0.M, 1024, 2, &nbwg, &ksg);
+  gemm_sk_shape(d0.O, d0.M, 3072, 1, &nbwd, &ksd);
+  const int tg = g0.O / 32, td = d0.O / 32;
+  if (nbwg <= 0 || nbwd <= 0 || tg % ksd || tg % 8 || td % 8) return false;
+  const int64_t gpart = (int64_t)tg * ksg * 2 * 1024, dpart = (int64_t)td * ksd * 1024;
+  if (tg + td > g0.kcnt_n || gpart + dpart > g0.kpart_n) return false;
+  GemvArgs g = g0, d = d0;
+  g.pf_q = nullptr;  // the down blocks load their own rows
+  d.kpart = g0.kpart + gpart;
+  d.kpart_n = dpart;
+  d.kcnt = g0.kcnt + tg * CNT_LINE;
+  d.kcnt_n = td;
+  SkFuse fz;
+  fz.arr = cnt;
+  fz.dep = cnt + 32 * CNT_LINE;
+  fz.tiles_per_split = tg / ksd;
+  fz.consumers = td;
+  fz.err = err;
+  const int n_pf = d.pf_q && d.pf_slabs > 0 && d.pf_O % 256 == 0 && d.pf_K % 128 == 0 ? d.pf_slabs * td : 0;
+  if (!n_pf) d.pf_q = nullptr;
+  const dim3 grid(tg * ksg + td * ksd + n_pf);
+  const int kmg = ksg == 1 ? 1 : ksg <= 4 ? 4 : 16, kmd = ksd == 1 ? 1 : ksd <= 4 ? 4 : 16;
+  switch (nbwg * 100000 + kmg * 1000 + nbwd * 100 + kmd) {
+#define GD(A, B, C, D)                                                                                     \
+  case A * 100000 + B * 1000 + C * 100 + D:                                                                \
+    hipLaunchKernelGGL((k_gemm_q8_gu_down<A, B, C, D>), grid, dim3(256), 0, s, g, d, ksg, ksd, fz, n_pf); \
+    return true;
+    GD(8, 4, 4, 16) GD(4, 4, 4, 16) GD(8, 4, 2, 16) GD(4, 4, 2, 16) GD(8, 4, 8, 4) GD(4, 4, 8, 4)
+#undef GD
+    default: return false;
   }
 }
 
@@ -2799,24 +2955,6 @@ void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s) {
 // 1.5-1.9 us plus the weight stream's first-byte latency (profiles/); the fan-ins here are 16 / 32 blocks
 // deep and the slices' weights are already in registers when their inputs arrive. Every block of a launch is
 // resident (128 / 256 blocks, at most 2 per CU); every spin is bounded: a timeout sets *err and falls through.
-// Every in-launch wait is bounded by time, not spin count: SPIN_TICKS of the 100 MHz reference clock (10 ms) from
-// the first poll (checked every 16 polls). A group that is not co-resident (another kernel holding CUs) then costs a
-// few ms per wait instead of seconds; the timed-out block sets *err and falls through, and fa_llm_generate_end re-runs
-// the chunk on the 5-launch layer (engine.cpp, recover_fused_chunk).
-constexpr uint64_t SPIN_TICKS = 1000000;
-struct SpinDeadline {
-  uint64_t t0 = 0;
-  unsigned n = 0;
-  __device__ __forceinline__ bool expired() {
-    if ((++n & 15) != 1) return false;
-    const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    if (n == 1) {
-      t0 = t;
-      return false;
-    }
-    return t - t0 > SPIN_TICKS;
-  }
-};
 
 __device__ __forceinline__ void fanin_wait(unsigned* cnt, unsigned n, int* err) {
   __shared__ unsigned s_target;

@@ -680,15 +680,17 @@ def test_write_after_barrier_gemm_staging_bit_identical(monkeypatch):
 
 def test_encoder_activation_planes_bit_identical(monkeypatch):
     """bf16x3 encoder: the SANM blocks' GEMM inputs written as bf16 hi / lo planes by their producers (layernorm, the
-    attention epilogue, the ffn1 epilogue; FUNASR_ENC_PLANES=1, the default) instead of f32 rows split by the GEMM's
-    staging. The split is the same, so every product is: a batch of eight 60 s clips (the 256x256 tile) and one 60 s
-    clip (the few-tile shapes) encode bit-identically with FUNASR_ENC_PLANES=0, with the 256x256 tile's planes staged
-    by LDS-DMA (k_gemm_bf3_256d, FUNASR_BF3_DMA=1, the default) and by registers (=0)."""
+    attention epilogue, the ffn1 epilogue) instead of f32 rows split by the GEMM's staging. The split is the same, so
+    every product is: a batch of eight 60 s clips (the 256x256 tile) and one 60 s clip (the few-tile shapes) encode
+    bit-identically with f32 rows (FUNASR_ENC_PLANES=0), with planes at every size (=2) staged by registers or by
+    LDS-DMA (k_gemm_bf3_256d, FUNASR_BF3_DMA=1), as persistent blocks (FUNASR_BF3_PERSIST=1), and with the default (=1:
+    planes below the 256x256 tile's sizes)."""
     from fun_asr_gguf import _native
     from fun_asr_gguf.synthetic import synth_audio
     clips = [synth_audio(SR * 60, 400 + i) for i in range(8)]
     outs = []
-    modes = (("0", "1", "0"), ("1", "1", "0"), ("1", "0", "0"), ("0", "1", "1"), ("1", "1", "1"), ("1", "0", "1"))
+    modes = (("0", "1", "0"), ("2", "1", "0"), ("2", "0", "0"), ("0", "1", "1"), ("2", "1", "1"), ("2", "0", "1"),
+             ("1", "0", "0"))  # 2: planes at every size; 1 (default): below enc_planes_max_rows
     for planes, dma, persist in modes:  # ..., and as persistent blocks (FUNASR_BF3_PERSIST=1)
         monkeypatch.setenv("FUNASR_ENC_PLANES", planes)
         monkeypatch.setenv("FUNASR_BF3_DMA", dma)

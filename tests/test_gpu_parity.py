@@ -668,6 +668,34 @@ def test_batched_decode_gemm_l2_prefetch_bit_identical(monkeypatch):
     assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
 
 
+@pytest.mark.parametrize("n_seq", [12, 32])
+def test_batched_decode_ffn_one_launch_bit_identical(monkeypatch, n_seq):
+    """gate|up + SwiGLU and the down projection of a batched-decode layer in one launch (FUNASR_GU_DOWN=1, an A/B
+    form: the down blocks wait per K split for their act tiles) keep the two launches' per-tile arithmetic and split
+    order: the same tokens and logits over 24 graph-replayed steps and one eager step."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(9)
+    prompts = [(rng.standard_normal((30 + 5 * q, 1024)) * 0.5).astype(np.float32) for q in range(n_seq)]
+    runs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("FUNASR_GU_DOWN", fuse)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=n_seq), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            for q in range(n_seq):
+                eng.llm_reset(q)
+                eng.llm_prefill(q, prompts[q])
+            toks = eng.llm_generate(list(range(n_seq)), 24)
+            toks1 = eng.llm_generate(list(range(n_seq)), 1)
+            runs.append((toks, toks1, [eng.llm_logits(q) for q in range(n_seq)], eng.llm_decode_recoveries()))
+        finally:
+            eng.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
+    assert runs[1][3] == (0, 0)  # no hand-off timed out
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
