@@ -167,6 +167,7 @@ struct Engine {
   // Measured (graph-replayed, full model): 1 / 8 / 32 steps per graph -> batch 1 0.489 / 0.499 / 0.525 ms per step,
   // batch 32 1.223 / 1.239 / 1.358 ms: one step per graph replay stays the default
   int graph_steps = 1;
+  int graph_sync_every = 0;  // FUNASR_GRAPH_SYNC_EVERY (profiling aid, see enqueue_steps)
   // profiler experiment hook (FUNASR_STEP_MASK, default all): which launches a batch-1 fused decode step enqueues --
   // bit 0 the attention launches (AB), 1 the FFN launches (C), 2 the LM head, 3 the sampler. Steps with bits cleared
   // compute garbage; only for bisecting which graph node rocprofv3's kernel trace rejects (scripts/gpu_r5_graphprof.sh)
@@ -1463,7 +1464,12 @@ struct Engine {
       }
       if (st < n_steps) {
         const hipGraphExec_t ex = step_graph(n_seqs);
-        for (; st < n_steps; ++st) FA_HIP(hipGraphLaunch(ex, stream));
+        for (; st < n_steps; ++st) {
+          FA_HIP(hipGraphLaunch(ex, stream));
+          // profiling aid (FUNASR_GRAPH_SYNC_EVERY): bound the captured-graph packets in flight (under rocprofv3 with
+          // HIP's graph packet capture on, more than a queue ring of them crashes the process: DESIGN.md section 4)
+          if (graph_sync_every > 0 && (st + 1) % graph_sync_every == 0) FA_HIP(hipStreamSynchronize(stream));
+        }
       }
     } else {
       for (int st = 0; st < n_steps; ++st) {
@@ -1747,6 +1753,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_lm_head_mt6 = g ? atoi(g) != 0 : 1;
     }
     if (const char* g = getenv("FUNASR_STEP_MASK")) e->step_mask = atoi(g) & 15;
+    if (const char* g = getenv("FUNASR_GRAPH_SYNC_EVERY")) e->graph_sync_every = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
