@@ -400,8 +400,10 @@ __device__ __forceinline__ f16x4a ld_tr4h(const _Float16* p) {
 // (oracle/encoder_fp16.py); 3 MFMAs per 16 keys x 16 dims instead of the exact-f32 form's 8 x 64 cycles
 // S = 1: write-after-barrier staging (as k_gemm_bf3_256 S = 1): the registers holding key tile kt + 1, loaded a whole
 // step earlier, go to the free stage at the top of step kt and then take tile kt + 2's loads. Same MFMA order.
+// Two blocks per CU (launch bounds; LDS 76.8 KB per block at D = 128): unbounded, hipcc parked 64 values in AGPRs
+// beside 254 VGPRs and the kernel ran one wave per SIMD; bounded it fits 256 registers without scratch.
 template <int D, int P = 3, int S = 0>
-__global__ __launch_bounds__(256) void k_attn_bf3(const float* __restrict__ Q, const float* __restrict__ Kp,
+__global__ __launch_bounds__(256, 2) void k_attn_bf3(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
                                                   const int* __restrict__ lens, float scale, int KS,

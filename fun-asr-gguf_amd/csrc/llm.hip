@@ -1349,8 +1349,10 @@ __device__ __forceinline__ void qt_store(uint8_t* st, int t, const i32x4_t (&rw)
 
 // S = 1: write-after-barrier staging (the encoder GEMM tiles' schedule): the registers holding K-step kt + 1, loaded a
 // whole step earlier, go to the free stage at the top of step kt and then take step kt + 2's loads
+// Two blocks per CU (launch bounds): the SwiGLU form held 255 VGPRs + 16 AGPRs and ran one wave per SIMD, with its
+// per-block f32 scaling issue-bound (profiles/r05_pmc_sq_stalls.txt); bounded, it fits 256 registers without scratch.
 template <int EPI, int S = 0>
-__global__ __launch_bounds__(256) void k_gemm_q8_t(GemvArgs a, int K) {
+__global__ __launch_bounds__(256, 2) void k_gemm_q8_t(GemvArgs a, int K) {
   using T = QTile<EPI>;
   constexpr int NM = T::NM;
   extern __shared__ __attribute__((aligned(16))) uint8_t qsm[];
@@ -2300,7 +2302,7 @@ __global__ __launch_bounds__(NW * 64, NW > AWV ? 1 : LEAN ? 4 : 1) void k_attn_b
 // rows (f32) and their q8_0 blocks for the o GEMM. Tiles: int4 {row0, n_rows, seq, 0} from the host.
 constexpr int PAQ = 128, PAK = 32, PAD = 128, PAS = PAD + 8;  // query slots, keys per tile, head dim, LDS row stride
 
-__global__ __launch_bounds__(256) void k_attn_prefill(const int4* __restrict__ tiles, const int* __restrict__ tok_pos,
+__global__ __launch_bounds__(256, 2) void k_attn_prefill(const int4* __restrict__ tiles, const int* __restrict__ tok_pos,
                                                       int H, int KV, int64_t seq_stride, int64_t head_stride,
                                                       const __half* __restrict__ kc, const __half* __restrict__ vc,
                                                       const float* __restrict__ q, float scale, float* __restrict__ out,

@@ -28,4 +28,12 @@ for _ in range(reps):
 eng.synchronize()
 dt = (time.perf_counter() - t) / reps
 print(f"encode batch {B} x 60 s ({'fp16' if fp16 else 'fp32 ' + gemm}): {dt * 1e3:.2f} ms per call, {dt * 1e3 / B:.2f} ms per clip")
+if os.environ.get("ENC_HASH"):  # bit-identity check across builds / settings: hash of every clip's encoder rows
+    import hashlib
+    import numpy as np
+    out = eng.encode(clips, resident=h, want_enc=True)
+    hs = hashlib.sha256()
+    for e in out["enc"]:
+        hs.update(np.ascontiguousarray(e).tobytes())
+    print(f"encoder rows hash: {hs.hexdigest()[:16]}")
 eng.close()
