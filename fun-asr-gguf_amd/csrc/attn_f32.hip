@@ -191,8 +191,9 @@ __device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m
   if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// two blocks per CU (LDS 70.7 KB per block at D = 128; 234 VGPRs, no AGPRs or scratch), as k_attn_bf3 below
 template <int D>
-__global__ __launch_bounds__(256) void k_attn_f32(const float* __restrict__ Q, const float* __restrict__ Kp,
+__global__ __launch_bounds__(256, 2) void k_attn_f32(const float* __restrict__ Q, const float* __restrict__ Kp,
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
                                                   const int* __restrict__ lens, float scale, int KS, int r16,
