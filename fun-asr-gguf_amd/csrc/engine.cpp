@@ -914,7 +914,9 @@ struct Engine {
     const int d = ec.d_model;
     const float* xin = first ? hbuf : xa;  // block0 input = PE'd LFR features (hbuf holds them)
     float* x = xa;
-    const bool pl = planes_on(rows) && WB(w.qkv_w).hi && WB(w.out_w).hi && WB(w.w1).hi && WB(w.w2).hi;
+    // planes fit the f32 buffers they replace (att holds rows x max(d, d_llm) floats, ffn rows x >= d_ffn floats)
+    const bool pl = planes_on(rows) && std::max(w.d_in, d) <= std::max(d, ec.d_llm) && WB(w.qkv_w).hi &&
+                    WB(w.out_w).hi && WB(w.w1).hi && WB(w.w2).hi;
     const APlanes p_ln1 = pl ? planes_in(att, rows, w.d_in) : APlanes{}, p_att = pl ? planes_in(att, rows, d) : APlanes{};
     const APlanes p_ffn = pl ? planes_in(ffn, rows, ec.d_ffn) : APlanes{};
     // LN1
