@@ -1804,6 +1804,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     // scripts/ubench/attn_batch at batch 32, 42.7 MB of K/V: 14.65 vs 15.7-15.9 us for the split blocks
     fa::g_attn_wide = 256;
     if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
+    if (const char* g = getenv("FUNASR_ATTN_LDSPF")) fa::g_attn_ldspf = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));

@@ -1781,6 +1781,7 @@ constexpr int AWV = 4;    // waves per block
 int g_attn_blocks = 1024;  // key splits are added while (token, kv head, split) blocks stay within this many
 int g_attn_lean = -1;      // -1: lean blocks when a launch needs more than 3 per CU; 0 / 1 force (A/B)
 int g_attn_wide = 0;       // decode launches with at least this many (token, kv head) pairs: one 16-wave block each
+int g_attn_ldspf = 0;      // ... (off: measured slower, batch-32 step 1.207 -> 1.248 ms, same one block per CU) whose waves pull each next pass's K/V into LDS during the current pass (FUNASR_ATTN_LDSPF)
 constexpr int AGI = 16;   // 4-key groups per wave per pass (registers: 16 int4 of K + 16 of V)
 constexpr int ASPLIT = ATTN_SPLITS;  // key splits (blocks) per (token, kv head)
 #ifndef FA_AMIN_G
@@ -1838,13 +1839,28 @@ struct AttnQIn {
 // PRE: the first pass's K/V (groups g0 + AW i, i < NI) were loaded by the caller (the first NI of AKV_PRE groups:
 // the same clamped addresses load_kv_groups<NI> would use)
 constexpr int AKV_PRE = 4;
-template <int NI, int AW, bool PIPE, bool PRE = false>
+// LPF (the 16-wave batched-decode blocks, lean passes): the NEXT pass's K/V rows are pulled into this wave's LDS slot
+// (slot[0 K / 1 V][i][lane], 16 B per lane, lane-linear as LDS-DMA writes them) while the current pass computes, so a
+// context longer than one pass costs one memory round trip instead of one per pass; each lane reads back only the
+// bytes its own DMA lane wrote (s_waitcnt vmcnt(0) orders them). Same values, same arithmetic.
+template <int NI, int AW, bool PIPE, bool PRE = false, bool LPF = false>
 __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const __half* __restrict__ vb, int KV, int g0,
                                           int ge, int n_keys, int kq, int dq, int lane, bool decode, bool fresh_here,
                                           int pos, float eps, float scale, const AttnQIn& qi, __half* __restrict__ kd,
                                           __half* __restrict__ vd, float (*s_qw)[128], float* s_kn, float* s_vn,
                                           float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
-                                          const int4* pk = nullptr, const int4* pv = nullptr) {
+                                          const int4* pk = nullptr, const int4* pv = nullptr, int4* slot = nullptr) {
+  constexpr int SD = 128;
+  auto lpf_issue = [&](int g1) {  // next pass's groups -> slot (clamped rows as load_kv_groups clamps them)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int k = min(4 * (g1 + AW * i) + kq, n_keys - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(kb + (int64_t)k * SD + dq * 8),
+                                       (__attribute__((address_space(3))) void*)(slot + i * 64), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(vb + (int64_t)k * SD + dq * 8),
+                                       (__attribute__((address_space(3))) void*)(slot + (4 + i) * 64), 16, 0, 0);
+    }
+  };
   int4 kt[NI], vt[NI];
   if constexpr (PRE) {
     static_assert(NI <= AKV_PRE, "attn_wave: preloaded groups");
@@ -1856,6 +1872,9 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
   } else {
     load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
     load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+  }
+  if constexpr (LPF) {
+    if (g0 + AW * NI < ge) lpf_issue(g0 + AW * NI);
   }
   __builtin_amdgcn_sched_barrier(0);  // the q math below must not be hoisted above the K/V stream's issue
   STAMP(2);
@@ -1977,6 +1996,15 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
         kt[i] = kn_[PIPE ? i : 0];
         vt[i] = vn_[PIPE ? i : 0];
       }
+    } else if constexpr (LPF) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into its slot has landed
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        kt[i] = slot[i * 64 + lane];
+        vt[i] = slot[(4 + i) * 64 + lane];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the slot is refilled
+      if (g0 + AW * NI < ge) lpf_issue(g0 + AW * NI);
     } else {
       load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
       load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
@@ -2014,7 +2042,7 @@ __device__ __forceinline__ void store_q8_row4(int8_t* __restrict__ qout, float* 
 // split's softmax state in (M, L, o) for lane -> head j = lane >> 5, dims [d0, d0 + 4) (d0 = 4 (lane & 31)).
 // Shared by k_attn_block (partials + last-arriver combine) and k_attn_o (fused decode: every split combines, then
 // multiplies its slice of the o projection).
-template <int DM, int LEAN, bool PRE = false, int NW = AWV>
+template <int DM, int LEAN, bool PRE = false, int NW = AWV, bool LPF = false>
 __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, int seq, int nsplit, int H, int KV,
                                                  int64_t seq_stride, int64_t head_stride, __half* __restrict__ kc,
                                                  __half* __restrict__ vc, const float* __restrict__ qsrc,
@@ -2041,7 +2069,12 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   __shared__ float s_q[NW][GQ][D];          // per-wave q (scaled, roped) in natural dim order
   __shared__ float s_kn[D], s_vn[D];        // fresh K/V row (decode)
   __shared__ float s_ml[NW][GQ][2];
-  __shared__ float s_o[NW][GQ][D];          // [wave][head][dim], summed over the wave's 4 key rows
+  static_assert(!LPF || (LEAN && !PRE), "attn_split_merge: LDS prefetch with lean passes only");
+  // LPF: per-wave K/V slots [2][4 groups][64 lanes] of 16 B; the per-wave o partials alias them after the passes
+  __shared__ __attribute__((aligned(16))) int4 s_slot[LPF ? NW : 1][2 * 4 * 64];
+  __shared__ float s_o_own[LPF ? 1 : NW][GQ][D];  // [wave][head][dim], summed over the wave's 4 key rows
+  float(*s_o)[GQ][D] = LPF ? reinterpret_cast<float(*)[GQ][D]>(&s_slot[0][0]) : s_o_own;
+  static_assert(!LPF || sizeof(s_slot) >= sizeof(float) * NW * GQ * D, "attn_split_merge: o partials fit the slots");
   const int kq = lane >> 4, dq = lane & 15;
   float mx[GQ], l[GQ], acc[GQ][8];
 #pragma unroll
@@ -2091,15 +2124,16 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
     __half* kd = kb + (int64_t)pos * D;
     __half* vd = vb + (int64_t)pos * D;
     const int ni = (ge - g0 + NW - 1) / NW;
+    int4* slot = LPF ? &s_slot[wave][0] : nullptr;
     if (ni <= 1)
-      attn_wave<1, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
-                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
+      attn_wave<1, NW, !LEAN, PRE, LPF>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale,
+                                        qi, kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv, slot);
     else if (ni <= 2)
-      attn_wave<2, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
-                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
+      attn_wave<2, NW, !LEAN, PRE, LPF>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale,
+                                        qi, kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv, slot);
     else if (ni <= 4 || LEAN)
-      attn_wave<4, NW, !LEAN, PRE>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi,
-                                 kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv);
+      attn_wave<4, NW, !LEAN, PRE, LPF>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale,
+                                        qi, kd, vd, s_q[wave], s_kn, s_vn, mx, l, acc, pk, pv, slot);
     else
       attn_wave<8, NW, !LEAN>(kb, vb, KV, g0, ge, n_keys, kq, dq, lane, DM != 0, fresh_here, pos, eps, scale, qi, kd, vd,
                        s_q[wave], s_kn, s_vn, mx, l, acc);
@@ -2107,6 +2141,10 @@ __device__ __forceinline__ bool attn_split_merge(int g, int sp, int m, int pos, 
   // publish per-wave (m, l) and o summed over the wave's 4 key rows (m is wave-uniform, so the rows add
   // unscaled): permlane32_swap pairs fold rows {r, r^2}, permlane16_swap pairs fold {r, r^1}; afterwards
   // red[k] of a lane in row r holds element t = 4k + 2(r&1) + (r>>1) of acc (t = 8 head + dim-in-lane).
+  if constexpr (LPF) {  // the o partials overwrite the slots: no DMA of any wave may still land there
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   float red[4];
   {
     float h8[8];
@@ -2226,7 +2264,7 @@ __device__ __forceinline__ float4 combine_splits(const __amdgpu_buffer_rsrc_t& r
 
 // NW = 16 (batched decode, one block per (token, kv head), n_active == 1 only): the 16 waves of one CU share the key
 // range, merged in LDS; no split partials, no combine hop
-template <int DM, int LEAN, int NW = AWV>
+template <int DM, int LEAN, int NW = AWV, bool LPF = false>
 __global__ __launch_bounds__(NW * 64, NW > AWV ? 1 : LEAN ? 4 : 1) void k_attn_block(const int* __restrict__ tok_seq, const int* __restrict__ tok_pos,
                                                          int nsplit, int decode_mode, int H, int KV,
                                                          int64_t seq_stride, int64_t head_stride,
@@ -2250,8 +2288,8 @@ __global__ __launch_bounds__(NW * 64, NW > AWV ? 1 : LEAN ? 4 : 1) void k_attn_b
   int n_active, j, d0;
   float M, L;
   float4 o;
-  if (!attn_split_merge<DM, LEAN, false, NW>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc, qsrc,
-                                              qn, kn, rcos, rsin, eps, scale, n_active, j, d0, M, L, o))
+  if (!attn_split_merge<DM, LEAN, false, NW, LPF>(g, sp, m, pos, seq, nsplit, H, KV, seq_stride, head_stride, kc, vc,
+                                                   qsrc, qn, kn, rcos, rsin, eps, scale, n_active, j, d0, M, L, o))
     return;
   float* op = out + ((int64_t)m * H + g * GQ + j) * D + d0;  // j, d0: wave 0's lane map
   if (NW != AWV || n_active == 1) {  // NW != AWV: the host launches one split
@@ -2462,9 +2500,14 @@ void attn_block(const float* qsrc, int decode_mode, const float* qn, const float
   // prefill. Batch 32 measured 14.7-17.0 us for every target of 256-1024 blocks, lean or not (attn_batch.hip): the
   // K/V stream of 512 (sequence, kv head) pairs comes in at ~2.8 TB/s whatever the block shape.
   if (decode_mode && g_attn_wide > 0 && M * KV >= g_attn_wide) {  // one 16-wave block per (token, kv head)
-    hipLaunchKernelGGL((k_attn_block<1, 1, 16>), dim3(KV, 1, M), dim3(16 * 64), 0, s, tok_seq, tok_pos, 1, decode_mode,
-                       H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale, out, wk.counters,
-                       wk.partials, qout, dout);
+    if (g_attn_ldspf)
+      hipLaunchKernelGGL((k_attn_block<1, 1, 16, true>), dim3(KV, 1, M), dim3(16 * 64), 0, s, tok_seq, tok_pos, 1,
+                         decode_mode, H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale,
+                         out, wk.counters, wk.partials, qout, dout);
+    else
+      hipLaunchKernelGGL((k_attn_block<1, 1, 16>), dim3(KV, 1, M), dim3(16 * 64), 0, s, tok_seq, tok_pos, 1,
+                         decode_mode, H, KV, seq_stride, seq_stride / KV, kc, vc, qsrc, qn, kn, rcos, rsin, eps, scale,
+                         out, wk.counters, wk.partials, qout, dout);
     return;
   }
   int ns = 1;

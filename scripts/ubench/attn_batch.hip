@@ -71,9 +71,10 @@ int main(int argc, char** argv) {
     printf("wide vs split blocks: max|diff| %.3g of max %.3g %s\n", e, mx, e <= 1e-5 * mx ? "ok" : "FAIL");
     g_attn_wide = 0;
   }
-  for (int target : {-1, 256, 512, 768, 1024}) {
+  for (int target : {-2, -1, 256, 512, 768, 1024}) {
     for (int lean : {0, 1}) {
       if (target < 0 && lean == 0) continue;
+      g_attn_ldspf = target == -1;  // -2: wide blocks with register loads per pass, -1: with the LDS-DMA prefetch
       g_attn_wide = target < 0 ? 1 : 0;
       g_attn_blocks = target < 0 ? 1024 : target; g_attn_lean = lean;
       hipGraph_t g; hipGraphExec_t ex;
@@ -87,7 +88,7 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(a, s)); for (int i = 0; i < R; ++i) CK(hipGraphLaunch(ex, s)); CK(hipEventRecord(b, s));
       CK(hipEventSynchronize(b)); float ms; CK(hipEventElapsedTime(&ms, a, b));
       const double us = ms * 1e3 / R / L;
-      printf("%s target %4d lean %d: %6.2f us per launch, K/V %.1f MB -> %.2f TB/s\n", target < 0 ? "wide  " : "blocks", target, lean, us, bytes / 1e6,
+      printf("%s target %4d lean %d: %6.2f us per launch, K/V %.1f MB -> %.2f TB/s\n", target == -1 ? "wide+pf" : target < 0 ? "wide   " : "blocks ", target, lean, us, bytes / 1e6,
              bytes / (us * 1e-6) / 1e12);
       CK(hipGraphExecDestroy(ex)); CK(hipGraphDestroy(g));
     }

@@ -696,6 +696,33 @@ def test_batched_decode_ffn_one_launch_bit_identical(monkeypatch, n_seq):
     assert runs[1][3] == (0, 0)  # no hand-off timed out
 
 
+def test_batched_decode_attention_lds_prefetch_bit_identical(monkeypatch):
+    """The 16-wave batched-decode attention pulls each next pass's K/V rows into LDS by LDS-DMA while the current pass
+    computes (FUNASR_ATTN_LDSPF=1; off by default, it measured slower): the same bytes reach the same arithmetic, so 32 sequences of 30-510
+    keys decode with the same tokens and logits as with register loads per pass."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(10)
+    lens = [30 + 15 * q for q in range(32)]
+    prompts = [(rng.standard_normal((n, 1024)) * 0.5).astype(np.float32) for n in lens]
+    runs = []
+    for pf in ("0", "1"):
+        monkeypatch.setenv("FUNASR_ATTN_LDSPF", pf)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=560, max_seqs=32), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            for q in range(32):
+                eng.llm_reset(q)
+                eng.llm_prefill(q, prompts[q])
+            toks = eng.llm_generate(list(range(32)), 24)
+            toks1 = eng.llm_generate(list(range(32)), 1)
+            runs.append((toks, toks1, [eng.llm_logits(q) for q in range(32)]))
+        finally:
+            eng.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
