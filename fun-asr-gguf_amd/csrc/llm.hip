@@ -585,6 +585,8 @@ static void launch_gemv_k(int K, const GemvArgs& a, hipStream_t s) {
 // Block = 4 waves over one 32x32 tile, each wave a contiguous quarter of K; partial tiles are summed in
 // LDS in fixed wave order (deterministic). Epilogues as k_gemv_q8.
 typedef int i32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // Scales of NBW consecutive q8_0 blocks of one weight row (fp16, NBW/2 dwords): one load instruction
 template <int NBW>
@@ -743,7 +745,11 @@ __device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx
   // of the coalesced rate)
   constexpr int RB = NBW * 32, LPR = RB / 16, RPI = 64 / LPR, SLD = RB + 16;
   int8_t(&s_ab)[4][2][32 * SLD] = *reinterpret_cast<int8_t(*)[4][2][32 * SLD]>(s_ab_mem);
-  uint32_t dw[16][NBW / 2];  // fp16 scales of this lane's 16 rows, 2 blocks per dword
+  // weight scales: lane (r, h) loads SQ dwords (2 fp16 block scales each) of row o0 + r, blocks [bw0 + 2 SQ h, +2 SQ)
+  // (NBW = 2: both halves load the one dword), converted once per wave into LDS below
+  constexpr int SQ = NBW >= 4 ? NBW / 4 : 1;
+  uint32_t dwr[SQ];
+  const __half* wdr = wd + (int64_t)min(o0 + r, a.O - 1) * nb + bw0 + (NBW >= 4 ? 2 * SQ * h : 0);
   float2 dx2[NBW / 2];
   {
     const int rr = lane / LPR, off = bw0 * 32 + 16 * (lane % LPR);
@@ -754,8 +760,7 @@ __device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx
       for (int i = 0; i < NBW; ++i)
         A[i] = *reinterpret_cast<const i32x4_t*>(wq + (int64_t)min(o0 + RPI * i + rr, a.O - 1) * K + off);
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
+      for (int q = 0; q < SQ; ++q) dwr[q] = *reinterpret_cast<const uint32_t*>(wdr + 2 * q);
       if (threadIdx.x == 0) {
         SpinDeadline dl;
         while ((int)__hip_atomic_load(fz.arr + ks * CNT_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -788,8 +793,7 @@ __device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx
         B[i] = *reinterpret_cast<const i32x4_t*>(a.xq + (int64_t)min(t0 + RPI * i + rr, a.M - 1) * K + off);
       }
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        load_scales<NBW>(wd + (int64_t)min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1) * nb + bw0, dw[reg]);
+      for (int q = 0; q < SQ; ++q) dwr[q] = *reinterpret_cast<const uint32_t*>(wdr + 2 * q);
 #pragma unroll
       for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + bw0 + 2 * q);
     }
@@ -838,16 +842,42 @@ __device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx
       B[j] = *reinterpret_cast<const i32x4_t*>(&s_ab[wave][1][r * SLD + 32 * j + 16 * h]);
     }
   }
+  // the wave's weight scales as f32 in LDS, [block][row], in its own staging image past the 4 KB that s_red takes
+  // below (its fragments are in registers by now); lane (r, h) reads rows 8 g + 4 h + [0, 4) of block j as a float4
+  static_assert(16 * 64 * 4 + NBW * 32 * 4 <= 2 * 32 * SLD, "k_gemm_q8_sk: scales must fit the wave's staging image");
+  float4(&s_dw4)[NBW][8] = *reinterpret_cast<float4(*)[NBW][8]>(&s_ab[wave][0][16 * 64 * 4]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // fragment reads before the scale writes
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    float* s_dw = reinterpret_cast<float*>(&s_dw4[0][0]);
+#pragma unroll
+    for (int q = 0; q < SQ; ++q) {
+      const __half* hq = reinterpret_cast<const __half*>(&dwr[q]);
+      const int j = (NBW >= 4 ? 2 * SQ * h : 0) + 2 * q;
+      s_dw[j * 32 + r] = __half2float(hq[0]);
+      s_dw[(j + 1) * 32 + r] = __half2float(hq[1]);
+    }
+  }
+  f32x2_t acc2[8];  // regs 2 p, 2 p + 1
+#pragma unroll
+  for (int p = 0; p < 8; ++p) acc2[p] = f32x2_t{0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
     const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
+    // acc += f32(dot) * (f32(d_w) * d_x): the scalar form's roundings, two values per instruction
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 1]);
-      acc[reg] += (float)D[reg] * (__half2float(hw[j & 1]) * dx);
+    for (int gq = 0; gq < 4; ++gq) {
+      const float4 d4 = s_dw4[j][2 * gq + h];
+      const f32x2_t lo = f32x2_t{d4.x, d4.y} * dx, hi = f32x2_t{d4.z, d4.w} * dx;
+      acc2[2 * gq] = __builtin_elementwise_fma(f32x2_t{(float)D[4 * gq], (float)D[4 * gq + 1]}, lo, acc2[2 * gq]);
+      acc2[2 * gq + 1] =
+          __builtin_elementwise_fma(f32x2_t{(float)D[4 * gq + 2], (float)D[4 * gq + 3]}, hi, acc2[2 * gq + 1]);
     }
   }
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) acc[reg] = acc2[reg >> 1][reg & 1];
   // fixed-order reduction over the waves
   // s_red[w] in wave w's own staging image (written after the wave read its fragments, read after the barrier)
   static_assert(16 * 64 * 4 <= 2 * 32 * SLD, "k_gemm_q8_sk: wave partials must fit the wave's staging image");
@@ -1078,28 +1108,31 @@ __global__ __launch_bounds__(256, LMB_PER_CU) void k_lm_head_b(GemvArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (tile + (int)gridDim.x < n_tiles) load_tile(tile + gridDim.x, W, sl);
-    float acc[16];
+    f32x2_t acc2[8];  // regs 2 p, 2 p + 1
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
+    for (int p = 0; p < 8; ++p) acc2[p] = f32x2_t{0.f, 0.f};
 #pragma unroll
     for (int jp = 0; jp < NBW / 2; ++jp) {
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int j = 2 * jp + jj;
-        float dw[16];  // block j's scales of rows (reg & 3) + 8 (reg >> 2) + 4 h (wave-half broadcast reads)
+        const i32x4_t Aj = *reinterpret_cast<const i32x4_t*>(sw + r * WLD + 32 * j + 16 * h);  // MFMA layout
+        const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aj, B[j], zero, 0, 0, 0);
+        // block j's scales of rows (reg & 3) + 8 (reg >> 2) + 4 h (wave-half broadcast reads); acc += f32(dot) *
+        // (d_w * d_x) with the scalar form's roundings, two values per instruction (v_pk_mul_f32 / v_pk_fma_f32)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 v = *reinterpret_cast<const float4*>(&s_sc[wave][j][8 * q + 4 * h]);
-          dw[4 * q] = v.x; dw[4 * q + 1] = v.y; dw[4 * q + 2] = v.z; dw[4 * q + 3] = v.w;
+          const f32x2_t lo = f32x2_t{v.x, v.y} * dx[j], hi = f32x2_t{v.z, v.w} * dx[j];
+          acc2[2 * q] = __builtin_elementwise_fma(f32x2_t{(float)D[4 * q], (float)D[4 * q + 1]}, lo, acc2[2 * q]);
+          acc2[2 * q + 1] =
+              __builtin_elementwise_fma(f32x2_t{(float)D[4 * q + 2], (float)D[4 * q + 3]}, hi, acc2[2 * q + 1]);
         }
-        const i32x4_t Aj = *reinterpret_cast<const i32x4_t*>(sw + r * WLD + 32 * j + 16 * h);  // MFMA layout
-        const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(Aj, B[j], zero, 0, 0, 0);
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) acc[reg] += (float)D[reg] * (dw[reg] * dx[j]);
       }
     }
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) *reinterpret_cast<float*>(s_w[wave] + (reg * 64 + lane) * 4) = acc[reg];
+    for (int reg = 0; reg < 16; ++reg)
+      *reinterpret_cast<float*>(s_w[wave] + (reg * 64 + lane) * 4) = acc2[reg >> 1][reg & 1];
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1160,19 +1193,34 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
     A[j] = *reinterpret_cast<const i32x4_t*>(wa + j * 32);
     B[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
   }
-  uint32_t dw[16][NBW / 2];  // fp16 scales of each of this lane's 16 rows, 2 blocks per dword
+  // weight scales: lane (r, h) loads NBW / 4 dwords (2 fp16 block scales each) of row o0 + r, blocks
+  // [b0 + h NBW / 2, +NBW / 2), instead of every lane loading its 16 rows' scales
+  constexpr int NQ = NBW / 4;
+  uint32_t dwr[NQ];
+  {
+    const __half* wr = wd + (int64_t)min(o0 + r, a.O - 1) * nb + b0 + h * (NBW / 2);
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int row = min(o0 + (reg & 3) + 8 * (reg >> 2) + 4 * h, a.O - 1);
-#pragma unroll
-    for (int q = 0; q < NBW / 2; ++q) dw[reg][q] = *reinterpret_cast<const uint32_t*>(wd + (int64_t)row * nb + b0 + 2 * q);
+    for (int q = 0; q < NQ; ++q) dwr[q] = *reinterpret_cast<const uint32_t*>(wr + 2 * q);
   }
   float2 dx2[NBW / 2];
 #pragma unroll
   for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + b0 + 2 * q);
-  float acc[16];
+  __builtin_amdgcn_sched_barrier(0);  // every load issued before any use (hipcc would hoist MFMAs between them)
+  // the wave's scales as f32 in LDS, [block][row]: each lane then reads its 16 rows' (rows 8 g + 4 h + [0, 4)) of a
+  // block as 4 float4, converted once per wave instead of once per lane (wave-private rows: no block barrier)
+  __shared__ float4 s_dw4[NW][NBW][8];
+  float* s_dw = reinterpret_cast<float*>(s_dw4[wave]);
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) acc[reg] = 0.f;
+  for (int q = 0; q < NQ; ++q) {
+    const __half* hq = reinterpret_cast<const __half*>(&dwr[q]);
+    const int j = h * (NBW / 2) + 2 * q;
+    s_dw[j * 32 + r] = __half2float(hq[0]);
+    s_dw[(j + 1) * 32 + r] = __half2float(hq[1]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  f32x2_t acc[8];  // regs 2 p, 2 p + 1
+#pragma unroll
+  for (int p = 0; p < 8; ++p) acc[p] = f32x2_t{0.f, 0.f};
   const i32x16_t zero = {};
 #ifdef FA_GEMV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1182,10 +1230,14 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   for (int j = 0; j < NBW; ++j) {
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
     const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
+    // acc += f32(dot) * (f32(d_w) * d_x): one rounding per product and per fused add, as the scalar form, two
+    // values per instruction (v_pk_mul_f32 / v_pk_fma_f32)
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const __half* hw = reinterpret_cast<const __half*>(&dw[reg][j >> 1]);
-      acc[reg] += (float)D[reg] * (__half2float(hw[j & 1]) * dx);
+    for (int g = 0; g < 4; ++g) {
+      const float4 d4 = s_dw4[wave][j][2 * g + h];
+      const f32x2_t lo = f32x2_t{d4.x, d4.y} * dx, hi = f32x2_t{d4.z, d4.w} * dx;
+      acc[2 * g] = __builtin_elementwise_fma(f32x2_t{(float)D[4 * g], (float)D[4 * g + 1]}, lo, acc[2 * g]);
+      acc[2 * g + 1] = __builtin_elementwise_fma(f32x2_t{(float)D[4 * g + 2], (float)D[4 * g + 3]}, hi, acc[2 * g + 1]);
     }
   }
   // fixed-order reduction over the waves of each matrix (NW = 16: waves w and w + 8 first pair up); thread t then
@@ -1198,18 +1250,18 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   if (NW == 16) {
     if (wave >= 8) {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) s_red[wave - 8][reg][lane] = acc[reg];
+      for (int reg = 0; reg < 16; ++reg) s_red[wave - 8][reg][lane] = acc[reg >> 1][reg & 1];
     }
     __syncthreads();
     if (wave < 8) {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) acc[reg] += s_red[wave][reg][lane];
+      for (int reg = 0; reg < 16; ++reg) acc[reg >> 1][reg & 1] += s_red[wave][reg][lane];
     }
     __syncthreads();
   }
   if (wave < NR) {
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg];
+    for (int reg = 0; reg < 16; ++reg) s_red[wave][reg][lane] = acc[reg >> 1][reg & 1];
   }
   __syncthreads();
   GSTAMP(2);
@@ -1290,7 +1342,6 @@ static bool gemm_q8_kw(const GemvArgs& a, int K, int epi, hipStream_t s, bool fo
 // (EPI 2) runs gate and up in the same waves and quantises the act rows for the down GEMM in registers (a token's
 // 32 rows of a tile are lanes l and l + 32). LDS rows of 64 B + 16 B: 16-B operand reads of 16 rows start in distinct
 // 4-bank groups.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int QT_LD = 80;  // bytes per staged row
 template <int EPI>
 struct QTile {

@@ -4,8 +4,9 @@ python scripts/prof_decode_ab.py [steps] SETTING [SETTING ...]
 SETTING = comma-separated ENV=VALUE assignments applied before the engine is created ('-' = defaults), e.g.
   FUNASR_AB_FULL=0  FUNASR_AB_FULL=1024
 AB_M=<M> decodes M sequences per step; AB_REPS=<r> timed repetitions per setting (default 3); AB_PREFILL=<rows>.
-Prints ms per step per setting and whether its tokens equal the first setting's (settings that change the f32
-summation order may legitimately differ)."""
+Prints ms per step per setting, whether its tokens equal the first setting's (settings that change the f32
+summation order may legitimately differ) and a hash of the tokens and the last logits row (library A/B across processes)."""
+import hashlib
 import os
 import sys
 import time
@@ -49,6 +50,7 @@ for st in settings:
     if ref is None:
         ref = toks
     same = bool(np.array_equal(toks, ref))
+    th = hashlib.sha256(np.ascontiguousarray(toks).tobytes() + eng.llm_logits(0).tobytes()).hexdigest()[:12]
     print(f"M={M} [{st}]: {' '.join(f'{m:.4f}' for m in ms)} ms/step (min {min(ms):.4f}); tokens "
-          f"{'equal' if same else 'differ'}; invariant width {eng.llm_invariant_width()}", flush=True)
+          f"{'equal' if same else 'differ'}; invariant width {eng.llm_invariant_width()}; tokens+logits {th}", flush=True)
     eng.close()
