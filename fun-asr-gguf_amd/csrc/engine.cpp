@@ -136,6 +136,7 @@ struct Engine {
   int4* d_ptiles = nullptr;                     // prefill query tiles {row0, n_rows, seq, 0} (attn_prefill)
   int n_ptiles = 0;                             // tiles of the forward being run (0: per-row attn_block)
   int attn_pf_min_m = 512;                      // query-tiled prefill attention from this many rows (env knob)
+  int attn_pf_rl = 1;                           // ... in row-local forwards, at any size (FUNASR_ATTN_PF_RL; 0: never)
   float* lxg = nullptr;                         // gathered last rows of a prefill batch
   int* d_lastrow = nullptr;
   int chunk_cur = 1;                            // rows per partial of the last lm_head
@@ -1201,9 +1202,13 @@ struct Engine {
   // prefill rows -> query tiles of <= 64 consecutive positions of one sequence (uploaded on the stream; host copy
   // kept in h_ptiles until the next call). Below attn_pf_min_m rows (or head dim != 128) the per-row path runs.
   std::vector<int4> h_ptiles;
-  void set_prefill_tiles(const int* sq, const int* ps, int rows) {
+  // rl (row-local forward): tiles at every row count (a threshold on the call's rows would give a prompt other
+  // arithmetic alone than in a batch), on the f16-MFMA tile kernel only: a row's result there depends on its own keys
+  // alone (fully masked key tiles add exact zeros, rescale by exactly 1), so the forward stays row-local
+  void set_prefill_tiles(const int* sq, const int* ps, int rows, bool rl = false) {
     n_ptiles = 0;
-    if (rows < attn_pf_min_m || lc.head_dim != 128 || lc.n_head != 2 * lc.n_head_kv) return;
+    if (rl ? (!fa::g_attn_pf_f16 || !attn_pf_rl) : rows < attn_pf_min_m) return;
+    if (lc.head_dim != 128 || lc.n_head != 2 * lc.n_head_kv) return;
     h_ptiles.clear();
     for (int r = 0; r < rows; ++r) {
       const bool cont = r > 0 && h_ptiles.back().y < 64 && h_ptiles.back().z == sq[r] && ps[r - 1] + 1 == ps[r];
@@ -1273,7 +1278,7 @@ struct Engine {
           qk_rope_store(lqkv, M, H, KV, lc.rms_eps, w.q_norm, w.k_norm, rcos, rsin, d_tok_seq, d_tok_pos, lq, kc, vc,
                         seq_stride, stream);
         // M > 4: the attention also leaves its rows as q8_0 blocks for the o GEMM (no prep launch)
-        if (!decode && n_ptiles > 0 && !rl)  // query tiles: each K/V tile serves 64 rows x 2 heads
+        if (!decode && n_ptiles > 0)  // query tiles: each K/V tile serves 64 rows x 2 heads (set_prefill_tiles)
           attn_prefill(d_ptiles, n_ptiles, d_tok_pos, H, KV, seq_stride, kc, vc, lq, latt, small ? nullptr : lxq2,
                        small ? nullptr : lxd2, stream);
         else
@@ -1577,7 +1582,7 @@ struct Engine {
     for (int i = 0; i < n_tokens; ++i) ps[i] = n_past[seq] + i;
     FA_HIP(hipMemcpyAsync(d_tok_seq, sq.data(), n_tokens * 4, hipMemcpyHostToDevice, stream));
     FA_HIP(hipMemcpyAsync(d_tok_pos, ps.data(), n_tokens * 4, hipMemcpyHostToDevice, stream));
-    set_prefill_tiles(sq.data(), ps.data(), n_tokens);
+    set_prefill_tiles(sq.data(), ps.data(), n_tokens, n_tokens <= pf_rl_max);
     pf_row_local = n_tokens <= pf_rl_max;
     try {
       llm_forward(n_tokens, false, n_past[seq] + n_tokens - 1);
@@ -1805,6 +1810,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     fa::g_attn_wide = 256;
     if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_ATTN_LDSPF")) fa::g_attn_ldspf = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ATTN_PF_F16")) fa::g_attn_pf_f16 = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ATTN_PF_RL")) e->attn_pf_rl = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
@@ -2265,7 +2272,7 @@ static void prefill_batch(Engine* e, const int32_t* seqs, int32_t n_seqs, const 
     FA_HIP(hipMemcpyAsync(e->d_tok_seq, sq.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_tok_pos, ps.data(), rows * 4, hipMemcpyHostToDevice, e->stream));
     FA_HIP(hipMemcpyAsync(e->d_lastrow, last.data(), n * 4, hipMemcpyHostToDevice, e->stream));
-    e->set_prefill_tiles(sq.data(), ps.data(), rows);
+    e->set_prefill_tiles(sq.data(), ps.data(), rows, e->pf_row_local);
     try {
       e->llm_forward(rows, false, 0, n);
     } catch (...) {

@@ -588,6 +588,23 @@ typedef int i32x16_t __attribute__((ext_vector_type(16)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+// int8 MFMA returning f32: the accumulator starts at 1.5 * 2^23, so every element is the f32 bit pattern of
+// 12582912 + dot (|dot| <= 32 * 128 * 128 < 2^22) and as_float(D) - 12582912 == (float)dot exactly (both operands in
+// [2^23, 2^24): Sterbenz), two elements per v_pk_add_f32 instead of one v_cvt_f32_i32 each
+// (MAGIC = false: the plain conversion, for kernels where the constant's 16 registers would spill)
+template <bool MAGIC = true>
+__device__ __forceinline__ f32x16 mfma_i8_f32(const i32x4_t& a, const i32x4_t& b) {
+  if constexpr (MAGIC) {
+    constexpr int M = 0x4B400000;
+    const i32x16_t magic = {M, M, M, M, M, M, M, M, M, M, M, M, M, M, M, M};
+    const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, magic, 0, 0, 0);
+    return __builtin_bit_cast(f32x16, D) - 12582912.0f;
+  } else {
+    const i32x16_t zero = {};
+    return __builtin_convertvector(__builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, zero, 0, 0, 0), f32x16);
+  }
+}
+
 // Scales of NBW consecutive q8_0 blocks of one weight row (fp16, NBW/2 dwords): one load instruction
 template <int NBW>
 __device__ __forceinline__ void load_scales(const __half* p, uint32_t (&d)[NBW / 2]) {
@@ -864,6 +881,7 @@ __device__ __forceinline__ void sk_tile(const GemvArgs& a, int K, int KS, int bx
   for (int p = 0; p < 8; ++p) acc2[p] = f32x2_t{0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
+    // (the 1.5 * 2^23 accumulator start of mfma_i8_f32 measured 1 % slower here)
     const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
     const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
     // acc += f32(dot) * (f32(d_w) * d_x): the scalar form's roundings, two values per instruction
@@ -1228,7 +1246,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
 #endif
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
-    const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);
+    const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], B[j], zero, 0, 0, 0);  // (1.5 * 2^23 start: no gain)
     const float dx = (j & 1) ? dx2[j >> 1].y : dx2[j >> 1].x;
     // acc += f32(dot) * (f32(d_w) * d_x): one rounding per product and per fused add, as the scalar form, two
     // values per instruction (v_pk_mul_f32 / v_pk_fma_f32)
@@ -1463,11 +1481,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_q8_t(GemvArgs a, int K) {
           }
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
-            const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(aw, bx[jj], zero, 0, 0, 0);
+            const f32x16 D = mfma_i8_f32<EPI != 2>(aw, bx[jj]);  // SwiGLU form: 255 VGPRs already
             // acc += f32(dot) * (f32(d_w) * d_x), one rounding per product and per fused add as before, on 16-wide
             // vectors: v_pk_mul_f32 / v_pk_fma_f32 (two values per instruction; hipcc packed the EPI 0 / 1 forms by
             // itself but not the SwiGLU one)
-            acc[m][i][jj] = __builtin_elementwise_fma(__builtin_convertvector(D, f32x16), dwv * dx[jj], acc[m][i][jj]);
+            acc[m][i][jj] = __builtin_elementwise_fma(D, dwv * dx[jj], acc[m][i][jj]);
           }
           __builtin_amdgcn_sched_barrier(0);  // one (matrix, row tile) at a time: two MFMA results live, not eight
         }
@@ -2532,12 +2550,180 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill(const int4* __restrict_
   }
 }
 
+// The same tiles on f16 MFMAs (v_mfma_f32_32x32x16_f16, 16x the f32 MFMA rate): the cache's K and V are fp16 values,
+// so they are exact f16 operands. S^T = K . Q^T takes q split into f16 hi + lo (q * d^-0.5, then times 2^8 so the lo
+// part stays out of the f16 subnormals; the scores are scaled back by 2^-8, exactly): two MFMAs per 16 dims, products
+// exact, q kept to 22 of f32's 24 bits. O^T += V^T . P^T takes P^T straight from the S accumulator split into f16
+// hi + lo (as the fp16 encoder attention, attn_f32.hip) with V^T fragments from ds_read_b64_tr_b16. Masking, online
+// softmax and the epilogue are k_attn_prefill's; per row the result depends only on its own keys (row-local).
+typedef _Float16 f16x8p __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4p __attribute__((ext_vector_type(4)));
+typedef short v4i16p __attribute__((ext_vector_type(4)));
+typedef float f32x8v __attribute__((ext_vector_type(8)));
+constexpr int PHK = PAD + 8, PHV = PAD + 32;  // K rows: 16-B reads of 16 rows on distinct banks; V rows: the tr reads'
+constexpr int PH_STAGE = PAK * PHK + PAK * PHV;  // halves per stage (K plane, V plane)
+
+__global__ __launch_bounds__(256, 2) void k_attn_prefill_h(const int4* __restrict__ tiles, const int* __restrict__ tok_pos,
+                                                        int H, int KV, int64_t seq_stride, int64_t head_stride,
+                                                        const __half* __restrict__ kc, const __half* __restrict__ vc,
+                                                        const float* __restrict__ q, float scale, float* __restrict__ out,
+                                                        int8_t* __restrict__ qout, float* __restrict__ dout) {
+  constexpr int OS = PAD + 4;
+  constexpr int SMEM_F = (2 * PH_STAGE / 2 > 64 * OS) ? 2 * PH_STAGE / 2 : 64 * OS;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM_F];  // 2 stages of f16 K / V planes; O staging reuses it
+  __shared__ float s_l[PAQ];
+  const int4 td = tiles[blockIdx.x];
+  const int row0 = td.x, nr = td.y, seq = td.z, g = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int hh = wave >> 1, rr = (wave & 1) * 32 + r;  // this lane's query slot: head 2 g + hh, tile row rr
+  const int rrc = min(rr, nr - 1);
+  const int pos = tok_pos[row0 + rrc];
+  const int pmax = tok_pos[row0 + nr - 1];
+  const __half* kb = kc + (int64_t)seq * seq_stride + g * head_stride;
+  const __half* vb = vc + (int64_t)seq * seq_stride + g * head_stride;
+  f16x8p qh[PAD / 16], ql[PAD / 16];  // k-step st: dims 16 st + 8 h + [0, 8) of this lane's slot
+  {
+    const float* p = q + (int64_t)(row0 + rrc) * H * PAD + (2 * g + hh) * PAD + 8 * h;
+#pragma unroll
+    for (int st = 0; st < PAD / 16; ++st) {
+      const float4 a = *reinterpret_cast<const float4*>(p + 16 * st);
+      const float4 b = *reinterpret_cast<const float4*>(p + 16 * st + 4);
+      const f32x8v x = f32x8v{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w} * scale * 256.0f;
+      qh[st] = __builtin_convertvector(x, f16x8p);
+      ql[st] = __builtin_convertvector(x - __builtin_convertvector(qh[st], f32x8v), f16x8p);
+    }
+  }
+  // staging: 32 keys x 128 dims fp16 per K (and V) tile = 512 chunks of 8 halves, 2 per thread (chunk f = t + 256 c:
+  // key f >> 4, dims 8 (f & 15) + [0, 8)); plain registers, not arrays (hipcc kept lambda-captured arrays in scratch)
+  const int ld_key = threadIdx.x >> 4, ld_d8 = threadIdx.x & 15;
+  uint4 pk0, pk1, pv0, pv1;
+#define PFH_LOAD(kt)                                                                               \
+  do {                                                                                             \
+    const int k0_ = min((kt) * PAK + ld_key, pmax), k1_ = min((kt) * PAK + 16 + ld_key, pmax);     \
+    pk0 = *reinterpret_cast<const uint4*>(kb + (int64_t)k0_ * PAD + 8 * ld_d8);                    \
+    pv0 = *reinterpret_cast<const uint4*>(vb + (int64_t)k0_ * PAD + 8 * ld_d8);                    \
+    pk1 = *reinterpret_cast<const uint4*>(kb + (int64_t)k1_ * PAD + 8 * ld_d8);                    \
+    pv1 = *reinterpret_cast<const uint4*>(vb + (int64_t)k1_ * PAD + 8 * ld_d8);                    \
+  } while (0)
+  _Float16* sh = reinterpret_cast<_Float16*>(smem);
+#define PFH_STORE(stage)                                                                           \
+  do {                                                                                             \
+    _Float16* ks_w = sh + (stage) * PH_STAGE;                                                      \
+    _Float16* vs_w = ks_w + PAK * PHK;                                                             \
+    *reinterpret_cast<uint4*>(ks_w + ld_key * PHK + 8 * ld_d8) = pk0;                              \
+    *reinterpret_cast<uint4*>(vs_w + ld_key * PHV + 8 * ld_d8) = pv0;                              \
+    *reinterpret_cast<uint4*>(ks_w + (16 + ld_key) * PHK + 8 * ld_d8) = pk1;                       \
+    *reinterpret_cast<uint4*>(vs_w + (16 + ld_key) * PHV + 8 * ld_d8) = pv1;                       \
+  } while (0)
+  f32x16 o[PAD / 32];
+#pragma unroll
+  for (int i = 0; i < PAD / 32; ++i) o[i] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int n_kt = pmax / PAK + 1;
+  PFH_LOAD(0);
+  PFH_STORE(0);
+  __syncthreads();
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int stage = kt & 1;
+    if (kt + 1 < n_kt) PFH_LOAD(kt + 1);
+    const _Float16* ks_ = sh + stage * PH_STAGE;
+    const _Float16* vs_ = ks_ + PAK * PHK;
+    f32x16 sc = {};
+#pragma unroll
+    for (int st = 0; st < PAD / 16; ++st) {
+      const f16x8p kf = *reinterpret_cast<const f16x8p*>(ks_ + r * PHK + 16 * st + 8 * h);
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, ql[st], sc, 0, 0, 0);
+      sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qh[st], sc, 0, 0, 0);
+    }
+    sc *= 1.0f / 256.0f;
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int key = kt * PAK + (t & 3) + 8 * (t >> 2) + 4 * h;
+      const float v = key <= pos ? sc[t] : -INFINITY;
+      sc[t] = v;
+      mt = fmaxf(mt, v);
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float pr = sc[t] == -INFINITY ? 0.f : __expf(sc[t] - m_new);
+      sc[t] = pr;
+      ls += pr;
+    }
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < PAD / 32; ++i) o[i] *= alpha;
+    // P^T k-step s2 = accumulator registers 8 s2 .. 8 s2 + 7 (keys 16 s2 + 8 (j >> 2) + 4 h + (j & 3))
+#pragma unroll
+    for (int s2 = 0; s2 < PAK / 16; ++s2) {
+      f16x8p ph, pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ph[j] = (_Float16)sc[8 * s2 + j];
+        pl[j] = (_Float16)(sc[8 * s2 + j] - (float)ph[j]);
+      }
+      const int gq = lane >> 4, key = 16 * s2 + 4 * (gq >> 1) + ((lane >> 2) & 3);
+#pragma unroll
+      for (int i = 0; i < PAD / 32; ++i) {
+        const int off = key * PHV + 32 * i + 16 * (gq & 1) + 4 * (lane & 3);
+        const f16x4p h0 = __builtin_bit_cast(
+            f16x4p, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16p*)(vs_ + off)));
+        const f16x4p h1 = __builtin_bit_cast(
+            f16x4p,
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16p*)(vs_ + off + 8 * PHV)));
+        const f16x8p vh = f16x8p{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[i], 0, 0, 0);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[i], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < n_kt) PFH_STORE(stage ^ 1);
+    __syncthreads();
+  }
+#undef PFH_LOAD
+#undef PFH_STORE
+  // epilogue: k_attn_prefill's (O^T has the same accumulator layout: dims on registers, slots on lanes)
+  float* so = smem;
+  if (h == 0) s_l[hh * 64 + rr] = l_run;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (hh == half) {
+#pragma unroll
+      for (int i = 0; i < PAD / 32; ++i)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) so[rr * OS + i * 32 + (t & 3) + 8 * (t >> 2) + 4 * h] = o[i][t];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int f = threadIdx.x + 256 * c, row = f >> 5, d4 = f & 31;
+      const float inv = 1.0f / s_l[half * 64 + row];
+      float4 v = *reinterpret_cast<const float4*>(so + row * OS + 4 * d4);
+      v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
+      const int orow = row0 + min(row, nr - 1);
+      const int64_t e = (int64_t)orow * H * PAD + (2 * g + half) * PAD + 4 * d4;
+      if (row < nr) {
+        *reinterpret_cast<float4*>(out + e) = v;
+        if (qout) store_q8_row4(qout, dout, e, threadIdx.x, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int g_attn_pf_f16 = 1;  // query-tiled prefill attention on f16 MFMAs (FUNASR_ATTN_PF_F16; 0: exact-f32 MFMAs)
+
 void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int KV, int64_t seq_stride, const __half* kc,
                   const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s) {
   FA_REQUIRE(H == KV * GQ, "attn_prefill: n_head must be 2*n_head_kv");
   if (n_tiles <= 0) return;
-  hipLaunchKernelGGL(k_attn_prefill, dim3(n_tiles, KV), dim3(256), 0, s, tiles, tok_pos, H, KV, seq_stride,
-                     seq_stride / KV, kc, vc, q, 1.0f / sqrtf(128.0f), out, qout, dout);
+  hipLaunchKernelGGL(g_attn_pf_f16 ? k_attn_prefill_h : k_attn_prefill, dim3(n_tiles, KV), dim3(256), 0, s, tiles,
+                     tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, q, 1.0f / sqrtf(128.0f), out, qout, dout);
 }
 
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,

@@ -543,6 +543,33 @@ def test_llm_prefill_batch_continuation_query_tiles(llm_tiny_oracle, monkeypatch
         e.close()
 
 
+@pytest.mark.parametrize("f16", ["0", "1"])
+def test_llm_prefill_query_tiles_f16_mfma_vs_oracle(llm_tiny_oracle, monkeypatch, f16):
+    """The query-tiled prefill attention on f16 MFMAs (k_attn_prefill_h: the cache's fp16 K / V exact, q split into f16
+    hi + lo, P split into f16 hi + lo; FUNASR_ATTN_PF_F16=1, the default) and on exact-f32 MFMAs (=0): a four-prompt
+    batch above the invariant width (tiles cut at 64 rows, one prompt continuing a cached prefix) against the oracle's
+    teacher-forced logits, and the two kernels' logits within the q8_0 noise floor of each other."""
+    from fun_asr_gguf import _native
+    monkeypatch.setenv("FUNASR_ATTN_PF_F16", f16)
+    monkeypatch.setenv("FUNASR_ATTN_PREFILL_MIN_M", "8")
+    monkeypatch.setenv("FUNASR_FUSED_MAX_M", "1")  # invariant width 1: the batch takes the shared-forward kernels
+    m = llm_tiny_oracle
+    rng = np.random.default_rng(44)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (100, 9, 66, 40)]
+    e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=160, max_seqs=4), max_batch=1, max_samples=16000)
+    try:
+        e.synthetic_weights(0)
+        for s in range(4):
+            e.llm_reset(s)
+        e.llm_prefill_batch([0, 1], [prompts[0][:30], prompts[1]], temperature=0.0)
+        e.llm_prefill_batch([2, 0, 3], [prompts[2], prompts[0][30:], prompts[3]], temperature=0.0)
+        for s in (0, 2, 3):
+            m.reset()
+            _check_step(e.llm_logits(s), m.forward(prompts[s], 0))
+    finally:
+        e.close()
+
+
 def test_llm_generate_begin_end_equals_generate(llm_tiny_oracle):
     """fa_llm_generate_begin / _end (the host works while the chunk runs) give the tokens of fa_llm_generate, chunk
     after chunk, and the other LLM calls refuse while a chunk is in flight."""
