@@ -394,6 +394,22 @@ __device__ __forceinline__ f16x4a ld_tr4h(const _Float16* p) {
   return __builtin_bit_cast(f16x4a, v);
 }
 
+// XCD-aware block order: the blocks that stream the same K/V rows -- the query tiles of one (key split, head, clip)
+// group -- are dispatched to one XCD, so that XCD's L2 fetches those rows once, instead of the round-robin dispatch
+// (linear block id % 8) sending them to eight L2s. Linear id -> XCD lin % 8, slot lin / 8 -> query tile slot % per of
+// group (slot / per) 8 + XCD (per = the grid's query tiles per group); a bijection of the same grid when the group
+// count is a multiple of 8 (otherwise the dispatch order stays). Results unchanged.
+__device__ __forceinline__ void attn_xcd_coords(int per, int KS, int& qt, int& ks, int& head, int& clip) {
+  const int G = KS * gridDim.y * gridDim.z;
+  if ((int)gridDim.x != per * KS || (G & 7)) return;
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int slot = lin >> 3, grp = (slot / per) * 8 + (lin & 7);
+  qt = slot % per;
+  ks = grp % KS;
+  head = (grp / KS) % gridDim.y;
+  clip = grp / (KS * gridDim.y);
+}
+
 // P = 1: the fp16 graph's attention (C5) on v_mfma_f32_32x32x16_f16: q, k and v are fp16 values (outputs of the fp16
 // q|k|v projection), so S^T = K . Q^T is one f16 MFMA per 16 of k with exact products (d^-0.5 applied to the f32
 // scores after the dot), and O^T += V^T . P^T is two (P^T split into f16 hi + lo in registers, V^T exact): the
@@ -408,14 +424,16 @@ __global__ __launch_bounds__(256, 2) void k_attn_bf3(const float* __restrict__ Q
                                                   const float* __restrict__ V, int64_t ldq, int64_t ldk, int64_t ldv,
                                                   float* __restrict__ O, int64_t ldo, int t_stride,
                                                   const int* __restrict__ lens, float scale, int KS,
-                                                  float* __restrict__ part, int* __restrict__ cnt, APlanesD op) {
+                                                  float* __restrict__ part, int* __restrict__ cnt, APlanesD op,
+                                                  int xcd_order) {
   using L = AttnLds3<D>;
   constexpr int NDT = D / 32;
   constexpr int NKS = D / 16;  // k-steps of the S product
   extern __shared__ float lds[];
   const int n_qt = (t_stride + AQ - 1) / AQ;
   const int n_qt8 = (n_qt + 7) & ~7;
-  const int qt = blockIdx.x % n_qt8, ks = blockIdx.x / n_qt8, head = blockIdx.y, clip = blockIdx.z;
+  int qt = blockIdx.x % n_qt8, ks = blockIdx.x / n_qt8, head = blockIdx.y, clip = blockIdx.z;
+  if (xcd_order) attn_xcd_coords(KS == 1 ? n_qt : n_qt8, KS, qt, ks, head, clip);
   if (qt >= n_qt) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -598,6 +616,7 @@ __global__ __launch_bounds__(256, 2) void k_attn_bf3(const float* __restrict__ Q
 int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hip)
 int g_attn_f16_mfma = 1;          // fp16 graph attention on f16 MFMAs (k_attn_bf3<D, 1>); 0: exact f32 + rounding (A/B)
 int g_attn_wab = 0;               // k_attn_bf3 write-after-barrier staging (S = 1; FUNASR_ATTN_WAB)
+int g_attn_xcd = 0;               // k_attn_bf3 XCD-aware block order (FUNASR_ATTN_XCD=1; measured neutral: off)
 
 template <int D, int P>
 static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const float* K, const float* V, int64_t ldq,
@@ -609,12 +628,13 @@ static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const floa
     (void)hipFuncSetAttribute((const void*)k_attn_bf3<D, P, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds3<D>::BYTES);
     attr = true;
   }
+  const int xo = g_attn_xcd;
   if (g_attn_wab)
     hipLaunchKernelGGL((k_attn_bf3<D, P, 1>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt, op);
+                       t_stride, lens, scale, KS, wk.part, wk.cnt, op, xo);
   else
     hipLaunchKernelGGL((k_attn_bf3<D, P, 0>), grid, dim3(256), AttnLds3<D>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, wk.part, wk.cnt, op);
+                       t_stride, lens, scale, KS, wk.part, wk.cnt, op, xo);
 }
 
 int attn_f32_splits(int batch, int t_stride, int n_heads) {

@@ -1811,6 +1811,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_ATTN_WIDE")) fa::g_attn_wide = std::max(0, atoi(g));
     if (const char* g = getenv("FUNASR_ATTN_LDSPF")) fa::g_attn_ldspf = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_PF_F16")) fa::g_attn_pf_f16 = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ATTN_XCD")) fa::g_attn_xcd = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_PF_RL")) e->attn_pf_rl = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = std::min(2, std::max(0, atoi(g)));

@@ -170,6 +170,7 @@ bool gemm_q8_gu_down(const GemvArgs& g, const GemvArgs& d, unsigned* cnt, int* e
 extern int g_attn_lean;    // -1 auto, 0/1 force the 128-VGPR attention variant (A/B)
 extern int g_attn_blocks;  // attention key-split target (blocks per launch), 1024 by default
 extern int g_attn_wide;    // decode launches with >= this many (token, kv head) pairs: 16-wave blocks, no splits
+extern int g_attn_xcd;  // encoder attention (k_attn_bf3): the query tiles of one (head, clip) on one XCD
 extern int g_attn_pf_f16;  // query-tiled prefill attention on f16 MFMAs (q split hi + lo; 0: exact-f32 MFMAs)
 extern int g_attn_ldspf;   // ... with the next pass's K/V pulled into LDS by LDS-DMA during the current pass
 extern int g_lm_head_mt6;    // LM head of 3-6 token batches in one block row (default 1)

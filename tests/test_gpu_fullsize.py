@@ -708,3 +708,30 @@ def test_encoder_activation_planes_bit_identical(monkeypatch):
                 assert np.array_equal(outs[0][k]["enc"][b], outs[v][k]["enc"][b]), f"mode {v} call {k} clip {b}: encoder"
                 assert np.array_equal(outs[0][k]["audio_embd"][b], outs[v][k]["audio_embd"][b]), f"mode {v} {k} {b}"
                 assert np.array_equal(outs[0][k]["ctc_ids"][b], outs[v][k]["ctc_ids"][b]), f"mode {v} {k} {b}: CTC ids"
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_encoder_attention_xcd_order_bit_identical(monkeypatch, fp16):
+    """The encoder attention's XCD-aware block order (FUNASR_ATTN_XCD=1, off by default: the query tiles of one (key split,
+    head, clip) group dispatched to one XCD so its L2 fetches their K/V rows once) is a permutation of the same blocks:
+    eight 60 s clips (no key splits) and one 60 s clip (key splits) encode bit-identically with the dispatch order, in
+    the bf16x3 and the fp16 graphs."""
+    from fun_asr_gguf import _native
+    from fun_asr_gguf.synthetic import synth_audio
+    clips = [synth_audio(SR * 60, 500 + i) for i in range(8)]
+    outs = []
+    for xo in ("0", "1"):
+        monkeypatch.setenv("FUNASR_ATTN_XCD", xo)
+        e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=8,
+                           max_samples=SR * 62)
+        try:
+            e.synthetic_weights(0)
+            e.set_encoder_fp16(fp16)
+            outs.append((e.encode(clips, want_enc=True), e.encode(clips[5:6], want_enc=True)))
+        finally:
+            e.close()
+    for k in range(2):
+        for b in range(len(outs[0][k]["enc"])):
+            assert np.array_equal(outs[0][k]["enc"][b], outs[1][k]["enc"][b]), f"call {k} clip {b}: encoder rows"
+            assert np.array_equal(outs[0][k]["audio_embd"][b], outs[1][k]["audio_embd"][b]), f"call {k} clip {b}"
+
