@@ -261,25 +261,42 @@ __global__ __launch_bounds__(256, 2) void k_attn_f32(const float* __restrict__ Q
       s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qreg[c + 3], s, 0, 0, 0);
     }
     // mask + online softmax (per query = per lane column; keys on registers and lane halves)
+    // a tile of valid keys only (block-uniform; every tile but a clip's last) needs no mask and holds no -inf score:
+    // the same values without the per-score compares and selects
+    const bool full = k0 + AK <= min(len, t_stride);
     float mt = -INFINITY;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
-      float v = s[t];
-      if (key >= t_stride) v = -INFINITY;
-      else if (key >= len) v = v + -10000.0f;
-      s[t] = v;
-      mt = fmaxf(mt, v);
+      for (int t = 0; t < 16; ++t) mt = fmaxf(mt, s[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
+        float v = s[t];
+        if (key >= t_stride) v = -INFINITY;
+        else if (key >= len) v = v + -10000.0f;
+        s[t] = v;
+        mt = fmaxf(mt, v);
+      }
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
     float ls = 0.f;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
-      s[t] = p;
-      ls += p;
+      for (int t = 0; t < 16; ++t) {
+        const float p = __expf(s[t] - m_new);
+        s[t] = p;
+        ls += p;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
+        s[t] = p;
+        ls += p;
+      }
     }
     ls += __shfl_xor(ls, 32, 64);
     l_run = l_run * alpha + ls;
@@ -520,25 +537,42 @@ __global__ __launch_bounds__(256, 2) void k_attn_bf3(const float* __restrict__ Q
     asm volatile("" : "+v"(alpha));
     m_run = 0.f;
 #else
+    // a tile of valid keys only (block-uniform; every tile but a clip's last) needs no mask and holds no -inf score:
+    // the same values without the per-score compares and selects
+    const bool full = k0 + AK <= min(len, t_stride);
     float mt = -INFINITY;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
-      float v = s[t];
-      if (key >= t_stride) v = -INFINITY;
-      else if (key >= len) v = v + -10000.0f;
-      s[t] = v;
-      mt = fmaxf(mt, v);
+      for (int t = 0; t < 16; ++t) mt = fmaxf(mt, s[t]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int key = k0 + (t & 3) + 8 * (t >> 2) + 4 * h;
+        float v = s[t];
+        if (key >= t_stride) v = -INFINITY;
+        else if (key >= len) v = v + -10000.0f;
+        s[t] = v;
+        mt = fmaxf(mt, v);
+      }
     }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
     float ls = 0.f;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
-      s[t] = p;
-      ls += p;
+      for (int t = 0; t < 16; ++t) {
+        const float p = __expf(s[t] - m_new);
+        s[t] = p;
+        ls += p;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const float p = s[t] == -INFINITY ? 0.f : __expf(s[t] - m_new);
+        s[t] = p;
+        ls += p;
+      }
     }
     ls += __shfl_xor(ls, 32, 64);
     l_run = l_run * alpha + ls;
