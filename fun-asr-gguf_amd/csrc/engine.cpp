@@ -791,7 +791,7 @@ struct Engine {
     lxg = alloc<float>((size_t)lc.max_seqs * E);   // prefill batch: the last row of each sequence (LM head input)
     d_lastrow = alloc<int>(lc.max_seqs);
     logits = alloc<float>((size_t)lc.max_seqs * lc.n_vocab);
-    n_part = std::max(lm_head_parts(lc.n_vocab, 1), lm_head_parts(lc.n_vocab, lc.max_seqs));
+    n_part = std::max(lm_head_parts(lc.n_vocab, 1, E), cdiv(lc.n_vocab, 32));  // the GEMV's partials or one per 32-row tile
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
     d_ssp = alloc<float>((size_t)lc.max_seqs * 32);
@@ -1340,8 +1340,8 @@ struct Engine {
     h.M = n_rows; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
-    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows);
-    chunk_cur = lm_head_chunk(lc.n_vocab, n_rows);
+    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, n_rows, E);
+    chunk_cur = lm_head_chunk(lc.n_vocab, n_rows, E);
     if (gemv_small(n_rows)) { h.x = xrow; h.ldx = E; h.norm_w = out_norm; }
     else if (nrm) { h.xq = lxq; h.xd = lxd; h.ssp = d_ssp; }  // rows from the last down epilogue
     else { prep_q8(xrow, E, out_norm, lc.rms_eps, n_rows, E, lxq, lxd, stream); h.xq = lxq; h.xd = lxd; }
@@ -1431,8 +1431,8 @@ struct Engine {
     h.M = 1; h.eps = lc.rms_eps; h.wq = tok_embd.q; h.wd = tok_embd.d; h.O = lc.n_vocab;
     h.rpw = gemv_rows_per_wave(lc.n_vocab);
     h.out = logits; h.ldo = lc.n_vocab;
-    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, 1);
-    chunk_cur = lm_head_chunk(lc.n_vocab, 1);
+    h.pval = pval; h.pidx = pidx; h.n_part = n_part_cur = lm_head_parts(lc.n_vocab, 1, E);
+    chunk_cur = lm_head_chunk(lc.n_vocab, 1, E);
     h.x = fdw.xmid; h.ldx = E; h.norm_w = out_norm; h.psum = fdw.dpart;
     if (step_mask & 4) gemv(h, E, 3);
   }
@@ -1758,6 +1758,12 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     {
       const char* g = getenv("FUNASR_LM_HEAD_MT6");
       fa::g_lm_head_mt6 = g ? atoi(g) != 0 : 1;
+    }
+    {  // small-batch MFMA LM head (k_lm_head_s): re-read (or reset) at every engine creation
+      const char* g = getenv("FUNASR_LM_HEAD_S");
+      fa::g_lm_head_s = g ? std::min(2, std::max(0, atoi(g))) : 1;
+      const char* g1 = getenv("FUNASR_LM_HEAD_S1");
+      fa::g_lm_head_s1 = g1 ? std::min(2, std::max(0, atoi(g1))) : 0;
     }
     if (const char* g = getenv("FUNASR_STEP_MASK")) e->step_mask = atoi(g) & 15;
     if (const char* g = getenv("FUNASR_GRAPH_SYNC_EVERY")) e->graph_sync_every = std::max(0, atoi(g));

@@ -161,7 +161,7 @@ void prep_q8(const float* x, int64_t ldx, const float* w, float eps, int M, int 
 void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s);
 int gemv_rows_per_wave(int O);
 // argmax partials per token written by the lm_head launch for M tokens (GEMV for gemv_small(M), MFMA GEMM above)
-int lm_head_parts(int O, int M);
+int lm_head_parts(int O, int M, int K = 1024);
 int gemm_k_splits(int O, int M, int K, int epi);  // K splits of the split-K GEMM form for this shape
 // batched decode (M <= 32, producer-normalised inputs): gate|up + SwiGLU and the down projection in one launch with a
 // group-local hand-off per down K split; cnt = 64 zeroed counter lines (re-armed in-launch), err = timeout flag.
@@ -180,6 +180,8 @@ extern int g_gemv_small_max;  // fused-GEMV decode path for M <= this (default 5
 extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (default 2)
 bool gemv_small(int M);
 extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
+extern int g_lm_head_s;     // LM head of 2-8 tokens (fused decode path) on k_lm_head_s (bit-identical to batch 1): 0 off, 1/2 = PF
+extern int g_lm_head_s1;    // ... and of one token (0: the GEMV)
 extern int g_lm_head_b;     // 1: batched LM head on the persistent tile loop (k_lm_head_b); 0: split-K block kernel
 extern int g_gemm_t_min_m;  // token count from which the 128x128-tile int8 GEMM runs (prefill batches; default 512)
 void qk_rope_store(const float* qkv, int M, int H, int KV, float eps, const float* qn, const float* kn, const float* rcos,
@@ -286,7 +288,7 @@ struct SampleParams {
 void sample_tokens(const float* logits, int64_t ldl, int V, const float* pval, const int* pidx, int n_part, int chunk,
                    int M, const SampleParams* d_params, const int* row_seq, const int* row_pos, int* step_ctr,
                    int* tok_out, int* tok_hist, int hist_stride, const EmbedNext* en, hipStream_t s);
-int lm_head_chunk(int O, int M);  // rows per argmax partial of the lm_head launch for M tokens
+int lm_head_chunk(int O, int M, int K = 1024);  // rows per argmax partial of the lm_head launch for M tokens
 void advance_positions(int* tok_pos, int* step_ctr, int M, hipStream_t s);
 void gpu_delay_us(int us, hipStream_t s);
 

@@ -1184,6 +1184,188 @@ __global__ __launch_bounds__(256, LMB_PER_CU) void k_lm_head_b(GemvArgs a) {
   }
 }
 
+// Small-batch LM head (2-8 tokens, K = 1024, fused rmsnorm + q8_0 prologue): the persistent tile loop of k_lm_head_b
+// with the operands swapped (A = the block's token rows from LDS, held in registers for the whole launch; B = the
+// tile's weight rows through the LDS image), so a lane's D registers 0-3 are tokens 4 h .. 4 h + 3 of weight row
+// lane & 31 and only those four are scaled. Every logit is BIT-IDENTICAL to the batch-1 GEMV's (k_gemv_q8, EPI 3):
+// the same prologue (norm_quant_block_regs per token), the same per-block product f32(dot) * (f32(d_w) * d_x) and the
+// same balanced tree over the 32 blocks in block order that wave_sum forms (pairs, quads, eights inside a wave's 8
+// blocks, then (w0 + w1) + (w2 + w3) across the waves; the GEMV's leaves pass through one + 0.0f, so a pair of -0
+// products sums to +0 here too); no contraction into fma. Argmax partial per (token, 32-row tile), as k_lm_head_b.
+// Replaces the 3-6 token GEMV (one block row for every token: 63.8 us per launch at 6 tokens) and the two-row-pass
+// 2-token GEMV.
+constexpr int LMS_PER_CU = 3;
+constexpr int LMS_BLOCKS = 256 * LMS_PER_CU;
+constexpr int LMS_STEPS = 8;  // tiles per block at most (151936 rows: 4748 tiles over 768 blocks = 7)
+int g_lm_head_s = 1;  // FUNASR_LM_HEAD_S: 0 the GEMV forms; 1 k_lm_head_s<1>; 2 k_lm_head_s<2> (A/B)
+int g_lm_head_s1 = 0;  // FUNASR_LM_HEAD_S1: the batch-1 fused decode's LM head on k_lm_head_s too (1 / 2 = PF; A/B)
+
+// PF = weight tiles in flight per wave (1: the next tile's loads go out when the current one lands; 2: two ahead, in
+// registers, clamped to the last tile so every load is unconditional). PS (M = 1, the fused decode's LM head): the row
+// is first completed as x + psum[0] + ... + psum[7], as k_gemv_q8<PS> does.
+template <int PF, bool PS>
+__global__ __launch_bounds__(256, LMS_PER_CU) void k_lm_head_s(GemvArgs a) {
+#pragma clang fp contract(off)
+  constexpr int K = 1024, NB = K / 32, NBW = 8, WLD = 256 + 16, PERB = 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
+  const int bw0 = wave * NBW;
+  const int M = PS ? 1 : a.M;  // 1 .. 8 (host-checked)
+  const int n_tiles = (a.O + 31) >> 5;
+  __shared__ __attribute__((aligned(16))) int8_t s_w[4][32 * WLD];  // per wave: its K quarter of the tile's 32 rows
+  // the token rows (prologue) and, once they are in registers, the per-tile wave partials [parity][wave][reg][lane]
+  __shared__ __attribute__((aligned(16))) int8_t s_qr[8 * K];
+  __shared__ __attribute__((aligned(16))) float s_dT[NB][8];  // [block][token]: d_x
+  __shared__ float s_d[8 * NB];
+  __shared__ float s_nred[8][4];
+  // the landed scales pass through LDS like the weights (a register copy of a loop-carried load would make the loop
+  // latch wait for every load in flight)
+  __shared__ __attribute__((aligned(16))) uint4 s_sl[4][64];
+  auto load_tile = [&](int tile, i32x4_t (&W)[NBW], uint4& sl) {
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      const int row = min(tile * 32 + 4 * i + (lane >> 4), a.O - 1);
+      W[i] = __builtin_nontemporal_load(
+          reinterpret_cast<const i32x4_t*>(a.wq + (int64_t)row * K + bw0 * 32 + 16 * (lane & 15)));
+    }
+    sl = *reinterpret_cast<const uint4*>(a.wd + (int64_t)min(tile * 32 + n, a.O - 1) * NB + bw0);
+  };
+  // activations first (the whole block waits on them), then the first weight tile(s), then the prologue math
+  constexpr int MX = PS ? 1 : 8;
+  float xv[MX][PERB], xw[PERB];
+  float pv[PS ? FUSED_PARTS : 1][PERB];
+  if constexpr (PS) {
+#pragma unroll
+    for (int g = 0; g < FUSED_PARTS; ++g) {
+      const float4 f = *reinterpret_cast<const float4*>(a.psum + g * 1024 + threadIdx.x * PERB);
+      pv[g][0] = f.x; pv[g][1] = f.y; pv[g][2] = f.z; pv[g][3] = f.w;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MX; ++m) {
+    const float4 f = *reinterpret_cast<const float4*>(a.x + (int64_t)min(m, M - 1) * a.ldx + threadIdx.x * PERB);
+    xv[m][0] = f.x; xv[m][1] = f.y; xv[m][2] = f.z; xv[m][3] = f.w;
+  }
+  {
+    const float4 g = *reinterpret_cast<const float4*>((a.norm_w ? a.norm_w : a.x) + threadIdx.x * PERB);
+    xw[0] = g.x; xw[1] = g.y; xw[2] = g.z; xw[3] = g.w;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  i32x4_t W0[NBW], W1[NBW];
+  uint4 sl0, sl1;
+  int tile = blockIdx.x;  // < n_tiles: the host launches at most one block per tile
+  load_tile(tile, W0, sl0);  // (no branch: the wait-count pass would drain these loads at the join)
+  if constexpr (PF == 2) load_tile(tile + (int)gridDim.x < n_tiles ? tile + (int)gridDim.x : tile, W1, sl1);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PS) {
+#pragma unroll
+    for (int j = 0; j < PERB; ++j) {
+      float v = xv[0][j];
+#pragma unroll
+      for (int g = 0; g < FUSED_PARTS; ++g) v = v + pv[g][j];
+      xv[0][j] = v;
+    }
+    if (a.xsum && blockIdx.x == 0)
+      *reinterpret_cast<float4*>(a.xsum + threadIdx.x * PERB) = make_float4(xv[0][0], xv[0][1], xv[0][2], xv[0][3]);
+  }
+#pragma unroll
+  for (int m = 0; m < MX; ++m) {
+    if (m < M) {  // block-uniform
+      float v[PERB];
+#pragma unroll
+      for (int j = 0; j < PERB; ++j) v[j] = xv[m][j];
+      norm_quant_block_regs<PERB>(v, xw, a.norm_w != nullptr, a.eps, K, s_qr + m * K, s_d + m * NB, s_nred[m]);
+    }
+  }
+  __syncthreads();
+  i32x4_t A[NBW];  // lane: token row min(n, M - 1) (rows past M: a copy, never stored), K bytes 16 h of each block
+  {
+    const int8_t* xb = s_qr + min(n, M - 1) * K + bw0 * 32 + 16 * h;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) A[j] = *reinterpret_cast<const i32x4_t*>(xb + j * 32);
+    const int b = threadIdx.x >> 3, t = threadIdx.x & 7;
+    s_dT[b][t] = s_d[min(t, M - 1) * NB + b];
+  }
+  __syncthreads();  // s_qr becomes the partials buffer
+  float* s_red = reinterpret_cast<float*>(s_qr);  // [2][4][4][64]
+  int8_t* sw = s_w[wave];
+  const i32x16_t zero = {};
+  auto step = [&](int tile, int par, i32x4_t (&W)[NBW], uint4& sl) {
+    const int o0 = tile * 32;
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+      *reinterpret_cast<i32x4_t*>(sw + (4 * i + (lane >> 4)) * WLD + 16 * (lane & 15)) = W[i];
+    s_sl[wave][lane] = sl;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the tile PF steps ahead, or (past the end) this tile again: unconditional loads keep the wait counts exact
+    const int nxt = tile + PF * (int)gridDim.x;
+    load_tile(nxt < n_tiles ? nxt : tile, W, sl);
+    const uint4 cs = s_sl[wave][lane];
+    const uint32_t pr[4] = {cs.x, cs.y, cs.z, cs.w};
+    f32x2_t t1[2], t2[2], t3[2];  // tree levels (pairs, quads, the wave's eight blocks), tokens (0, 1) / (2, 3)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const i32x4_t Bj = *reinterpret_cast<const i32x4_t*>(sw + n * WLD + 32 * j + 16 * h);
+      const i32x16_t D = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[j], Bj, zero, 0, 0, 0);
+      const float dw = __half2float(reinterpret_cast<const __half*>(&pr[j >> 1])[j & 1]);
+      const float4 dx = *reinterpret_cast<const float4*>(&s_dT[bw0 + j][4 * h]);
+      f32x2_t b[2];
+      b[0] = f32x2_t{(float)D[0], (float)D[1]} * (f32x2_t{dw, dw} * f32x2_t{dx.x, dx.y});
+      b[1] = f32x2_t{(float)D[2], (float)D[3]} * (f32x2_t{dw, dw} * f32x2_t{dx.z, dx.w});
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if ((j & 1) == 0) {
+          t1[q] = b[q];
+        } else {
+          const f32x2_t p = (t1[q] + b[q]) + f32x2_t{0.f, 0.f};
+          if ((j & 3) == 1) {
+            t2[q] = p;
+          } else {
+            const f32x2_t p2 = t2[q] + p;
+            if (j == 3) t3[q] = p2;
+            else t3[q] = t3[q] + p2;
+          }
+        }
+      }
+    }
+    float* rp = s_red + ((par * 4 + wave) * 4) * 64;
+    rp[0 * 64 + lane] = t3[0][0];
+    rp[1 * 64 + lane] = t3[0][1];
+    rp[2 * 64 + lane] = t3[1][0];
+    rp[3 * 64 + lane] = t3[1][1];
+    __syncthreads();
+    {  // thread: token t = tid >> 5, row o0 + (tid & 31): (w0 + w1) + (w2 + w3), logit out, argmax over the 32 rows
+      const int t = threadIdx.x >> 5, rr = threadIdx.x & 31, g = t & 3, ln = rr + 32 * (t >> 2);
+      const float* r0 = s_red + (par * 4) * 4 * 64 + g * 64 + ln;
+      const float y = (r0[0] + r0[256]) + (r0[512] + r0[768]);
+      const int row = o0 + rr;
+      if (t < M && row < a.O) a.out[(int64_t)t * a.ldo + row] = y;
+      float bv = row < a.O ? y : -INFINITY;
+      int bi = row;
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        argmax_combine(bv, bi, ov, oi);
+      }
+      if (rr == 0 && t < M) {
+        a.pval[(int64_t)t * a.n_part + tile] = bv;
+        a.pidx[(int64_t)t * a.n_part + tile] = bi;
+      }
+    }
+  };
+  // at most LMS_STEPS tiles per block (host-checked), unrolled: with a loop back-edge the wait-count pass merges the
+  // in-flight loads of both register sets and waits for all of them at the loop head
+#pragma unroll
+  for (int it = 0; it < LMS_STEPS; ++it) {
+    const int tl = tile + it * (int)gridDim.x;
+    if (tl >= n_tiles) break;
+    if (PF == 1 || (it & 1) == 0) step(tl, it & 1, W0, sl0);
+    else step(tl, it & 1, W1, sl1);
+  }
+}
+
 // Same GEMM with K split over the NW waves of ONE block instead of over blocks: no cross-block split-K hop (on
 // this chip an in-launch hand-off costs about a kernel boundary: scripts/ubench/edge_chain.hip), and every wave
 // issues ALL its loads (NBW q8_0 blocks of weights and activations, their scales) before its MFMAs, so a tile
@@ -1622,6 +1804,11 @@ int g_gemv_mt = 2;
 int g_lm_head_mt6 = 1;  // LM head of 3-6 token batches: one block row for every token (FUNASR_LM_HEAD_MT6=0: pairs)
 
 bool gemv_small(int M) { return M <= g_gemv_small_max; }
+// the small-batch MFMA LM head (k_lm_head_s) takes 2-8 tokens of the fused decode path at K = 1024
+static bool lm_head_s_takes(int M, int K, int O) {
+  return K == 1024 && gemv_small(M) && cdiv(O, 32) <= LMS_STEPS * LMS_BLOCKS &&
+         ((g_lm_head_s && M >= 2 && M <= 8) || (g_lm_head_s1 && M == 1));
+}
 
 template <int MT>
 static void launch_gemv_fused(int K, int epi, const GemvArgs& a, hipStream_t s) {
@@ -1637,12 +1824,27 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   const bool fused = a.x != nullptr && a.ssp == nullptr;
   if (a.psum) {  // fused decode layer (M = 1): q|k|v (EPI 0) or the LM head (EPI 3) after a split down projection
     FA_REQUIRE(fused && a.M == 1 && K == 1024 && (epi == 0 || epi == 3), "gemv_q8: partial-sum prologue shape");
-    if (epi == 0) launch_gemv<1, 1, true, 0, true>(a, s);
-    else launch_gemv<1, 1, true, 3, true>(a, s);
+    if (epi == 0) {
+      launch_gemv<1, 1, true, 0, true>(a, s);
+    } else if (lm_head_s_takes(1, K, a.O)) {  // (n_part: lm_head_parts counts the tiles then)
+      const dim3 grid(std::min(cdiv(a.O, 32), LMS_BLOCKS));
+      FA_REQUIRE(cdiv(a.O, 32) <= LMS_STEPS * (int)grid.x && a.norm_w, "lm_head_s: vocabulary too large / no norm");
+      if (g_lm_head_s1 == 2) hipLaunchKernelGGL((k_lm_head_s<2, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_lm_head_s<1, true>), grid, dim3(256), 0, s, a);
+    } else {
+      launch_gemv<1, 1, true, 3, true>(a, s);
+    }
     return;
   }
   if (gemv_small(a.M) && fused) {
-    FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemv_q8: n_part");
+    FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M, K), "gemv_q8: n_part");
+    if (epi == 3 && lm_head_s_takes(a.M, K, a.O)) {
+      const dim3 grid(std::min(cdiv(a.O, 32), LMS_BLOCKS));
+      FA_REQUIRE(cdiv(a.O, 32) <= LMS_STEPS * (int)grid.x && a.norm_w, "lm_head_s: vocabulary too large / no norm");
+      if ((a.M == 1 ? g_lm_head_s1 : g_lm_head_s) == 2) hipLaunchKernelGGL((k_lm_head_s<2, false>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_lm_head_s<1, false>), grid, dim3(256), 0, s, a);
+      return;
+    }
     // decode path: MT tokens per block row (the block's weight rows are streamed once for its MT tokens). The LM head
     // (165 MB of rows) takes all of a 3-6 token batch in one block row: re-streaming it per token pair cost 86 us per
     // launch at 6 tokens. A token's arithmetic does not depend on MT (compute_group runs it per token).
@@ -1662,7 +1864,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     return;
   }
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
-  FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M), "gemm_q8: n_part");
+  FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M, K), "gemm_q8: n_part");
   if (epi == 3 && K == 1024 && a.M <= 32 && g_lm_head_b) {  // batched LM head: persistent tile loop
     const int nblk = std::min(cdiv(a.O, 32), LMB_BLOCKS);
     if (a.ssp) hipLaunchKernelGGL(k_lm_head_b<true>, dim3(nblk), dim3(256), 0, s, a);
@@ -1767,8 +1969,10 @@ bool gemm_q8_gu_down(const GemvArgs& g0, const GemvArgs& d0, unsigned* cnt, int*
   }
 }
 
-int lm_head_parts(int O, int M) { return gemv_small(M) ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32); }
-int lm_head_chunk(int O, int M) { return gemv_small(M) ? gemv_rows_per_wave(O) : 32; }
+int lm_head_parts(int O, int M, int K) {
+  return gemv_small(M) && !lm_head_s_takes(M, K, O) ? cdiv(O, 4 * gemv_rows_per_wave(O)) * 4 : cdiv(O, 32);
+}
+int lm_head_chunk(int O, int M, int K) { return gemv_small(M) && !lm_head_s_takes(M, K, O) ? gemv_rows_per_wave(O) : 32; }
 
 // ------------------------------------------------------------------------------------------------
 // q/k RMSNorm per head (attn_q_norm/attn_k_norm) + NEOX RoPE + KV-cache store (fp16).

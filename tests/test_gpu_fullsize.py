@@ -376,6 +376,27 @@ def test_llm_full_invariant_width_batch_equals_single(eng, g60):
         assert [t[s] for t in toks] == single[s][0], f"seq {s}: tokens differ from decoding it alone"
 
 
+@pytest.mark.parametrize("M", [2, 3, 5])
+def test_llm_full_small_batch_lm_head_equals_single(eng, g60, M):
+    """Batches of 2-5 full-dims sequences (the 151936-row LM head on k_lm_head_s, the small-batch MFMA form whose
+    every logit sums in the batch-1 GEMV's order) give bit-identical logits and tokens to each sequence decoded alone
+    (width 6 is test_llm_full_invariant_width_batch_equals_single)."""
+    from fun_asr_gguf.core.decoder import prefill_group
+    prompts = _bench_prompts(eng, g60["adaptor"].astype(np.float32), M)
+    K = 4
+    single = _single_runs(eng, prompts, K)
+    seqs = [2 * i + 1 for i in range(M)]  # non-contiguous slots
+    for s in seqs:
+        eng.llm_reset(s)
+    firsts = prefill_group(eng, seqs, prompts, dict(temperature=0.0))
+    assert list(firsts) == [single[i][0][0] for i in range(M)]
+    for k in range(K):
+        toks = [int(t) for t in eng.llm_generate(seqs, 1)[:, 0]]
+        for i, s in enumerate(seqs):
+            assert toks[i] == single[i][0][k + 1], f"M={M} seq {i} step {k}: token differs from alone"
+            assert np.array_equal(eng.llm_logits(s), single[i][1][k + 1]), f"M={M} seq {i} step {k}: logits differ"
+
+
 def test_llm_full_batch32_vs_single_streams_bound(eng, g60):
     """Above the invariant width (configs[2]: 32 streams at M = 32 on the int8 MFMA GEMMs with producer-side
     quantisation and the batched LM head, prefilled as one 6528-row batch) a stream's logits differ from decoding it
