@@ -1764,6 +1764,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_lm_head_s = g ? std::min(2, std::max(0, atoi(g))) : 1;
       const char* g1 = getenv("FUNASR_LM_HEAD_S1");
       fa::g_lm_head_s1 = g1 ? std::min(2, std::max(0, atoi(g1))) : 0;
+      const char* g2 = getenv("FUNASR_LM_GRID");
+      fa::g_lm_grid = g2 ? std::max(0, atoi(g2)) : 0;
     }
     if (const char* g = getenv("FUNASR_STEP_MASK")) e->step_mask = atoi(g) & 15;
     if (const char* g = getenv("FUNASR_GRAPH_SYNC_EVERY")) e->graph_sync_every = std::max(0, atoi(g));

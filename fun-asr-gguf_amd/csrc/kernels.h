@@ -181,6 +181,7 @@ extern int g_gemv_mt;         // tokens per fused-GEMV block from M = 3 on (defa
 bool gemv_small(int M);
 extern int g_gemm_q8_kw;  // 1 (default): K-in-block int8 MFMA GEMM where instantiated; 0: split-K block kernel
 extern int g_lm_head_s;     // LM head of 2-8 tokens (fused decode path) on k_lm_head_s (bit-identical to batch 1): 0 off, 1/2 = PF
+extern int g_lm_grid;       // blocks of the persistent LM-head launches (0: all resident)
 extern int g_lm_head_s1;    // ... and of one token (0: the GEMV)
 extern int g_lm_head_b;     // 1: batched LM head on the persistent tile loop (k_lm_head_b); 0: split-K block kernel
 extern int g_gemm_t_min_m;  // token count from which the 128x128-tile int8 GEMM runs (prefill batches; default 512)

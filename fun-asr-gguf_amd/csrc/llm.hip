@@ -1198,6 +1198,7 @@ constexpr int LMS_PER_CU = 3;
 constexpr int LMS_BLOCKS = 256 * LMS_PER_CU;
 constexpr int LMS_STEPS = 8;  // tiles per block at most (151936 rows: 4748 tiles over 768 blocks = 7)
 int g_lm_head_s = 1;  // FUNASR_LM_HEAD_S: 0 the GEMV forms; 1 k_lm_head_s<1>; 2 k_lm_head_s<2> (A/B)
+int g_lm_grid = 0;  // FUNASR_LM_GRID: blocks of the persistent LM-head launches (0: every block resident; A/B)
 int g_lm_head_s1 = 0;  // FUNASR_LM_HEAD_S1: the batch-1 fused decode's LM head on k_lm_head_s too (1 / 2 = PF; A/B)
 
 // PF = weight tiles in flight per wave (1: the next tile's loads go out when the current one lands; 2: two ahead, in
@@ -1827,7 +1828,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
     if (epi == 0) {
       launch_gemv<1, 1, true, 0, true>(a, s);
     } else if (lm_head_s_takes(1, K, a.O)) {  // (n_part: lm_head_parts counts the tiles then)
-      const dim3 grid(std::min(cdiv(a.O, 32), LMS_BLOCKS));
+      const dim3 grid(std::min(cdiv(a.O, 32), g_lm_grid > 0 ? std::min(g_lm_grid, LMS_BLOCKS) : LMS_BLOCKS));
       FA_REQUIRE(cdiv(a.O, 32) <= LMS_STEPS * (int)grid.x && a.norm_w, "lm_head_s: vocabulary too large / no norm");
       if (g_lm_head_s1 == 2) hipLaunchKernelGGL((k_lm_head_s<2, true>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((k_lm_head_s<1, true>), grid, dim3(256), 0, s, a);
@@ -1839,7 +1840,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   if (gemv_small(a.M) && fused) {
     FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M, K), "gemv_q8: n_part");
     if (epi == 3 && lm_head_s_takes(a.M, K, a.O)) {
-      const dim3 grid(std::min(cdiv(a.O, 32), LMS_BLOCKS));
+      const dim3 grid(std::min(cdiv(a.O, 32), g_lm_grid > 0 ? std::min(g_lm_grid, LMS_BLOCKS) : LMS_BLOCKS));
       FA_REQUIRE(cdiv(a.O, 32) <= LMS_STEPS * (int)grid.x && a.norm_w, "lm_head_s: vocabulary too large / no norm");
       if ((a.M == 1 ? g_lm_head_s1 : g_lm_head_s) == 2) hipLaunchKernelGGL((k_lm_head_s<2, false>), grid, dim3(256), 0, s, a);
       else hipLaunchKernelGGL((k_lm_head_s<1, false>), grid, dim3(256), 0, s, a);
@@ -1866,7 +1867,7 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   FA_REQUIRE(K % 1024 == 0 && K <= 3072, "gemm_q8: K must be 1024/2048/3072");
   FA_REQUIRE(epi != 3 || a.n_part == lm_head_parts(a.O, a.M, K), "gemm_q8: n_part");
   if (epi == 3 && K == 1024 && a.M <= 32 && g_lm_head_b) {  // batched LM head: persistent tile loop
-    const int nblk = std::min(cdiv(a.O, 32), LMB_BLOCKS);
+    const int nblk = std::min(cdiv(a.O, 32), g_lm_grid > 0 ? std::min(g_lm_grid, LMB_BLOCKS) : LMB_BLOCKS);
     if (a.ssp) hipLaunchKernelGGL(k_lm_head_b<true>, dim3(nblk), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_lm_head_b<false>, dim3(nblk), dim3(256), 0, s, a);
     return;
