@@ -1772,7 +1772,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GRAPH_STEPS")) e->graph_steps = std::min(64, std::max(1, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_DECODE")) e->use_fused = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FUSED_MAX_M")) e->fused_max_m = std::min(fa::FUSED_MAX_M, std::max(1, atoi(g)));
-    fa::g_ffn_pair_min_m = 4;
+    fa::g_ffn_pair_min_m = 2;
     fa::g_gemm_bf3_pf = 2;
     if (const char* g = getenv("FUNASR_BF3_PF")) fa::g_gemm_bf3_pf = atoi(g) >= 2 ? 2 : 1;
     // 256x256 bf16x3 tiles from 192 tiles per launch (batched encoder; bit-identical outputs): scripts/ubench/

@@ -260,7 +260,7 @@ void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq,
                hipStream_t s, int M = 1);
 extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
 extern int g_gemm_bf3_256;    // bf16x3 GEMMs: 256x256 tiles when a launch has at least this many (0 = off)
-extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 4)
+extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 2)
 // out[m] = xmid[m] + sum_p dpart[m][p] for m < M (a small batch's residual rows after its last fused layer)
 void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);
 // dst[i] = src[rows[i]] (n rows of E floats; row stride E both sides)

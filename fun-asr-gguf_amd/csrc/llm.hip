@@ -4185,7 +4185,9 @@ void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, 
   hipLaunchKernelGGL(k_psum_rows, dim3(cdiv(E / 4, 256), M), dim3(256), 0, s, xmid, dpart, E, out);
 }
 
-int g_ffn_pair_min_m = 4;  // decode batches from this width run the fused FFN with two tokens per block
+int g_ffn_pair_min_m = 2;  // decode batches from this width run the fused FFN with two tokens per block (round 5,
+// profiles/r05_exp_ffn_pairs.txt: graph-replayed steps, pairs vs one token per block, bit-identical: M = 2 0.530-0.538
+// vs 0.541 ms, M = 4 0.672 vs 0.727, M = 6 0.885-0.894 vs 0.974; the threshold was 4)
 // (three tokens per block, tried in round 4: 184 VGPRs, 2 blocks per CU; at batches 3-6 the in-launch fan-ins timed out
 // and every chunk fell back to the 5-launch layer: not kept)
 
