@@ -1806,8 +1806,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_l2pf_blocks = g ? std::min(64, std::max(0, atoi(g))) : 16;
       const char* d = getenv("FUNASR_L2PF_DELAY");
       fa::g_l2pf_delay = d ? std::max(0, atoi(d)) : 50;
-      const char* mm = getenv("FUNASR_L2PF_MAX_M");
-      fa::g_l2pf_max_m = mm ? std::max(1, atoi(mm)) : 1;
+      const char* mm = getenv("FUNASR_L2PF_MAX_M");  // set: one mask for every batch up to it (A/B); unset: the table
+      fa::g_l2pf_max_m = mm ? std::max(1, atoi(mm)) : 0;
       const char* k = getenv("FUNASR_L2PF_MASK");
       fa::g_l2pf_mask = k ? atoi(k) & 7 : 7;
     }

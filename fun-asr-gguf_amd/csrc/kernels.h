@@ -239,7 +239,7 @@ struct L2Prefetch {
   int F = 0;
 };
 extern int g_l2pf_blocks;  // L2 prefetch blocks per kv head in the two-launch attention launch (0 = off, <= 16)
-extern int g_l2pf_max_m;   // ... for decode batches up to this width
+extern int g_l2pf_max_m;   // > 0 (A/B): ... with g_l2pf_mask for decode batches up to this width (0: per-batch table)
 extern int g_l2pf_delay;   // their start delay, ticks of the 100 MHz clock
 extern int g_l2pf_mask;    // A/B: which byte sets they pull (1 FFN weights, 2 next attention weights, 4 next K/V)
 void attn_o_fused(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,

@@ -3550,7 +3550,13 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
 
 int g_l2pf_blocks = 16;
 int g_l2pf_delay = 50;
-int g_l2pf_max_m = 1;
+int g_l2pf_max_m = 0;  // > 0 (A/B): the slabs with g_l2pf_mask at every batch up to this width; 0: l2pf_small_mask
+// Small decode batches (two-launch layer, M = 2-6, one grid slab per token): which prefetch families pay off depends on
+// the batch (scripts/gpu_r5_pfm.sh, profiles/r05_exp_l2pf_small_batches.txt, graph-replayed steps, mask 1 the FFN
+// weights, 2 the next layer's q|k|v / o weights, 4 its K/V rows): M = 2 none (0.535 vs 0.568-0.580 ms), 3 mask 3 (0.635
+// vs 0.645-0.657), 4 none (0.670-0.678 vs 0.699-0.736), 5 mask 3 (0.778 vs 0.864-0.868), 6 mask 3 (0.860 vs
+// 0.902-0.904); the K/V family (4) loses at every M > 1 (it loops over the batch's sequences)
+static const int l2pf_small_mask[FUSED_MAX_M + 1] = {0, 7, 0, 3, 0, 3, 3, 0, 0};  // M = 7, 8: not measured
 int g_l2pf_mask = 7;
 
 // L2 prefetch blocks of the two-launch layer (the last z slab of k_attn_o<true>, after the M token slabs: block
@@ -3959,14 +3965,15 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
   FA_REQUIRE(!FA_QKV_GRANULE || fw.gqkv, "qkv_attn_o_fused: granule workspace");
   FA_REQUIRE(!FA_PART_GRANULE || fw.gpart, "qkv_attn_o_fused: partial granule workspace");
   int nz = M;
-  if (pf && M <= g_l2pf_max_m && g_l2pf_blocks > 0) {
+  const int pf_mask = g_l2pf_max_m > 0 ? (M <= g_l2pf_max_m ? g_l2pf_mask : 0) : M == 1 ? g_l2pf_mask : l2pf_small_mask[M];
+  if (pf && pf_mask && g_l2pf_blocks > 0) {
     FA_REQUIRE(pf->F == 3072 && pf->gq && pf->uq && pf->dq && pf->gd && pf->ud && pf->dd &&
                    (!pf->qkv_q || (pf->qkv_d && pf->o_q && pf->o_d && pf->kc && pf->vc)),
                "qkv_attn_o_fused: L2 prefetch set");
     a.pf = *pf;
     a.pf_blocks = std::min(g_l2pf_blocks, ASPLIT);
     a.pf_delay = g_l2pf_delay;
-    a.pf_mask = g_l2pf_mask;
+    a.pf_mask = pf_mask;
     nz += 1;
   }
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, nz), dim3(AWV * 64), 0, s, a);
