@@ -107,7 +107,6 @@ __device__ __forceinline__ void st_sc1_f4(f32x4_t v, __amdgpu_buffer_rsrc_t rs, 
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4v_t, v), rs, byte_off, 0, CPOL_SC1);
 }
 
-// (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).
 // bf16x3 encoder activations handed between kernels as their two bf16 planes (APlanes in kernels.h): hi = bf16_rn(v),
 // lo = bf16_rn(v - hi), exactly the split the bf16x3 GEMM's staging applies to an f32 A row
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -125,6 +124,7 @@ __device__ __forceinline__ void split_bf16(const float v, __bf16& h, __bf16& l) 
   l = (__bf16)(v - (float)h);
 }
 
+// (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).
 __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i) || (v != v)) {
     v = v2;

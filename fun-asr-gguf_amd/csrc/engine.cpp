@@ -403,7 +403,33 @@ struct Engine {
     FA_REQUIRE(it != wb.end(), "bf16x3 encoder: GEMM weight without a split copy");
     return it->second;
   }
-  void weights_changed() { w16_stale = wb_stale = true; }
+  void weights_changed() { w16_stale = wb_stale = qn_stale = true; }
+
+  // The f16-MFMA prefill attention (k_attn_prefill_h) holds q * D^-0.5 * 2^8 as f16 hi + lo. After the q RMSNorm
+  // every |x_i| <= sqrt(D), so |q_i| <= max|q_norm| * sqrt(D), and RoPE rotates pairs (|q'| <= max|q_norm| * sqrt(D)
+  // as well): the f16 image stays finite while max|q_norm| * 256 (D = 128, scale D^-0.5) is below 65504 with margin.
+  // Above that (a q_norm weight > ~234) the prefill attention runs the exact-f32 MFMA kernel (k_attn_prefill), and
+  // row-local forwards take the per-row path. Checked lazily after every weight change.
+  bool qn_stale = true, qn_f16_safe = true;
+  bool prefill_attn_f16() {
+    if (!fa::g_attn_pf_f16) return false;
+    if (qn_stale && !layers.empty()) {
+      const int D = lc.head_dim;
+      std::vector<float> h(D);
+      float mx = 0.f;
+      for (const LlmLayerW& w : layers) {
+        FA_HIP(hipMemcpy(h.data(), w.q_norm, D * 4, hipMemcpyDeviceToHost));
+        for (float v : h) mx = std::max(mx, std::isfinite(v) ? std::fabs(v) : INFINITY);
+      }
+      const bool ok = mx * std::sqrt((float)D) * (1.0f / std::sqrt(128.0f)) * 256.0f < 60000.0f;  // kernel: D = 128
+      if (!ok && qn_f16_safe)
+        log(2, "prefill attention: max|q_norm| = " + std::to_string(mx) +
+                   " would overflow the f16 query image; using the exact-f32 MFMA prefill attention");
+      qn_f16_safe = ok;
+      qn_stale = false;
+    }
+    return qn_f16_safe;
+  }
 
   // ---- int8-dynamic CTC graph (Fun-ASR-Nano-CTC.int8.onnx, the reference README's default CTC model: 02-Quantize-ONNX.py
   // :38-46): every CTC-graph linear with an ORT dynamic-quant weight (fa_set_tensor_u8dq) runs DynamicQuantizeLinear +
@@ -1202,12 +1228,14 @@ struct Engine {
   // prefill rows -> query tiles of <= 64 consecutive positions of one sequence (uploaded on the stream; host copy
   // kept in h_ptiles until the next call). Below attn_pf_min_m rows (or head dim != 128) the per-row path runs.
   std::vector<int4> h_ptiles;
+  bool ptiles_f16 = true;  // the tiles run k_attn_prefill_h (prefill_attn_f16), else k_attn_prefill
   // rl (row-local forward): tiles at every row count (a threshold on the call's rows would give a prompt other
   // arithmetic alone than in a batch), on the f16-MFMA tile kernel only: a row's result there depends on its own keys
   // alone (fully masked key tiles add exact zeros, rescale by exactly 1), so the forward stays row-local
   void set_prefill_tiles(const int* sq, const int* ps, int rows, bool rl = false) {
     n_ptiles = 0;
-    if (rl ? (!fa::g_attn_pf_f16 || !attn_pf_rl) : rows < attn_pf_min_m) return;
+    ptiles_f16 = prefill_attn_f16();
+    if (rl ? (!ptiles_f16 || !attn_pf_rl) : rows < attn_pf_min_m) return;
     if (lc.head_dim != 128 || lc.n_head != 2 * lc.n_head_kv) return;
     h_ptiles.clear();
     for (int r = 0; r < rows; ++r) {
@@ -1233,7 +1261,7 @@ struct Engine {
     // batched decode: the residual GEMMs (o, down) quantise their new rows times the next RMSNorm weight and leave
     // per-token sum-of-squares partials; q|k|v, gate|up and the LM head apply rstd to those rows' block scales
     // (no k_prep_q8 launches but layer 0's)
-    const bool fused = decode && fused_shape_ok() && ((M == 1 && use_fused) || (M <= fused_max_m && use_fused == 1));
+    const bool fused = decode && fused_layer_runs(M);
     const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm && !fused;
 
     (void)max_pos;
@@ -1280,7 +1308,7 @@ struct Engine {
         // M > 4: the attention also leaves its rows as q8_0 blocks for the o GEMM (no prep launch)
         if (!decode && n_ptiles > 0)  // query tiles: each K/V tile serves 64 rows x 2 heads (set_prefill_tiles)
           attn_prefill(d_ptiles, n_ptiles, d_tok_pos, H, KV, seq_stride, kc, vc, lq, latt, small ? nullptr : lxq2,
-                       small ? nullptr : lxd2, stream);
+                       small ? nullptr : lxd2, stream, ptiles_f16);
         else
           attn_block(decode ? lqkv : lq, decode ? 1 : 0, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV,
                      d_tok_seq, d_tok_pos, seq_stride, latt, attn_wk, stream, small ? nullptr : lxq2,
@@ -1354,6 +1382,11 @@ struct Engine {
   int invariant_width() const {
     if (use_fused == 1 && fused_shape_ok()) return std::max(1, std::min(fused_max_m, fa::g_gemv_small_max));
     return 1;
+  }
+
+  // a decode step of M sequences runs on the fused layer (two- or three-launch); else on the 5-launch / batched layer
+  bool fused_layer_runs(int M) const {
+    return fused_shape_ok() && ((M == 1 && use_fused) || (M <= fused_max_m && use_fused == 1));
   }
 
   bool fused_shape_ok() const {
@@ -2398,8 +2431,12 @@ int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
   FA_HIP(hipEventSynchronize(e->ev_gen));
   const int n_seqs = (int)e->gen_seqs.size(), n_steps = e->gen_steps;
   e->prof_collect();
-  if (n_seqs <= fa::FUSED_MAX_M && e->fused_error()) e->recover_fused_chunk();
-  else if (n_seqs > fa::FUSED_MAX_M && e->use_gu_down && e->fused_error()) {
+  // the recovery follows the layer the chunk actually ran on (a batch of 7-8 with FUNASR_GU_DOWN=1 is above the fused
+  // width: its error flag can only come from the gate|up -> down hand-off)
+  if (e->fused_layer_runs(n_seqs)) {
+    if (e->fused_error()) e->recover_fused_chunk();
+    else e->fused_fail_streak = 0;  // a clean fused chunk ends a run of fallbacks ("three in a row", funasr_hip.h)
+  } else if (e->use_gu_down && e->fused_error()) {
     // a gate|up -> down hand-off timed out (not expected: the producers are dispatched first): two launches from now on
     fa::log(3, "batched decode: the gate|up -> down hand-off timed out; re-running the chunk with two launches");
     e->use_gu_down = false;

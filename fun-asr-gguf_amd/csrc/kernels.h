@@ -40,7 +40,7 @@ extern int g_gemm_t_wab;  // k_gemm_q8_t: 1 = write-after-barrier staging
 extern int g_attn_wab;  // k_attn_bf3: 1 = write-after-barrier K/V staging
 extern int g_gemm_bf3_256_s;  // 256x256 tile: 1 = write-after-barrier staging
 extern int g_gemm_bf3_persist;  // 256x256 tiles as persistent blocks, one per CU (A/B, default 0)
-extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gemm_bf3_256d; default 1)
+extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gemm_bf3_256d; default 0: measured slower)
 extern int g_gemm_f16_deep;  // fp16 one-clip GEMMs on 128-deep stages (default 1)
 extern int g_gemm_bf3_kw4;  // 1: four K groups per block for few-tile K >= 2048 shapes (FUNASR_BF3_KW4)
 extern int g_gemm_bf3_mid;  // 1: 128x64 tiles for one clip's 256-1024-tile GEMM shapes (A/B, default 0)
@@ -201,8 +201,9 @@ struct AttnWork {
 };
 // Prefill over query tiles (multi-sequence batches): tiles[i] = {row0, n_rows <= 64, seq, 0}, rows of one sequence at
 // consecutive positions; q from qk_rope_store (head dim 128); out / qout / dout as attn_block's
+// f16: the f16-MFMA kernel (k_attn_prefill_h; the caller checks the q range, Engine::prefill_attn_f16), else exact f32
 void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int KV, int64_t seq_stride, const __half* kc,
-                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s);
+                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s, bool f16);
 // qout/dout (optional): the output rows also as q8_0 blocks (the o GEMM's pre-quantised input, no prep launch)
 void attn_block(const float* qsrc, int decode_mode, const float* qn, const float* kn, float eps, const float* rcos,
                 const float* rsin, __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,

@@ -706,7 +706,7 @@ __device__ __forceinline__ void gemm_l2_prefetch(const GemvArgs& a, int idx, int
 // Every in-launch wait is bounded by time, not spin count: SPIN_TICKS of the 100 MHz reference clock (10 ms) from
 // the first poll (checked every 16 polls). A group that is not co-resident (another kernel holding CUs) then costs a
 // few ms per wait instead of seconds; the timed-out block sets *err and falls through, and fa_llm_generate_end re-runs
-// the chunk on the 5-launch layer (engine.cpp, recover_fused_chunk).
+// the chunk on the fused layer first and only then on the 5-launch layer (engine.cpp, recover_fused_chunk).
 constexpr uint64_t SPIN_TICKS = 1000000;
 struct SpinDeadline {
   uint64_t t0 = 0;
@@ -2924,10 +2924,10 @@ __global__ __launch_bounds__(256, 2) void k_attn_prefill_h(const int4* __restric
 int g_attn_pf_f16 = 1;  // query-tiled prefill attention on f16 MFMAs (FUNASR_ATTN_PF_F16; 0: exact-f32 MFMAs)
 
 void attn_prefill(const int4* tiles, int n_tiles, const int* tok_pos, int H, int KV, int64_t seq_stride, const __half* kc,
-                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s) {
+                  const __half* vc, const float* q, float* out, int8_t* qout, float* dout, hipStream_t s, bool f16) {
   FA_REQUIRE(H == KV * GQ, "attn_prefill: n_head must be 2*n_head_kv");
   if (n_tiles <= 0) return;
-  hipLaunchKernelGGL(g_attn_pf_f16 ? k_attn_prefill_h : k_attn_prefill, dim3(n_tiles, KV), dim3(256), 0, s, tiles,
+  hipLaunchKernelGGL(f16 ? k_attn_prefill_h : k_attn_prefill, dim3(n_tiles, KV), dim3(256), 0, s, tiles,
                      tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, q, 1.0f / sqrtf(128.0f), out, qout, dout);
 }
 

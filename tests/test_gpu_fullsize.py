@@ -250,12 +250,42 @@ def test_sampler_full_vocab_membership(eng, cllm, g60):
             assert lg[t] >= v[n - 1]
 
 
-def test_c4_300s_long_audio_full_model(cenc):
+def _pin_segment_decode(api, cllm, prompt, seg_text, n_gen=253):
+    """One segment's decoder pinned token by token: its prompt rows (prefix | audio rows of the segment | suffix)
+    prefilled alone on the engine, then n_gen - 1 greedy steps. (a) The detokenised tokens equal the segment's text
+    from the public path (the batch gave it exactly its single-sequence arithmetic, DESIGN §1 batch invariance);
+    (b) the prefill logits and every step's logits, teacher-forced on the GPU's own tokens, pass the oracle's
+    per-step bar (cref at full dims: cosine >= 0.9995, argmax equal where its top-2 margin > 0.25)."""
+    from fun_asr_gguf.core.decoder import PieceStream
+    eng = api.models.engine
+    eng.llm_reset(0)
+    tok, lg = eng.llm_prefill(0, prompt, want_logits=True, temperature=0.0)
+    ref = cllm.forward(prompt, 0)
+    _check_step(lg, ref)
+    toks, pos, worst = [tok], prompt.shape[0], _cos(lg, ref)
+    for _ in range(n_gen - 1):
+        nxt = int(eng.llm_generate([0], 1, temperature=0.0)[0][0])
+        lg = eng.llm_logits(0)
+        ref = cllm.forward(cllm.embed_tokens([toks[-1]]), pos)
+        _check_step(lg, ref)
+        worst = min(worst, _cos(lg, ref))
+        toks.append(nxt)
+        pos += 1
+    ps = PieceStream(api.models.vocab)
+    for t in toks:
+        ps.push(t)
+    ps.flush()
+    assert ps.generated_text.strip() == seg_text
+    return worst
+
+
+def test_c4_300s_long_audio_full_model(cenc, cllm):
     """configs[3]: one 300 s file, segment 60 / overlap 4 -> 6 segments through the public transcribe() long path
     (one device batch), 253 greedy tokens per segment (pinned length). Pinned: the windows (oracle of
     orchestrator.py:123-136), every segment's CTC ids / audio rows against the oracle encoder on the unpadded
-    chunk, and the merged text + char timestamps = the reference merge rule (oracle.ctc.merge_results, pinned to
-    text_merge.py goldens) applied to the per-segment results."""
+    chunk, the merged text + char timestamps = the reference merge rule (oracle.ctc.merge_results, pinned to
+    text_merge.py goldens) applied to the per-segment results, and the decoded text of the first and the last
+    segment token by token against the oracle decoder (_pin_segment_decode: all 253 steps teacher-forced)."""
     from fun_asr_gguf import create_asr_engine
     from fun_asr_gguf.synthetic import synth_audio
     api = create_asr_engine("synthetic", "synthetic", "synthetic", "synthetic", verbose=False, model="full",
@@ -278,6 +308,85 @@ def test_c4_300s_long_audio_full_model(cenc):
             r = cenc.encode(c)
             _check_encoder(out["enc"][b], out["audio_embd"][b], out["ctc_ids"][b], r["enc"], r["audio_embd"],
                            r["ctc_ids"], r["ctc_margin"], f"segment {b}")
+        pe, se, n_p, n_s, _ = api.models.prompt_builder.build_prompt([], None, None)
+        assert all((d.n_prefix, d.n_suffix) == (n_p, n_s) for d in per)
+        for b in (0, 5):
+            prompt = np.concatenate([pe, per[b].audio_embd.astype(np.float32), se], 0)
+            worst = _pin_segment_decode(api, cllm, prompt, per[b].text)
+            print(f"C4 segment {b}: 253 steps teacher-forced, worst logits cosine {worst:.6f}")
+    finally:
+        api.cleanup()
+
+
+# configs[4]'s hotword / context prompt (bench.py C5_CONTEXT / C5_HOTWORDS)
+C5_CONTEXT = "这是一段关于人工智能的会议"
+C5_HOTWORDS = ["通义千问", "语音识别", "魔搭社区", "大模型"]
+
+
+def test_c5_300s_fp16_hotword_prompt_full_path(cllm):
+    """configs[4] end to end: the 300 s file through the public transcribe() long path with the fp16 encoder graph
+    (encoder_precision="fp16") and the hotword / context prompt. The prompt text comes from the reference's
+    prompt_texts (prompt_utils.py:16-54) for C5_HOTWORDS (supplied by a hotword source from the CTC text, the
+    reference's decoder.py:39-44 step) and C5_CONTEXT, tokenized by the product's GGUF tokenizer (fa_tokenize on the
+    synthetic Qwen2 BPE vocabulary: 73 prefix + 5 suffix tokens). Pinned:
+      * every segment's fp16 audio rows against oracle/encoder_fp16 on the unpadded chunk;
+      * the merged text + char timestamps = oracle.ctc.merge_results of the per-segment results;
+      * the first and last segments' decodes token by token against cref (_pin_segment_decode, 253 steps)."""
+    from fun_asr_gguf import create_asr_engine
+    from fun_asr_gguf.prompt_utils import prompt_texts
+    from fun_asr_gguf.synthetic import synth_audio
+    from fun_asr_gguf.vocab import GGUFVocab
+    from oracle import encoder_fp16 as oe16
+
+    class _C5Hotwords:  # the hotword source's interface (model_manager.match_hotwords)
+        def __init__(self):
+            self.texts = []
+
+        def hotwords_for(self, ctc_text, k):
+            self.texts.append(ctc_text)
+            return list(C5_HOTWORDS)[:k]
+
+    api = create_asr_engine("synthetic", "synthetic", "synthetic", "synthetic", verbose=False, model="full",
+                            max_batch=6, n_ctx=512, n_predict=253, ignore_eos=True, encoder_precision="fp16")
+    try:
+        m = api.models
+        vocab = GGUFVocab(os.path.join(GOLDEN, "tokenizer_qwen2_synth.gguf"))
+        m.prompt_builder.vocab = vocab  # prompt tokenisation only; the LLM's own ids detokenise on m.vocab
+        m.hotword_source = _C5Hotwords()
+        pt, st = prompt_texts(C5_HOTWORDS, None, C5_CONTEXT)
+        pre_ids, suf_ids = vocab.tokenize(pt), vocab.tokenize(st)
+        assert (len(pre_ids), len(suf_ids)) == (73, 5)
+        audio = synth_audio(300 * SR, 4000)
+        res = api.transcribe(audio, segment_size=60.0, overlap=4.0, context=C5_CONTEXT, temperature=0.0,
+                             verbose=False)
+        wins = octc.segments_info(300.0, 60.0, 4.0)
+        chunks = [audio[int(s * SR):int(e * SR)] for s, e in wins]
+        per = api.transcribe_batch(chunks, context=C5_CONTEXT, temperature=0.0)
+        assert len(m.hotword_source.texts) >= 12 and all(m.hotword_source.texts)  # CTC text reached the source
+        for d in per:
+            assert (d.n_prefix, d.n_suffix, d.n_gen) == (73, 5, 253) and list(d.hotwords) == C5_HOTWORDS
+        seg_results = [{"text": d.text, "segments": d.aligned or []} for d in per]
+        text, segs = octc.merge_results(seg_results, [s for s, _ in wins], 4.0)
+        assert res.text == text and len(text) > 0
+        assert [(c["char"], round(c["start"], 6)) for c in res.segments] == \
+               [(c["char"], round(c["start"], 6)) for c in segs]
+        W = synth.make_weights(synth.encoder_tensors(synth.ENC_FULL))
+        for b, c in enumerate(chunks):
+            r = oe16.encode(c, W, synth.ENC_FULL)
+            emb = per[b].audio_embd
+            assert emb.shape == r["audio_embd"].shape, b
+            assert (emb.astype(np.float16).astype(np.float32) == emb).all(), b
+            e, cs = _rel(emb, r["audio_embd"]), _cos(emb, r["audio_embd"])
+            print(f"C5 segment {b}: fp16 audio rows max-abs/max {e:.2e} cos {cs:.7f}")
+            assert e < 1e-2 and cs > 0.9999, b
+        del W
+        pe, se, n_p, n_s, _ = m.prompt_builder.build_prompt(C5_HOTWORDS, None, C5_CONTEXT)
+        assert (n_p, n_s) == (73, 5)
+        assert np.array_equal(pe, cllm.embed_prompt(pre_ids)) and np.array_equal(se, cllm.embed_prompt(suf_ids))
+        for b in (0, 5):
+            prompt = np.concatenate([pe, per[b].audio_embd.astype(np.float32), se], 0)
+            worst = _pin_segment_decode(api, cllm, prompt, per[b].text)
+            print(f"C5 segment {b}: 253 steps teacher-forced, worst logits cosine {worst:.6f}")
     finally:
         api.cleanup()
 

@@ -571,6 +571,47 @@ def test_llm_prefill_query_tiles_f16_mfma_vs_oracle(llm_tiny_oracle, monkeypatch
         e.close()
 
 
+def test_llm_prefill_large_q_norm_takes_exact_f32_attention(monkeypatch):
+    """The f16-MFMA prefill attention holds q * d^-0.5 * 2^8 as f16: a q_norm weight above ~234 could overflow it. The
+    engine bounds |q| by max|q_norm| * sqrt(head_dim) after every weight change and then runs the exact-f32 prefill
+    attention (tiled batches) and the per-row path (row-local prefill). With q_norm scaled to ~300 the default run
+    equals a FUNASR_ATTN_PF_F16=0 run bit for bit, its logits are finite, and they match the oracle teacher-forced."""
+    from fun_asr_gguf import _native
+    from oracle import qwen3 as oq
+    monkeypatch.setenv("FUNASR_ATTN_PREFILL_MIN_M", "8")
+    W = synth.make_weights(synth.llm_tensors(synth.LLM_TINY))
+    names = [n for n in W if n.endswith("attn_q_norm.weight")]
+    for n in names:
+        W[n] = (W[n] * 300.0).astype(np.float32)
+    m = oq.Qwen3Q8(W, synth.LLM_TINY, n_ctx=160)
+    rng = np.random.default_rng(45)
+    prompts = [m.embed_prompt(rng.integers(0, 4096, n)) for n in (70, 9, 40)]
+    runs = []
+    for f16 in ("1", "0"):
+        monkeypatch.setenv("FUNASR_ATTN_PF_F16", f16)
+        for fmax in ("6", "1"):  # row-local batch (invariant width 6), shared-forward tiles (width 1)
+            monkeypatch.setenv("FUNASR_FUSED_MAX_M", fmax)
+            e = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=160, max_seqs=3), max_batch=1,
+                               max_samples=16000)
+            try:
+                e.synthetic_weights(0)
+                for n in names:
+                    e.set_tensor(n, W[n])
+                for q in range(3):
+                    e.llm_reset(q)
+                e.llm_prefill_batch([0, 1, 2], prompts, temperature=0.0)
+                runs.append([e.llm_logits(q) for q in range(3)])
+            finally:
+                e.close()
+    for a, b in ((runs[0], runs[2]), (runs[1], runs[3])):
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    for r in runs[:2]:
+        assert all(np.isfinite(x).all() for x in r)
+        for q in (0, 2):
+            m.reset()
+            _check_step(r[q], m.forward(prompts[q], 0))
+
+
 def test_llm_generate_begin_end_equals_generate(llm_tiny_oracle):
     """fa_llm_generate_begin / _end (the host works while the chunk runs) give the tokens of fa_llm_generate, chunk
     after chunk, and the other LLM calls refuse while a chunk is in flight."""
@@ -793,7 +834,8 @@ def test_fused_timeout_recovery_keeps_fused_layer():
     re-runs the chunk on the fused layer from the same positions and tokens. The tokens and logits equal an undisturbed
     run, and the invariant width stays 6 (DESIGN §3 decode step). With bit 2 too the re-run times out as well: that
     chunk runs on the 5-launch layer (tokens and logits equal a 5-launch run of it), the next chunk is fused again, and
-    three such chunks in a row keep the 5-launch layer (width 1)."""
+    three such chunks in a row keep the 5-launch layer (width 1); a clean fused chunk between fallbacks resets that count
+    (fallback, clean, fallback, clean, fallback keeps width 6)."""
     from fun_asr_gguf import _native
     from oracle import qwen3 as oq
     cfg = dict(synth.LLM_TINY, n_ctx=256, max_seqs=2)
@@ -809,9 +851,10 @@ def test_fused_timeout_recovery_keeps_fused_layer():
             eng.llm_reset(0)
             first = eng.llm_prefill(0, prompt)
             toks = []
-            for c in range(chunks):
-                if debug:
-                    eng.lib.fa_set_debug(eng.h, debug)
+            sched = debug if isinstance(debug, list) else [debug] * chunks
+            for dbg in sched:  # per chunk: 0 undisturbed, else the fa_set_debug bits set before it
+                if dbg:
+                    eng.lib.fa_set_debug(eng.h, dbg)
                 toks += [int(t) for t in eng.llm_generate([0], 3)[0]]
             lg = eng.llm_logits(0)
             more = [int(t) for t in eng.llm_generate([0], 2)[0]]  # undisturbed chunk after the recovery
@@ -840,11 +883,15 @@ def test_fused_timeout_recovery_keeps_fused_layer():
     # three fallbacks in a row: the engine keeps the 5-launch layer
     *_, w3, r3 = run(debug=6, chunks=3)
     assert r3 == (3, 3) and w3 == 1, (r3, w3)
+    # ... but not with clean fused chunks between them (the count is of consecutive fallbacks)
+    *_, w4, r4 = run(debug=[6, 0, 6, 0, 6])
+    assert r4 == (3, 3) and w4 == 6, (r4, w4)
 
 
 def test_llm_prefill_batch_row_local_exact(llm_tiny_oracle):
     """Within the invariant width fa_llm_prefill_batch is row-local: every prompt gets exactly the arithmetic of its own
-    fa_llm_prefill (K-in-block GEMMs, one key split, no query tiles, never the row-count-dependent fused-GEMV path), so
+    fa_llm_prefill (K-in-block GEMMs, one key split, f16-MFMA query tiles whose rows depend only on their own keys,
+    never the row-count-dependent fused-GEMV path), so
     first tokens and logits are bit-identical, for short prompts (<= 6 rows) and for prompts continuing a cached prefix."""
     from fun_asr_gguf import _native
     m = llm_tiny_oracle
