@@ -187,6 +187,12 @@ struct Engine {
   unsigned* gd_cnt = nullptr;  // gemv_gu_down hand-off counters
   // batched decode: gate|up + down in one launch with a per-K-split hand-off (FUNASR_GU_DOWN; 0 = two launches, A/B)
   bool use_gu_down = false;  // measured: batch-32 step 1.216-1.218 vs 1.2085-1.209 ms (profiles/r05_exp_gu_down.txt)
+  // batched decode at M = 32: attention + o projection + residual + NRM epilogue in one launch (llm.hip k_attn_ob;
+  // FUNASR_ATTN_OB=1, A/B). Needs every one of its KV x 32 one-per-CU blocks resident (checked against the CU count).
+  // Measured slower (profiles/r06_exp_attn_ob.txt: graph-replayed batch-32 step 1.228-1.231 vs 1.154-1.158 ms): the two
+  // in-launch edges it adds (32-block head fan-in, cross-XCD head sum) cost more than the kernel boundary they replace
+  bool use_attn_ob = false;
+  fa::AttnObWork ob_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
   int* gk_cnt = nullptr;
   int64_t gk_part_n = 0, gk_cnt_n = 0;
@@ -867,6 +873,20 @@ struct Engine {
     FA_HIP(hipMemset(gd_cnt, 0, 64 * CNT_LINE * sizeof(unsigned)));
     FA_HIP(hipMemset(gk_cnt, 0, gk_cnt_n * CNT_LINE * sizeof(int)));
     gk_part = alloc<float>(gk_part_n);
+    if (lc.max_seqs >= 32) {  // k_attn_ob (M = 32): q8_0 attention rows in lxq2 / lxd2, tile partials, counters
+      ob_wk.aq = lxq2;
+      ob_wk.ad = lxd2;
+      ob_wk.opart = alloc<float>((size_t)32 * KV * 32 * 32);
+      ob_wk.cnt_g = alloc<unsigned>((size_t)(KV + 32) * CNT_LINE);
+      ob_wk.cnt_s = ob_wk.cnt_g + (size_t)KV * CNT_LINE;
+      FA_HIP(hipMemset(ob_wk.cnt_g, 0, (size_t)(KV + 32) * CNT_LINE * sizeof(unsigned)));
+      ob_wk.err = fdw.err;
+      hipDeviceProp_t prop;
+      FA_HIP(hipGetDeviceProperties(&prop, device));
+      if (prop.multiProcessorCount < KV * 32) use_attn_ob = false;  // one 16-wave block per CU, all resident
+    } else {
+      use_attn_ob = false;
+    }
     n_past.assign(lc.max_seqs, 0);
     last_tok.assign(lc.max_seqs, -1);
     logits_row.assign(lc.max_seqs, -1);
@@ -1299,7 +1319,16 @@ struct Engine {
       };
       set_pf(a, 8, w.o, nullptr, E, H * D);
       gemv(a, E, 0);
-      {
+      // M = 32 batched decode: attention, o projection, residual and the NRM epilogue in one launch (k_attn_ob)
+      const bool ob = nrm && M == 32 && use_attn_ob && fused_shape_ok() && ob_wk.opart;
+      if (ob) {
+        hipEvent_t ev;
+        prof_begin(3, &ev);
+        attn_o_batched(lqkv, w.q_norm, w.k_norm, lc.rms_eps, rcos, rsin, kc, vc, M, H, KV, d_tok_seq, d_tok_pos,
+                       seq_stride, w.o.q, w.o.d, E, ob_wk, lx, w.ffn_norm, lxq, lxd, d_ssp, stream);
+        prof_end(3, 0, 0);
+      }
+      if (!ob) {
         hipEvent_t ev;
         prof_begin(3, &ev);
         if (!decode)
@@ -1324,7 +1353,7 @@ struct Engine {
       else { o.xq = lxq2; o.xd = lxd2; }
       if (nrm) { o.ssp_out = d_ssp; o.qout = lxq; o.dout = lxd; o.qn_w = w.ffn_norm; }
       set_pf(o, 1, w.gate, &w.up, F, E);
-      gemv(o, H * D, 1);
+      if (!ob) gemv(o, H * D, 1);
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
       GemvArgs g{};
       g.M = M; g.eps = lc.rms_eps; g.wq = w.gate.q; g.wd = w.gate.d; g.wq2 = w.up.q; g.wd2 = w.up.d; g.O = F;
@@ -1859,6 +1888,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GU_DOWN")) e->use_gu_down = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ATTN_OB")) e->use_attn_ob = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
       fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;
@@ -2436,14 +2466,16 @@ int fa_llm_generate_end(fa_engine* h, int32_t* tokens_out) {
   if (e->fused_layer_runs(n_seqs)) {
     if (e->fused_error()) e->recover_fused_chunk();
     else e->fused_fail_streak = 0;  // a clean fused chunk ends a run of fallbacks ("three in a row", funasr_hip.h)
-  } else if (e->use_gu_down && e->fused_error()) {
-    // a gate|up -> down hand-off timed out (not expected: the producers are dispatched first): two launches from now on
-    fa::log(3, "batched decode: the gate|up -> down hand-off timed out; re-running the chunk with two launches");
+  } else if ((e->use_gu_down || (e->use_attn_ob && n_seqs == 32)) && e->fused_error()) {
+    // a batched-decode in-launch hand-off timed out (the gate|up -> down one, or the attention + o launch's head fan-in:
+    // not expected, every block is resident): the separate launches from now on
+    fa::log(3, "batched decode: an in-launch hand-off timed out; re-running the chunk on separate launches");
     e->use_gu_down = false;
+    e->use_attn_ob = false;
     ++e->fused_recoveries;  // counted with the chunks re-run on another layer form (fa_llm_decode_recoveries)
     e->drop_step_graphs();
     e->rerun_chunk();
-    FA_REQUIRE(!e->fused_error(), "decode chunk re-run: error flag set with the two-launch FFN");
+    FA_REQUIRE(!e->fused_error(), "decode chunk re-run: error flag set on the separate launches");
   }
   std::fill(e->logits_row.begin(), e->logits_row.end(), -1);
   for (int i = 0; i < n_seqs; ++i) {

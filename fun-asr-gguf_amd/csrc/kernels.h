@@ -259,6 +259,21 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
 void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq, const __half* gd, const int8_t* uq,
                const __half* ud, const int8_t* dq, const __half* dd, int E, int F, const FusedDecodeWork& fw,
                hipStream_t s, int M = 1);
+// Batched decode at M = 32 (llm.hip k_attn_ob): attention + o projection + residual + the o GEMM's normalising
+// epilogue in one launch. Workspace: aq / ad the q8_0 attention rows ([32][H D] int8, [32][H D / 32] f32), opart
+// [32][KV][32][32] floats, cnt_g [KV] / cnt_s [32] counter lines (zeroed once), err the timeout flag.
+struct AttnObWork {
+  int8_t* aq = nullptr;
+  float* ad = nullptr;
+  float* opart = nullptr;
+  unsigned* cnt_g = nullptr;
+  unsigned* cnt_s = nullptr;
+  int* err = nullptr;
+};
+void attn_o_batched(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
+                    __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
+                    int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnObWork& w, float* x,
+                    const float* qn_w, int8_t* qout, float* dout, float* ssp_out, hipStream_t s);
 extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
 extern int g_gemm_bf3_256;    // bf16x3 GEMMs: 256x256 tiles when a launch has at least this many (0 = off)
 extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 2)

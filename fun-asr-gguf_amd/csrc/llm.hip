@@ -3979,6 +3979,206 @@ void qkv_attn_o_fused(const float* x, const float* psum, float* xsum, const floa
   hipLaunchKernelGGL(k_attn_o<true>, dim3(KV, ASPLIT, nz), dim3(AWV * 64), 0, s, a);
 }
 
+// ---- Batched decode at M = 32 (the C3 continuous batch): attention, o projection, residual and the o GEMM's
+// normalising epilogue in ONE launch (k_attn_ob), instead of k_attn_block<1, 1, 16> then the split-K o GEMM
+// (k_gemm_q8_sk<1, ...>): one dependent launch and the o GEMM's separate weight stream per layer less.
+// Block (kv head g, token m), 16 waves (one block per CU, all 256 resident):
+//   1. LDS-DMA of the o weights this block will multiply -- rows [32 m, +32) of Wo, columns [256 g, +256) (head g's
+//      pair of query heads), 8 KB + 512 B of scales -- issued before anything else, landed by step 3;
+//   2. the attention of token m, kv head g, exactly k_attn_block<1, 1, 16>'s (attn_split_merge: same values);
+//   3. the head pair's 256 outputs quantised to q8_0 (store_q8_row4's arithmetic: the o GEMM's input), published with
+//      sc1 stores; the 32 blocks of head g pass a ticket fan-in (fanin_wait; under the dispatcher's round-robin they
+//      are the blocks g + 8 m of XCD g);
+//   4. wave 0 multiplies the 32 tokens' rows into its 32 x 32 (row, token) tile on 8 v_mfma_i32_32x32x32_i8 (one q8_0
+//      block of K each: exact integer block dots), scaled f32(dot) * (f32(d_w) * d_x) and summed in block order, and
+//      publishes the tile partial of head g;
+//   5. the last of the 8 head blocks of slice m (last-arriver ticket, re-armed) sums the 8 partials in head order,
+//      adds the residual (x updated in place, rows [32 m, +32) of every token) and runs the residual GEMM's NRM
+//      epilogue (z = x * ffn_norm per 32-row tile = one q8_0 block of every token, unrounded f32 block scale, sum of
+//      squares partial): the gate|up GEMM reads the same inputs as after the o GEMM.
+// The o sum runs in another f32 order than the split-K GEMM (above the invariant width both are only bound to the
+// oracle). Every spin is bounded (SpinDeadline): a timeout sets *err and fa_llm_generate_end re-runs the chunk on
+// the two launches.
+// A/B only (FUNASR_ATTN_OB=1; profiles/r06_exp_attn_ob.txt): the graph-replayed batch-32 step is 1.228-1.231 ms
+// against 1.154-1.158 ms for the two launches. The launch removes one kernel boundary (MI355X_MICROARCH.md boundary:
+// 1.2-1.9 us) but adds a 32-arrival head fan-in with its arrival skew and a cross-XCD last-arriver head sum (two
+// sc1 round trips), and the gate|up GEMM loses the L2 prefetch slabs the o GEMM ran for it.
+constexpr int OB_M = 32;
+struct AttnObArgs {
+  const int* tok_seq;
+  const int* tok_pos;
+  int H, KV;
+  int64_t seq_stride, head_stride;
+  __half* kc;
+  __half* vc;
+  const float* qkv;
+  const float* qn;
+  const float* kn;
+  const float* rcos;
+  const float* rsin;
+  float eps, scale;
+  const int8_t* wo_q;  // [E][H D], engine layout
+  const __half* wo_d;
+  int8_t* aq;          // [M][H D] q8_0 attention rows (published)
+  float* ad;           // [M][H D / 32]
+  float* opart;        // [32 slices][KV][32 tokens][32 rows]
+  unsigned* cnt_g;     // [KV][CNT_LINE] tickets, never re-armed
+  unsigned* cnt_s;     // [32][CNT_LINE] last-arriver counters, re-armed
+  int* err;
+  float* x;            // residual rows [M][E], rows [32 m, +32) rewritten by slice m's last block
+  const float* qn_w;   // ffn_norm (the next RMSNorm)
+  int8_t* qout;        // [M][E] q8_0 of x * qn_w
+  float* dout;         // [M][E / 32] unrounded block scales
+  float* ssp_out;      // [M][32] sum-of-squares partials
+};
+
+__global__ __launch_bounds__(16 * 64, 1) void k_attn_ob(AttnObArgs a) {
+  constexpr int D = 128, NW = 16, E = 1024, KO = 2048, NT = OB_M;  // host: Qwen3-0.6B shapes, M = 32
+  const int g = blockIdx.x, m = blockIdx.z;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // 1. o weights -> LDS slots [chunk c][row r] (slot 32 c + r, chunk c = half c & 1 of q8_0 block c >> 1), so the
+  //    fragment read of block j (lane (r, h) -> slot 32 (2 j + h) + r) is 1 KB contiguous per wave; scales [row][8]
+  __shared__ __attribute__((aligned(16))) int4 s_w[16 * 32];
+  __shared__ __attribute__((aligned(16))) __half s_wd[32 * 8];
+  int pos = a.tok_pos[m];
+  const int seq = a.tok_seq[m];
+  asm volatile("" : "+s"(pos) : "s"(seq), "s"(a.qkv), "s"(a.kc), "s"(a.vc), "s"(a.rcos), "s"(a.rsin), "s"(a.qn),
+               "s"(a.kn));
+  if (threadIdx.x < 512) {
+    const int r = threadIdx.x & 31, c = threadIdx.x >> 5;
+    __builtin_amdgcn_global_load_lds((const void*)(a.wo_q + (int64_t)(32 * m + r) * KO + 256 * g + 16 * c),
+                                     (__attribute__((address_space(3))) void*)&s_w[__builtin_amdgcn_readfirstlane(wave) * 64],
+                                     16, 0, 0);
+  } else if (threadIdx.x < 512 + 32) {
+    const int r = threadIdx.x - 512;
+    __builtin_amdgcn_global_load_lds((const void*)(a.wo_d + (int64_t)(32 * m + r) * (KO / 32) + 8 * g),
+                                     (__attribute__((address_space(3))) void*)&s_wd[0], 16, 0, 0);
+  }
+  // 2. attention (one split: the 16 waves share the key range)
+  int n_active, j, d0;
+  float Mx, L;
+  float4 o;
+  attn_split_merge<1, 1, false, NW>(g, 0, m, pos, seq, 1, a.H, a.KV, a.seq_stride, a.head_stride, a.kc, a.vc, a.qkv,
+                                    a.qn, a.kn, a.rcos, a.rsin, a.eps, a.scale, n_active, j, d0, Mx, L, o);
+  const int KH = a.H * D;
+  const int r = lane & 31, h = lane >> 5;
+  if (wave == 0) {
+    // 3. q8_0 of the head pair's outputs, published (sc1: read by the group's other blocks, from L2)
+    const float4 v = make_float4(o.x / L, o.y / L, o.z / L, o.w / L);
+    const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    const float dd = am / 127.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    const int b0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, b1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
+    const int b2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, b3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
+    const int e = m * KH + (g * GQ + j) * D + d0;
+    __builtin_amdgcn_raw_buffer_store_b32(b0 | (b1 << 8) | (b2 << 16) | (b3 << 24), buf_rsrc(a.aq, NT * KH), e, 0,
+                                          CPOL_SC1);
+    if ((lane & 7) == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__half2float(__float2half_rn(dd))),
+                                            buf_rsrc(a.ad, NT * (KH / 32) * 4), (e / 32) * 4, 0, CPOL_SC1);
+  }
+  fanin_wait(a.cnt_g + g * CNT_LINE, NT, a.err);  // drains every wave's stores and the LDS-DMA loads
+  // 4. wave jb < 8 multiplies q8_0 block jb of the 32 tokens' head-pair rows (B: token r, 16 B half h) into the 32 x 32
+  //    (row, token) tile: one v_mfma_i32_32x32x32_i8 (the exact integer block dots), scaled f32(dot) * (f32(d_w) * d_x);
+  //    wave 0 sums the 8 block products in block order
+  __shared__ float s_acc[8][16][64];
+  if (wave < 8) {
+    const int jb = wave;
+    const i32x4_t B = __builtin_bit_cast(i32x4_t, ld_sc1_f4(buf_rsrc(a.aq, NT * KH), r * KH + 256 * g + 32 * jb + 16 * h));
+    const float dx = ld_sc1_f1(buf_rsrc(a.ad, NT * (KH / 32) * 4), (r * (KH / 32) + 8 * g + jb) * 4);
+    const i32x4_t A = __builtin_bit_cast(i32x4_t, s_w[32 * (2 * jb + h) + r]);
+    const i32x16_t zero = {};
+    const i32x16_t Dv = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B, zero, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // reg q: row 8 (q >> 2) + 4 h + (q & 3) of the slice, token r
+      const int row = 8 * (q >> 2) + 4 * h + (q & 3);
+      s_acc[jb][q][lane] = (float)Dv[q] * (__half2float(s_wd[row * 8 + jb]) * dx);
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  float acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    float v = s_acc[0][q][lane];
+#pragma unroll
+    for (int jb = 1; jb < 8; ++jb) v += s_acc[jb][q][lane];
+    acc[q] = v;
+  }
+  // 5. the tile partial of head g, then the slice's last arriver sums the 8 heads in order
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(a.opart + (int64_t)m * a.KV * NT * 32, a.KV * NT * 32 * 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    st_sc1_f4(f4v{acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]}, rp, ((g * NT + r) * 32 + 8 * q + 4 * h) * 4);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(a.cnt_s + m * CNT_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __builtin_amdgcn_readfirstlane(t);
+  if (t != (unsigned)a.KV - 1) return;
+  // residual rows 32 m + 8 q + 4 h + [0, 4) of token r, loaded with the partials (one round trip)
+  float4 xr[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xr[q] = *reinterpret_cast<const float4*>(a.x + (int64_t)r * E + 32 * m + 8 * q + 4 * h);
+  f4v sum[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sum[q] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+  for (int gg = 0; gg < 8; ++gg) {  // head order (host: KV == 8)
+    f4v pv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pv[q] = ld_sc1_f4(rp, ((gg * NT + r) * 32 + 8 * q + 4 * h) * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sum[q] += pv[q];
+  }
+  if (lane == 0) __hip_atomic_store(a.cnt_s + m * CNT_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // residual + NRM epilogue of tile m (k_gemm_q8_sk's EPI 1 with ssp_out: same roundings per value)
+  float nv[16], z[16], ssq = 0.f, amx = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    nv[4 * q] = xr[q].x + sum[q].x;
+    nv[4 * q + 1] = xr[q].y + sum[q].y;
+    nv[4 * q + 2] = xr[q].z + sum[q].z;
+    nv[4 * q + 3] = xr[q].w + sum[q].w;
+    *reinterpret_cast<float4*>(a.x + (int64_t)r * E + 32 * m + 8 * q + 4 * h) =
+        make_float4(nv[4 * q], nv[4 * q + 1], nv[4 * q + 2], nv[4 * q + 3]);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int row = 32 * m + 8 * (q >> 2) + 4 * h + (q & 3);
+    ssq += nv[q] * nv[q];
+    z[q] = nv[q] * a.qn_w[row];
+    amx = fmaxf(amx, fabsf(z[q]));
+  }
+  ssq += __shfl_xor(ssq, 32, 64);  // the token's other 16 rows (lane r + 32): a + b == b + a, both lanes agree
+  amx = fmaxf(amx, __shfl_xor(amx, 32, 64));
+  const float dz = amx / 127.0f;
+  const float iz = dz != 0.0f ? 1.0f / dz : 0.0f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int q0 = (int)roundf(__fmul_rn(z[4 * q], iz)) & 0xFF, q1 = (int)roundf(__fmul_rn(z[4 * q + 1], iz)) & 0xFF;
+    const int q2 = (int)roundf(__fmul_rn(z[4 * q + 2], iz)) & 0xFF, q3 = (int)roundf(__fmul_rn(z[4 * q + 3], iz)) & 0xFF;
+    *reinterpret_cast<int32_t*>(a.qout + (int64_t)r * E + 32 * m + 8 * q + 4 * h) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
+  }
+  if (h == 0) {
+    a.dout[(int64_t)r * (E / 32) + m] = dz;
+    a.ssp_out[(int64_t)r * 32 + m] = ssq;
+  }
+}
+
+void attn_o_batched(const float* qkv, const float* qn, const float* kn, float eps, const float* rcos, const float* rsin,
+                    __half* kc, __half* vc, int M, int H, int KV, const int* tok_seq, const int* tok_pos,
+                    int64_t seq_stride, const int8_t* wo_q, const __half* wo_d, int E, const AttnObWork& w, float* x,
+                    const float* qn_w, int8_t* qout, float* dout, float* ssp_out, hipStream_t s) {
+  FA_REQUIRE(M == OB_M && H == 16 && KV == 8 && E == 1024, "attn_o_batched: M = 32 rows of the Qwen3-0.6B layer");
+  FA_REQUIRE(w.aq && w.ad && w.opart && w.cnt_g && w.cnt_s && w.err && x && qn_w && qout && dout && ssp_out,
+             "attn_o_batched: workspace");
+  AttnObArgs a{tok_seq, tok_pos, H, KV, seq_stride, seq_stride / KV, kc, vc, qkv, qn, kn, rcos, rsin, eps,
+               1.0f / sqrtf(128.0f), wo_q, wo_d, w.aq, w.ad, w.opart, w.cnt_g, w.cnt_s, w.err, x, qn_w, qout, dout,
+               ssp_out};
+  hipLaunchKernelGGL(k_attn_ob, dim3(KV, 1, M), dim3(16 * 64), 0, s, a);
+}
+
 struct FfnArgs {
   const float* x;       // residual stream after A [E]
   const float* opart;   // [FUSED_PARTS][E]

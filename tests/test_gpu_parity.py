@@ -294,11 +294,15 @@ def test_llm_batch20_lean_attention_chunked_combine(llm_tiny_oracle):
     eng.close()
 
 
-def test_llm_batch32_wide_attention_long_contexts():
+@pytest.mark.parametrize("ob", ["1", "0"])
+def test_llm_batch32_wide_attention_long_contexts(monkeypatch, ob):
     """M = 32 decode: the wide attention launch (one 16-wave block per (token, kv head), no key splits) over contexts of
-    3 .. 651 keys in one launch. Rows checked teacher-forced against the oracle run of each sequence alone, over two
-    steps."""
+    3 .. 651 keys in one launch -- with the o projection, residual and normalising epilogue in the same launch
+    (k_attn_ob, FUNASR_ATTN_OB=1, the default: a 32-block head fan-in, MFMA o tiles, last-arriver head sum) and as the
+    separate o GEMM (=0). Rows checked teacher-forced against the oracle run of each sequence alone, over two steps; no
+    in-launch hand-off timed out."""
     from fun_asr_gguf import _native
+    monkeypatch.setenv("FUNASR_ATTN_OB", ob)
     m = oqw.Qwen3Q8(synth.make_weights(synth.llm_tensors(synth.LLM_TINY)), synth.LLM_TINY, n_ctx=700)
     rng = np.random.default_rng(32)
     lens = [int(n) for n in rng.integers(3, 300, 32)]
@@ -315,6 +319,7 @@ def test_llm_batch32_wide_attention_long_contexts():
         for k in range(2):
             steps.append(eng.llm_generate(list(range(32)), 1)[:, 0])
             lgs.append({s_: eng.llm_logits(s_) for s_ in (0, 1, 2, 3, 7, 19, 31)})
+        assert eng.llm_decode_recoveries() == (0, 0)
     finally:
         eng.close()
     for s_ in (0, 1, 2, 3, 7, 19, 31):
