@@ -1886,6 +1886,10 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_FSMN_VEC")) fa::g_fsmn_vec = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ENC_PLANES")) e->enc_planes = std::min(2, std::max(0, atoi(g)));
     if (const char* g = getenv("FUNASR_FFN_PAIR_MIN_M")) fa::g_ffn_pair_min_m = std::max(2, atoi(g));
+    {  // process-wide knob: re-read (or reset) at every engine creation
+      const char* g = getenv("FUNASR_FFN_WIDE");
+      fa::g_ffn_wide = g ? atoi(g) != 0 : 0;
+    }
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GU_DOWN")) e->use_gu_down = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_OB")) e->use_attn_ob = atoi(g) != 0;

@@ -276,6 +276,7 @@ void attn_o_batched(const float* qkv, const float* qn, const float* kn, float ep
                     const float* qn_w, int8_t* qout, float* dout, float* ssp_out, hipStream_t s);
 extern int g_gemm_bf3_pf;     // few-tile bf16x3 GEMMs: global loads 1 or 2 k-steps ahead (default 2)
 extern int g_gemm_bf3_256;    // bf16x3 GEMMs: 256x256 tiles when a launch has at least this many (0 = off)
+extern int g_ffn_wide;  // small decode batches of 3-6: the fused FFN as one slab, all tokens per block (A/B)
 extern int g_ffn_pair_min_m;  // small decode batches from this width: two tokens per fused-FFN block (default 2)
 // out[m] = xmid[m] + sum_p dpart[m][p] for m < M (a small batch's residual rows after its last fused layer)
 void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, hipStream_t s);

@@ -4214,8 +4214,11 @@ static_assert(FF_ROWS == 12 && FD_ROWS == 32 && FF_GROUP_BLOCKS == 32, "l2_prefe
 // Per token: x_mid = x + sum opart (block 0 stores it), rmsnorm + q8_0, gate|up + SwiGLU for the block's 12 rows, published
 // as granules {value, epoch} (the epoch of that token's attention launch); the group's 384 act rows polled, quantised
 // and multiplied into the block's 32-row slice of the down projection. Same arithmetic for every CT.
+// CT = 3..6 (round 6, FUNASR_FFN_WIDE): the whole batch in one slab of 256 blocks, one per CU (launch bounds (256, 1):
+// the per-token prologue registers of 6 tokens fit), so every block's gate|up and down weight rows are read once for the
+// batch and the group fan-ins stay 32 blocks deep with all 256 blocks resident.
 template <int CT>
-__global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
+__global__ __launch_bounds__(256, CT > 2 ? 1 : 2) void k_ffn_fused(FfnArgs f, int M) {
   constexpr int K = 1024, NB = K / 32, PER = 4, GB = FF_GROUP_ROWS / 32;
   const int b = blockIdx.x, grp = b / FF_GROUP_BLOCKS, bi = b % FF_GROUP_BLOCKS;
   const int m0 = blockIdx.y * CT, ct = min(CT, M - m0);
@@ -4319,20 +4322,43 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   STAMP(2);
+  // thread t < 192 polls 4 granules (act rows 4 pt .. +4 of the group) of tokens pc0, pc0 + 2, ... (NPT of them, all
+  // loads of a sweep in flight together)
   constexpr int QT = FF_GROUP_ROWS / 4;  // polling threads per token
-  const int pc = t / QT, pt = t % QT;
-  f4v gv0 = {0.f, 0.f, 0.f, 0.f}, gv1 = gv0;
-  if (pc < ct) {
-    const unsigned e = pc == 0 ? ep[0] : ep[CT - 1];
-    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act + (int64_t)(m0 + pc) * 2 * f.F, f.F * 8);
-    SpinDeadline dl;
+  constexpr int NPT = (CT + 1) / 2;      // tokens per polling thread
+  const int pc0 = t / QT, pt = t % QT;
+  f4v gv0[NPT], gv1[NPT];
+  unsigned ek[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    gv0[k] = gv1[k] = f4v{0.f, 0.f, 0.f, 0.f};
+    ek[k] = ep[0];
+#pragma unroll
+    for (int c = 1; c < CT; ++c)
+      if (pc0 + 2 * k == c) ek[k] = ep[c];
+  }
+  if (pc0 < 2 && pc0 < ct) {
     const int off = (FF_GROUP_ROWS * grp + 4 * pt) * 8;
+    SpinDeadline dl;
     for (;;) {
-      gv0 = ld_sc1_f4(ra, off);
-      gv1 = ld_sc1_f4(ra, off + 16);
-      if (__float_as_uint(gv0.y) == e && __float_as_uint(gv0.w) == e && __float_as_uint(gv1.y) == e &&
-          __float_as_uint(gv1.w) == e)
-        break;
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int pc = pc0 + 2 * k;
+        if (pc < ct) {
+          const __amdgpu_buffer_rsrc_t ra = buf_rsrc(f.act + (int64_t)(m0 + pc) * 2 * f.F, f.F * 8);
+          gv0[k] = ld_sc1_f4(ra, off);
+          gv1[k] = ld_sc1_f4(ra, off + 16);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const unsigned e = ek[k];
+        if (pc0 + 2 * k < ct)
+          ok = ok && __float_as_uint(gv0[k].y) == e && __float_as_uint(gv0[k].w) == e &&
+               __float_as_uint(gv1[k].y) == e && __float_as_uint(gv1[k].w) == e;
+      }
+      if (ok) break;
       if (dl.expired()) {
         __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -4342,15 +4368,21 @@ __global__ __launch_bounds__(256, 2) void k_ffn_fused(FfnArgs f, int M) {
   }
   STAMP(3);
   // ---- each token's 384 act rows -> q8_0 (8 threads per 32-row block) in LDS
-  if (pc < CT) {
-    const f4v v = {gv0.x, gv0.z, gv1.x, gv1.z};
-    const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    const float d = am / 127.0f;
-    const float id = d != 0.0f ? 1.0f / d : 0.0f;
-    const int q0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, q1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
-    const int q2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, q3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
-    *reinterpret_cast<int32_t*>(s_aq[pc] + 4 * pt) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
-    if ((pt & 7) == 0) s_ad[pc][pt >> 3] = __half2float(__float2half_rn(d));
+  if (pc0 < 2) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int pc = pc0 + 2 * k;
+      if (pc < CT) {
+        const f4v v = {gv0[k].x, gv0[k].z, gv1[k].x, gv1[k].z};
+        const float am = group_max<8>(fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        const float d = am / 127.0f;
+        const float id = d != 0.0f ? 1.0f / d : 0.0f;
+        const int q0 = (int)roundf(__fmul_rn(v.x, id)) & 0xFF, q1 = (int)roundf(__fmul_rn(v.y, id)) & 0xFF;
+        const int q2 = (int)roundf(__fmul_rn(v.z, id)) & 0xFF, q3 = (int)roundf(__fmul_rn(v.w, id)) & 0xFF;
+        *reinterpret_cast<int32_t*>(s_aq[pc] + 4 * pt) = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
+        if ((pt & 7) == 0) s_ad[pc][pt >> 3] = __half2float(__float2half_rn(d));
+      }
+    }
   }
   __syncthreads();
   STAMP(4);
@@ -4392,6 +4424,7 @@ void psum_rows(const float* xmid, const float* dpart, int M, int E, float* out, 
   hipLaunchKernelGGL(k_psum_rows, dim3(cdiv(E / 4, 256), M), dim3(256), 0, s, xmid, dpart, E, out);
 }
 
+int g_ffn_wide = 0;  // FUNASR_FFN_WIDE: decode batches of 3-6 as one slab of CT = M tokens per block (A/B)
 int g_ffn_pair_min_m = 2;  // decode batches from this width run the fused FFN with two tokens per block (round 5,
 // profiles/r05_exp_ffn_pairs.txt: graph-replayed steps, pairs vs one token per block, bit-identical: M = 2 0.530-0.538
 // vs 0.541 ms, M = 4 0.672 vs 0.727, M = 6 0.885-0.894 vs 0.974; the threshold was 4)
@@ -4407,10 +4440,18 @@ void ffn_fused(const float* x, const float* norm_w, float eps, const int8_t* gq,
   FA_REQUIRE(fw.opart && fw.dpart && fw.act && fw.xmid && fw.cnt && fw.err, "ffn_fused: workspace");
   FfnArgs f{x, fw.opart, norm_w, eps, fw.xmid, gq, gd, uq, ud, dq, dd, fw.act, fw.dpart,
             fw.cnt + FUSED_MAX_M * FUSED_PARTS * CNT_LINE, fw.err, E, F, fw.cnt};
-  if (M >= g_ffn_pair_min_m)
+  if (g_ffn_wide && M >= 3 && M <= 6) {  // the batch in one slab: weights read once, one block per CU
+    switch (M) {
+      case 3: hipLaunchKernelGGL(k_ffn_fused<3>, dim3(F / FF_ROWS, 1), dim3(256), 0, s, f, M); break;
+      case 4: hipLaunchKernelGGL(k_ffn_fused<4>, dim3(F / FF_ROWS, 1), dim3(256), 0, s, f, M); break;
+      case 5: hipLaunchKernelGGL(k_ffn_fused<5>, dim3(F / FF_ROWS, 1), dim3(256), 0, s, f, M); break;
+      default: hipLaunchKernelGGL(k_ffn_fused<6>, dim3(F / FF_ROWS, 1), dim3(256), 0, s, f, M); break;
+    }
+  } else if (M >= g_ffn_pair_min_m) {
     hipLaunchKernelGGL(k_ffn_fused<2>, dim3(F / FF_ROWS, cdiv(M, 2)), dim3(256), 0, s, f, M);
-  else
+  } else {
     hipLaunchKernelGGL(k_ffn_fused<1>, dim3(F / FF_ROWS, M), dim3(256), 0, s, f, M);
+  }
 }
 
 }  // namespace fa

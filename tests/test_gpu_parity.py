@@ -797,6 +797,35 @@ def test_batched_decode_attention_lds_prefetch_bit_identical(monkeypatch):
     assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
 
 
+@pytest.mark.parametrize("M", [3, 4, 6])
+def test_fused_ffn_one_slab_bit_identical(monkeypatch, M):
+    """Small decode batches with the fused FFN as ONE slab of M tokens per block (FUNASR_FFN_WIDE=1: every block's
+    gate|up and down weight rows read once for the batch, one block per CU) keep each token's batch-1 arithmetic: the
+    same tokens and logits as the token-pair slabs over 20 graph-replayed steps and one eager step, and no fan-in timed
+    out."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(60 + M)
+    prompts = [(rng.standard_normal((20 + 9 * q, 1024)) * 0.5).astype(np.float32) for q in range(M)]
+    runs = []
+    for wide in ("0", "1"):
+        monkeypatch.setenv("FUNASR_FFN_WIDE", wide)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=M), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            for q in range(M):
+                eng.llm_reset(q)
+                eng.llm_prefill(q, prompts[q])
+            toks = eng.llm_generate(list(range(M)), 20)
+            toks1 = eng.llm_generate(list(range(M)), 1)
+            runs.append((toks, toks1, [eng.llm_logits(q) for q in range(M)], eng.llm_decode_recoveries()))
+        finally:
+            eng.close()
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][2], runs[1][2]))
+    assert runs[1][3] == (0, 0)
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
