@@ -3569,12 +3569,17 @@ int g_l2pf_mask = 7;
 // q|k|v rows of kv head g, the o columns [256 g, +256) and head g's K/V rows [0, pos]. LDS-DMA loads into a scratch slot
 // (no VGPR results), drained before the block ends. Bytes and results are untouched: a prefetch only moves lines.
 // nseg segments of SU 16-B units, STRIDE bytes apart (compile-time shape: the unit -> address map is a multiply-shift)
+// FA_L2PF_AUX (A/B builds): cache-policy bits of the prefetch slabs' LDS-DMA loads (0 default; 2 nt)
+#ifndef FA_L2PF_AUX
+#define FA_L2PF_AUX 0
+#endif
 template <int NSEG, int SU, int64_t STRIDE>
 __device__ __forceinline__ void pf_family(const void* base, int tid, int T, __attribute__((address_space(3))) void* lds) {
   constexpr int U = NSEG * SU;
   for (int u = tid; u < U; u += T) {
     const int seg = u / SU, off = u - seg * SU;
-    __builtin_amdgcn_global_load_lds((const void*)((const char*)base + seg * STRIDE + (int64_t)off * 16), lds, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)((const char*)base + seg * STRIDE + (int64_t)off * 16), lds, 16, 0,
+                                     FA_L2PF_AUX);
   }
 }
 
@@ -3615,8 +3620,8 @@ __device__ __forceinline__ void l2_prefetch(const AttnOArgs& a, int g, int pb, i
       const int64_t kvo = (int64_t)seq * a.seq_stride + (int64_t)g * a.head_stride;
       const int U = (pos + 1) * D * 2 / 16;
       for (int u = tid; u < U; u += T) {
-        __builtin_amdgcn_global_load_lds((const void*)(p.kc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(p.kc + kvo + (int64_t)u * 8), lds, 16, 0, FA_L2PF_AUX);
+        __builtin_amdgcn_global_load_lds((const void*)(p.vc + kvo + (int64_t)u * 8), lds, 16, 0, FA_L2PF_AUX);
       }
     }
   }
