@@ -192,6 +192,10 @@ struct Engine {
   // Measured slower (profiles/r06_exp_attn_ob.txt: graph-replayed batch-32 step 1.228-1.231 vs 1.154-1.158 ms): the two
   // in-launch edges it adds (32-block head fan-in, cross-XCD head sum) cost more than the kernel boundary they replace
   bool use_attn_ob = false;
+  // row-local prefill on producer-normalised rows (FUNASR_PREFILL_NRM=1, A/B): measured slower (profiles/
+  // r06_exp_prefill_nrm.txt: one 204-row prompt 2.59-2.60 vs 2.41-2.43 ms, 512 rows 4.72 vs 4.16 ms): the normalising
+  // epilogue and the rstd prologue cost the K-in-block GEMMs more than the two k_prep_q8 launches per layer they replace
+  bool use_pnrm = false;
   fa::AttnObWork ob_wk;
   float* gk_part = nullptr;  // MFMA GEMM split-K workspace
   int* gk_cnt = nullptr;
@@ -826,7 +830,7 @@ struct Engine {
     n_part = std::max(lm_head_parts(lc.n_vocab, 1, E), cdiv(lc.n_vocab, 32));  // the GEMV's partials or one per 32-row tile
     pval = alloc<float>((size_t)lc.max_seqs * n_part);
     pidx = alloc<int>((size_t)lc.max_seqs * n_part);
-    d_ssp = alloc<float>((size_t)lc.max_seqs * 32);
+    d_ssp = alloc<float>((size_t)std::max(lc.max_seqs, pf_max) * 32);  // batched decode and row-local prefill rows
 
     d_tok_seq = alloc<int>(pf_max);
     d_tok_pos = alloc<int>(pf_max);
@@ -1283,6 +1287,10 @@ struct Engine {
     // (no k_prep_q8 launches but layer 0's)
     const bool fused = decode && fused_layer_runs(M);
     const bool nrm = decode && !small && M <= 32 && E == 1024 && use_nrm && !fused;
+    // row-local prefill: the same producer-normalised rows on the K-in-block GEMMs (k_gemm_q8_kw NRM): the o / down
+    // residual epilogues quantise x * the next RMSNorm weight and leave sum-of-squares partials, q|k|v and gate|up apply
+    // rstd to the block scales: no k_prep_q8 launch but layer 0's (FUNASR_PREFILL_NRM=0: the prep launches, A/B)
+    const bool pnrm = rl && E == 1024 && use_pnrm && M <= pf_max;
 
     (void)max_pos;
     if (fused) {
@@ -1308,7 +1316,7 @@ struct Engine {
       a.wq = w.qkv.q; a.wd = w.qkv.d; a.O = QKV; a.rpw = gemv_rows_per_wave(QKV);
       a.out = lqkv; a.ldo = QKV;
       if (small) { a.x = lx; a.ldx = E; a.norm_w = w.attn_norm; }
-      else if (nrm && l > 0) { a.xq = lxq; a.xd = lxd; a.ssp = d_ssp; }  // rows from the previous down epilogue
+      else if ((nrm || pnrm) && l > 0) { a.xq = lxq; a.xd = lxd; a.ssp = d_ssp; }  // rows from the previous down epilogue
       else { prep_q8(lx, E, w.attn_norm, lc.rms_eps, M, E, lxq, lxd, stream); a.xq = lxq; a.xd = lxd; }
       // batched decode: each split-K GEMM pulls the next one's weight rows into the reading XCDs' L2 (gemm_l2_prefetch)
       const bool gpf = nrm && fa::g_gemm_pf;
@@ -1351,7 +1359,7 @@ struct Engine {
       o.out = lx; o.ldo = E; o.res = lx; o.ldr = E;
       if (small) { o.x = latt; o.ldx = H * D; }
       else { o.xq = lxq2; o.xd = lxd2; }
-      if (nrm) { o.ssp_out = d_ssp; o.qout = lxq; o.dout = lxd; o.qn_w = w.ffn_norm; }
+      if (nrm || pnrm) { o.ssp_out = d_ssp; o.qout = lxq; o.dout = lxd; o.qn_w = w.ffn_norm; }
       set_pf(o, 1, w.gate, &w.up, F, E);
       if (!ob) gemv(o, H * D, 1);
       // act = silu(Wg . h) * (Wu . h), h = rms_norm(x)*ffn_norm
@@ -1361,7 +1369,7 @@ struct Engine {
       g.rpw = gemv_rows_per_wave(F); g.out = lact; g.ldo = F;
       if (small) { g.x = lx; g.ldx = E; g.norm_w = w.ffn_norm; }
       else {
-        if (nrm) { g.xq = lxq; g.xd = lxd; g.ssp = d_ssp; }  // rows from the o epilogue
+        if (nrm || pnrm) { g.xq = lxq; g.xd = lxd; g.ssp = d_ssp; }  // rows from the o epilogue
         else { prep_q8(lx, E, w.ffn_norm, lc.rms_eps, M, E, lxq, lxd, stream); g.xq = lxq; g.xd = lxd; }
         g.qout = lxq2; g.dout = lxd2;  // SwiGLU epilogue quantises act for the down GEMM (no prep launch)
       }
@@ -1373,7 +1381,7 @@ struct Engine {
       dn.out = lx; dn.ldo = E; dn.res = lx; dn.ldr = E;
       if (small) { dn.x = lact; dn.ldx = F; }
       else { dn.xq = lxq2; dn.xd = lxd2; }
-      if (nrm) {
+      if (nrm || (pnrm && l + 1 < lc.n_layer)) {  // (prefill: the LM head reads the last layer's f32 rows)
         dn.ssp_out = d_ssp; dn.qout = lxq; dn.dout = lxd;
         dn.qn_w = l + 1 < lc.n_layer ? layers[l + 1].attn_norm : out_norm;
       }
@@ -1893,6 +1901,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_DECODE_NRM")) e->use_nrm = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GU_DOWN")) e->use_gu_down = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_OB")) e->use_attn_ob = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_PREFILL_NRM")) e->use_pnrm = atoi(g) != 0;
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
       fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;

@@ -1373,9 +1373,14 @@ __global__ __launch_bounds__(256, LMS_PER_CU) void k_lm_head_s(GemvArgs a) {
 // costs one memory round trip. Waves are reduced in LDS in fixed order (deterministic). SwiGLU: the first half
 // of the waves take the gate matrix, the second half the up matrix. NW = 16 (1024 threads) for the few-tile
 // shapes (o and down at batch 32: 32 tiles) so each CU keeps twice the loads in flight.
-template <int EPI, int NW, int NBW>
+// NIN (row-local prefill, round 6; the batched decode's NRM form, k_gemm_q8_sk): the input rows come from the previous
+// residual GEMM's epilogue (EPI 1 with ssp_out below), which quantised z = x * norm_w per 32-block and left per-token
+// sum-of-squares partials; this GEMM applies rstd = 1/sqrtf(sum/K + eps) to the block scales, so the two k_prep_q8
+// launches per layer disappear.
+template <int EPI, int NW, int NBW, bool NIN = false>
 __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   static_assert(NBW % 2 == 0 && (NW == 8 || (NW == 16 && EPI != 2)), "k_gemm_q8_kw: shapes");
+  static_assert(!NIN || EPI == 0 || EPI == 2, "k_gemm_q8_kw: normalised inputs feed q|k|v and gate|up");
   constexpr int NWM = EPI == 2 ? NW / 2 : NW;  // waves per weight matrix
   const int nb = K >> 5;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -1388,6 +1393,11 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   const int t_b = min(t0 + r, a.M - 1);
   const int8_t* xb = a.xq + (int64_t)t_b * K + 16 * h + b0 * 32;
   GSTAMP(0);
+  float4 sv[NIN ? 8 : 1];
+  if constexpr (NIN) {  // this lane's token's 32 partials, issued first
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sv[i] = *reinterpret_cast<const float4*>(a.ssp + (int64_t)t_b * 32 + 4 * i);
+  }
   i32x4_t A[NBW], B[NBW];
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
@@ -1407,6 +1417,17 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
 #pragma unroll
   for (int q = 0; q < NBW / 2; ++q) dx2[q] = *reinterpret_cast<const float2*>(a.xd + (int64_t)t_b * nb + b0 + 2 * q);
   __builtin_amdgcn_sched_barrier(0);  // every load issued before any use (hipcc would hoist MFMAs between them)
+  if constexpr (NIN) {  // k_gemm_q8_sk's NRM arithmetic: the producer's 32 tile partials in tile order
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss = (((ss + sv[i].x) + sv[i].y) + sv[i].z) + sv[i].w;
+    const float rstd = 1.0f / sqrtf(ss / (float)K + a.eps);
+#pragma unroll
+    for (int q = 0; q < NBW / 2; ++q) {
+      dx2[q].x = __half2float(__float2half_rn(rstd * dx2[q].x));
+      dx2[q].y = __half2float(__float2half_rn(rstd * dx2[q].y));
+    }
+  }
   // the wave's scales as f32 in LDS, [block][row]: each lane then reads its 16 rows' (rows 8 g + 4 h + [0, 4)) of a
   // block as 4 float4, converted once per wave instead of once per lane (wave-private rows: no block barrier)
   __shared__ float4 s_dw4[NW][NBW][8];
@@ -1447,7 +1468,7 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
   constexpr int NRM = EPI == 2 ? NR / 2 : NR;
   constexpr int RPT = 16 / NW;
   __shared__ float s_red[NR][16][64];
-  __shared__ float s_act[EPI >= 2 ? 32 : 1][33];  // tile [token][row]: SwiGLU q8_0 epilogue, lm_head argmax
+  __shared__ float s_act[EPI >= 1 ? 32 : 1][33];  // tile [token][row]: SwiGLU / NRM q8_0 epilogues, lm_head argmax
   if (NW == 16) {
     if (wave >= 8) {
 #pragma unroll
@@ -1483,10 +1504,10 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
     if (row < a.O && tok < a.M) {
       float* op = a.out + (int64_t)tok * a.ldo + row;
       if (EPI == 0 || EPI == 3) *op = v = y;
-      else if (EPI == 1) *op = a.res[(int64_t)tok * a.ldr + row] + y;
+      else if (EPI == 1) *op = v = a.res[(int64_t)tok * a.ldr + row] + y;
       else *op = v = (y / (1.0f + expf(-y))) * y2;
     }
-    if (EPI == 2) s_act[col][rrow] = v;
+    if (EPI == 1 || EPI == 2) s_act[col][rrow] = v;
     if (EPI == 3) s_act[col][rrow] = row < a.O ? v : -INFINITY;
   }
   if (EPI == 3) {
@@ -1504,12 +1525,51 @@ __global__ __launch_bounds__(NW * 64) void k_gemm_q8_kw(GemvArgs a, int K) {
     __syncthreads();
     swiglu_tile_q8(s_act, a, t0, o0);
   }
+  if (EPI == 1 && a.ssp_out) {
+    // the next NRM GEMM's input (its K = this GEMM's O = 1024): the tile is one q8_0 block of every token; threads
+    // 0..63 (token t & 31, rows [16 (t >> 5), +16)) quantise z = x_new * qn_w (block scale amax / 127, unrounded f32)
+    // and leave the rows' sum of squares (the two halves added) in ssp_out[tok][tile]
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int tk = threadIdx.x & 31, hh = threadIdx.x >> 5, tokq = t0 + tk;
+      float z[16], am = 0.f, ssq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float xv = s_act[tk][16 * hh + i];
+        ssq += xv * xv;
+        z[i] = xv * a.qn_w[o0 + 16 * hh + i];
+        am = fmaxf(am, fabsf(z[i]));
+      }
+      ssq += __shfl_xor(ssq, 32, 64);
+      am = fmaxf(am, __shfl_xor(am, 32, 64));
+      const float d = am / 127.0f;
+      const float id = d != 0.0f ? 1.0f / d : 0.0f;
+      int32_t pk[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q0 = (int)roundf(__fmul_rn(z[4 * j], id)) & 0xFF, q1 = (int)roundf(__fmul_rn(z[4 * j + 1], id)) & 0xFF;
+        const int q2 = (int)roundf(__fmul_rn(z[4 * j + 2], id)) & 0xFF, q3 = (int)roundf(__fmul_rn(z[4 * j + 3], id)) & 0xFF;
+        pk[j] = q0 | (q1 << 8) | (q2 << 16) | (q3 << 24);
+      }
+      if (tokq < a.M) {
+        *reinterpret_cast<int4*>(a.qout + (int64_t)tokq * 1024 + o0 + 16 * hh) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+        if (hh == 0) {
+          a.dout[(int64_t)tokq * 32 + blockIdx.x] = d;
+          a.ssp_out[(int64_t)tokq * 32 + blockIdx.x] = ssq;
+        }
+      }
+    }
+  }
   GSTAMP(3);
 }
 
 template <int EPI, int NW, int NBW>
 static void launch_gemm_kw(const GemvArgs& a, int K, hipStream_t s) {
-  hipLaunchKernelGGL((k_gemm_q8_kw<EPI, NW, NBW>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)), dim3(NW * 64), 0, s, a, K);
+  if (a.ssp)
+    hipLaunchKernelGGL((k_gemm_q8_kw<EPI == 1 ? 0 : EPI, NW, NBW, true>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)),
+                       dim3(NW * 64), 0, s, a, K);
+  else
+    hipLaunchKernelGGL((k_gemm_q8_kw<EPI, NW, NBW>), dim3(cdiv(a.O, 32), cdiv(a.M, 32)), dim3(NW * 64), 0, s, a, K);
 }
 
 // K-in-block GEMM for the shapes it is instantiated for; false otherwise. 8 waves (16 measured slower on the
@@ -1860,7 +1920,11 @@ void gemv_q8(const GemvArgs& a, int K, int epi, hipStream_t s) {
   }
   FA_REQUIRE(!fused, "gemv_q8: fused prologue only for M <= g_gemv_small_max");
   if (a.row_local) {  // each token row's arithmetic independent of the token count: the K-in-block kernel only
-    FA_REQUIRE(epi != 3 && !a.ssp && !a.ssp_out, "gemv_q8: row-local rows are prefill layer GEMMs");
+    FA_REQUIRE(epi != 3, "gemv_q8: row-local rows are prefill layer GEMMs");
+    FA_REQUIRE(!a.ssp || (K == 1024 && (epi == 0 || epi == 2) && a.xq && a.xd),
+               "gemv_q8: normalised-input rows feed q|k|v / gate|up (K 1024)");
+    FA_REQUIRE(!a.ssp_out || (epi == 1 && a.O == 1024 && a.qout && a.dout && a.qn_w),
+               "gemv_q8: the normalising residual epilogue needs O 1024, qout / dout and qn_w");
     FA_REQUIRE(gemm_q8_kw(a, K, epi, s, true), "gemv_q8: row-local GEMM shape not instantiated");
     return;
   }
