@@ -3590,6 +3590,9 @@ struct AttnOArgs {
 #ifndef FA_KV_EARLY
 #define FA_KV_EARLY 2
 #endif
+#ifndef FA_QKV_POLL
+#define FA_QKV_POLL 0
+#endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
 
@@ -3846,7 +3849,36 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     if (FA_KV_EARLY == 2) kv_early(a, g, sp, pos, seq, wave, lane, qpre, kpre, vpre);
     STAMP(13);
     // thread t: head g's local rows 2t, 2t + 1 (q head GQ g, q head GQ g + 1, k head g, v head g; 128 each)
+    // (FA_QKV_POLL = 1, A/B builds: wave 0 alone polls all 512 granules, 8 rows per lane, the other waves wait at the
+    // barrier: a quarter of the polling traffic in the consumer CU's memory queue)
     __shared__ float s_qkv[(GQ + 2) * D];
+#if FA_QKV_POLL
+    if (wave == 0) {
+      const int lr = 8 * lane, sg = lr / D;
+      const int grow = (sg < GQ ? (g * GQ + sg) * D : sg == GQ ? (a.H + g) * D : (a.H + a.KV + g) * D) + lr % D;
+      const __amdgpu_buffer_rsrc_t rg = buf_rsrc(a.gqkv, (a.H + 2 * a.KV) * D * 8);
+      f4v gv[4];
+      SpinDeadline dl;
+      for (;;) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gv[k] = ld_sc1_f4(rg, (grow + 2 * k) * 8);
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ok = ok && __float_as_uint(gv[k].y) == ep_qkv && __float_as_uint(gv[k].w) == ep_qkv;
+        if (ok) break;
+        if (dl.expired()) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s_qkv[lr + 2 * k] = gv[k].x;
+        s_qkv[lr + 2 * k + 1] = gv[k].z;
+      }
+    }
+#else
     {
       const int lr = 2 * threadIdx.x, sg = lr / D;
       const int grow = (sg < GQ ? (g * GQ + sg) * D : sg == GQ ? (a.H + g) * D : (a.H + a.KV + g) * D) + lr % D;
@@ -3865,6 +3897,7 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
       s_qkv[lr] = gv.x;
       s_qkv[lr + 1] = gv.z;
     }
+#endif
     __syncthreads();
     STAMP(14);
 #pragma unroll
