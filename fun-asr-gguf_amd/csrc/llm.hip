@@ -3593,6 +3593,11 @@ struct AttnOArgs {
 #ifndef FA_QKV_POLL
 #define FA_QKV_POLL 0
 #endif
+// FA_ROPE_EARLY (two-launch layer): the rope row at pos loaded at kernel start with the weights (1) or in kv_early,
+// after the q|k|v rows are published (0)
+#ifndef FA_ROPE_EARLY
+#define FA_ROPE_EARLY 0
+#endif
 
 constexpr int FQ_ROWS = 32;  // q|k|v rows per split block in the two-launch layer ((GQ + 2) D / ASPLIT)
 
@@ -3604,8 +3609,10 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
   const int n_keys = pos + 1, n_groups = (n_keys + 3) >> 2;
   const int gps = max(AMIN_G, (int)ceilf((float)n_groups / (float)ASPLIT));
   const int n_active = (int)ceilf((float)n_groups / (float)gps);
+#if !FA_ROPE_EARLY
   qpre.c = a.rcos[(int64_t)pos * 64 + lane];
   qpre.sn = a.rsin[(int64_t)pos * 64 + lane];
+#endif
   if (sp >= n_active) return;
   const int g0 = sp * gps + wave, ge = min(n_groups, sp * gps + gps);
   if (g0 >= ge) return;
@@ -3805,6 +3812,12 @@ __global__ __launch_bounds__(AWV * 64, 1) void k_attn_o(AttnOArgs a0) {
     wk[k] = ld_nt16(a.wo_q + (int64_t)orow * KO + GQ * D * g + 16 * c16);
     dwk[k] = __half2float(a.wo_d[(int64_t)orow * (KO / 32) + (GQ * D * g) / 32 + (c16 >> 1)]);
   }
+#if FA_ROPE_EARLY
+  if constexpr (QKV) {  // the rope row at pos behind the weight loads (the q norm + rope waited for it in kv_early)
+    qpre.c = a.rcos[(int64_t)pos * 64 + lane];
+    qpre.sn = a.rsin[(int64_t)pos * 64 + lane];
+  }
+#endif
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (QKV) {
     // ---- prologue (k_gemv_q8 PS): x = x_mid + sum dpart; block (0, 0) stores it; rmsnorm + q8_0 into LDS
