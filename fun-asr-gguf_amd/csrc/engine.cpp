@@ -428,7 +428,10 @@ struct Engine {
       std::vector<float> h(D);
       float mx = 0.f;
       for (const LlmLayerW& w : layers) {
-        FA_HIP(hipMemcpy(h.data(), w.q_norm, D * 4, hipMemcpyDeviceToHost));
+        // on the engine's stream: the weight uploads are async on it (a null-stream copy does not wait for a
+        // non-blocking stream and could read the previous weights)
+        FA_HIP(hipMemcpyAsync(h.data(), w.q_norm, D * 4, hipMemcpyDeviceToHost, stream));
+        FA_HIP(hipStreamSynchronize(stream));
         for (float v : h) mx = std::max(mx, std::isfinite(v) ? std::fabs(v) : INFINITY);
       }
       const bool ok = mx * std::sqrt((float)D) * (1.0f / std::sqrt(128.0f)) * 256.0f < 60000.0f;  // kernel: D = 128
