@@ -228,11 +228,17 @@ struct Engine {
   std::unordered_map<int, hipGraphExec_t> step_graphs;
   bool use_graphs = true;
 
+  int fill_lo = -1, fill_hi = -2, fill_byte = 0;  // FUNASR_ALLOC_FILL (alloc)
   template <class T>
   T* alloc(size_t n) {
     void* p = nullptr;
     FA_HIP(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
     allocs.push_back(p);
+    // FUNASR_ALLOC_FILL=lo:hi:byte (test hook, read at engine creation): allocations lo..hi of this engine start filled
+    // with that byte instead of whatever bytes earlier buffers left (0xFF: NaN patterns), so a read of a never-written
+    // byte shows up in results (tests/test_gpu_parity.py::test_poisoned_allocations_decode_bit_identical)
+    const int idx = (int)allocs.size() - 1;
+    if (idx >= fill_lo && idx <= fill_hi) FA_HIP(hipMemset(p, fill_byte, std::max<size_t>(n, 1) * sizeof(T)));
     return (T*)p;
   }
   ~Engine() {
@@ -1905,6 +1911,7 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_GU_DOWN")) e->use_gu_down = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_OB")) e->use_attn_ob = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_PREFILL_NRM")) e->use_pnrm = atoi(g) != 0;
+    if (const char* g = getenv("FUNASR_ALLOC_FILL")) sscanf(g, "%d:%d:%d", &e->fill_lo, &e->fill_hi, &e->fill_byte);
     {  // process-wide GEMM shape knob: re-read (or reset) at every engine creation
       const char* g = getenv("FUNASR_GEMM_T_MIN_M");
       fa::g_gemm_t_min_m = g ? std::max(1, atoi(g)) : 512;

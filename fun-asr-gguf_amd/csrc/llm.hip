@@ -2131,13 +2131,20 @@ constexpr int APART = ATTN_PART_FLOATS;  // per-split partial: o[GQ][128], m[GQ]
 // Lane (kq = lane>>4, dq = lane&15) holds dims [8 dq, 8 dq + 8) of key 4 q + kq: each load instruction
 // reads 4 whole 256-B rows. Groups past the wave's share are loaded clamped (valid rows, compute skipped):
 // no branches around loads.
+// kmax: the last cache row a load may touch. Decode passes pos - 1: row pos is this launch's fresh row, stored by its
+// owner wave (which takes its values from LDS) possibly AFTER other waves' clamped loads, so a clamped re-read of it
+// would see stale bytes -- bytes a previous buffer left there, possibly NaN / Inf patterns -- and a masked key's
+// p = 0 times a NaN V is NaN. Masked keys re-read row pos - 1 instead (written, finite): valid keys are unchanged.
+#ifndef FA_KV_CLAMP_OLD  // 1 (A/B builds only): the pre-round-6 clamp to row pos (reproduces the stale-row read)
+#define FA_KV_CLAMP_OLD 0
+#endif
 template <int NI, int AW>
-__device__ __forceinline__ void load_kv_groups(const __half* __restrict__ base, int KV, int g0, int n_keys, int kq,
+__device__ __forceinline__ void load_kv_groups(const __half* __restrict__ base, int KV, int g0, int kmax, int kq,
                                                int dq, int4 (&t)[NI]) {
   constexpr int D = 128;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int k = min(4 * (g0 + AW * i) + kq, n_keys - 1);
+    const int k = min(4 * (g0 + AW * i) + kq, kmax);
     t[i] = *reinterpret_cast<const int4*>(base + (int64_t)k * D + dq * 8);  // head-major cache: rows D apart
   }
 }
@@ -2189,10 +2196,11 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
                                           float (&mx)[GQ], float (&l)[GQ], float (&acc)[GQ][8],
                                           const int4* pk = nullptr, const int4* pv = nullptr, int4* slot = nullptr) {
   constexpr int SD = 128;
+  const int kmax = decode && !FA_KV_CLAMP_OLD ? max(pos - 1, 0) : n_keys - 1;  // last cache row a load may touch
   auto lpf_issue = [&](int g1) {  // next pass's groups -> slot (clamped rows as load_kv_groups clamps them)
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int k = min(4 * (g1 + AW * i) + kq, n_keys - 1);
+      const int k = min(4 * (g1 + AW * i) + kq, kmax);
       __builtin_amdgcn_global_load_lds((const void*)(kb + (int64_t)k * SD + dq * 8),
                                        (__attribute__((address_space(3))) void*)(slot + i * 64), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(vb + (int64_t)k * SD + dq * 8),
@@ -2208,8 +2216,8 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
       vt[i] = pv[i];
     }
   } else {
-    load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-    load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+    load_kv_groups<NI, AW>(kb, KV, g0, kmax, kq, dq, kt);
+    load_kv_groups<NI, AW>(vb, KV, g0, kmax, kq, dq, vt);
   }
   if constexpr (LPF) {
     if (g0 + AW * NI < ge) lpf_issue(g0 + AW * NI);
@@ -2261,8 +2269,8 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
     if constexpr (PIPE) {
       const int g1 = g0 + AW * NI;
       if (g1 < ge) {
-        load_kv_groups<NI, AW>(kb, KV, g1, n_keys, kq, dq, kn_);
-        load_kv_groups<NI, AW>(vb, KV, g1, n_keys, kq, dq, vn_);
+        load_kv_groups<NI, AW>(kb, KV, g1, kmax, kq, dq, kn_);
+        load_kv_groups<NI, AW>(vb, KV, g1, kmax, kq, dq, vn_);
       }
     }
     // scores of key 4 (g0 + AW i) + kq: 8-dim partial dot per lane, summed over the row's 16 lanes (DPP)
@@ -2344,8 +2352,8 @@ __device__ __forceinline__ void attn_wave(const __half* __restrict__ kb, const _
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the slot is refilled
       if (g0 + AW * NI < ge) lpf_issue(g0 + AW * NI);
     } else {
-      load_kv_groups<NI, AW>(kb, KV, g0, n_keys, kq, dq, kt);
-      load_kv_groups<NI, AW>(vb, KV, g0, n_keys, kq, dq, vt);
+      load_kv_groups<NI, AW>(kb, KV, g0, kmax, kq, dq, kt);
+      load_kv_groups<NI, AW>(vb, KV, g0, kmax, kq, dq, vt);
     }
   }
 }
@@ -3618,8 +3626,8 @@ __device__ __forceinline__ void kv_early(const AttnOArgs& a, int g, int sp, int 
   if (g0 >= ge) return;
   const __half* kb = a.kc + (int64_t)seq * a.seq_stride + g * a.head_stride;
   const __half* vb = a.vc + (int64_t)seq * a.seq_stride + g * a.head_stride;
-  load_kv_groups<AKV_PRE, AWV>(kb, a.KV, g0, n_keys, lane >> 4, lane & 15, pk);
-  load_kv_groups<AKV_PRE, AWV>(vb, a.KV, g0, n_keys, lane >> 4, lane & 15, pv);
+  load_kv_groups<AKV_PRE, AWV>(kb, a.KV, g0, FA_KV_CLAMP_OLD ? pos : max(pos - 1, 0), lane >> 4, lane & 15, pk);
+  load_kv_groups<AKV_PRE, AWV>(vb, a.KV, g0, FA_KV_CLAMP_OLD ? pos : max(pos - 1, 0), lane >> 4, lane & 15, pv);
 }
 
 int g_l2pf_blocks = 16;

@@ -150,8 +150,12 @@ def test_reference_decode_loop_equals_engine(gguf):
         rest = e.llm_generate([0], 15)[0].tolist()
         assert (lg0 == elg).all()  # the prefill forward is the engine's
         assert toks == [t0] + rest  # host greedy over the copied logits == the engine's device greedy, step for step
+        el15 = e.llm_logits(0)
         e.llm_generate([0], 1)
-        assert (lg_last == e.llm_logits(0)).all()
+        el = e.llm_logits(0)
+        assert (lg_last == el).all(), (
+            f"max |diff| {np.abs(lg_last - el).max():.3g}, vs the engine's previous step {np.abs(lg_last - el15).max():.3g}"
+            f", engine recoveries {e.llm_decode_recoveries()}, n_past {e.llm_n_past(0)}")
         # a cleared context decodes the same prompt to the same tokens
         assert reference_decode_loop(L, ctx, embd, 16)[0] == toks
         eos = L.llama_vocab_eos(L.llama_model_get_vocab(model))

@@ -826,6 +826,37 @@ def test_fused_ffn_one_slab_bit_identical(monkeypatch, M):
     assert runs[1][3] == (0, 0)
 
 
+@pytest.mark.parametrize("M", [1, 6, 32])
+def test_poisoned_allocations_decode_bit_identical(monkeypatch, M):
+    """Every allocation of the engine starts filled with 0xFF bytes (NaN patterns as fp16 / f32; FUNASR_ALLOC_FILL)
+    instead of whatever earlier buffers left: prefill, 8 graph-replayed steps, 4 single-step calls give the same tokens
+    and logits bit for bit as an engine on zero-filled memory. Round 6 found the decode attention re-reading the fresh
+    cache row pos (the clamp target of masked keys) before its owner wave stored it: a masked key's p = 0 times a NaN V
+    poisoned the head's output when the memory held such bytes (tests/test_gpu_llama_compat.py failed after other
+    tests' engines had freed theirs)."""
+    from fun_asr_gguf import _native
+    rng = np.random.default_rng(80 + M)
+    prompts = [(rng.standard_normal((23 + 7 * q, 1024)) * 0.5).astype(np.float32) for q in range(M)]
+    runs = []
+    for fill in ("0:100000:0", "0:100000:255"):
+        monkeypatch.setenv("FUNASR_ALLOC_FILL", fill)
+        eng = _native.Engine(synth.ENC_TINY, dict(synth.LLM_TINY, n_ctx=256, max_seqs=M), max_batch=1,
+                             max_samples=16000)
+        try:
+            eng.synthetic_weights(0)
+            for q in range(M):
+                eng.llm_reset(q)
+                eng.llm_prefill(q, prompts[q])
+            toks = [eng.llm_generate(list(range(M)), 8)]
+            for _ in range(4):
+                toks.append(eng.llm_generate(list(range(M)), 1))
+            runs.append((np.concatenate(toks, 1), [eng.llm_logits(q) for q in range(M)]))
+        finally:
+            eng.close()
+    assert np.array_equal(runs[0][0], runs[1][0])
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0][1], runs[1][1]))
+
+
 def test_two_launch_layer_mixed_batch_widths(llm_tiny_oracle):
     """Sequences decoded under a changing batch schedule (widths 5, 2, 3, 1, 4 ...; a sequence takes different token
     slots from call to call, so every slot's granules and ticket lines see launches of other widths in between) give
