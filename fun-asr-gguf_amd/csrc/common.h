@@ -124,9 +124,13 @@ __device__ __forceinline__ void split_bf16(const float v, __bf16& h, __bf16& l) 
   l = (__bf16)(v - (float)h);
 }
 
-// (value, index) argmax with torch/numpy first-occurrence tie-break (smaller index wins on equal value).
+// (value, index) argmax with torch/numpy semantics: NaN ranks above every number (the first NaN wins, as
+// numpy.argmax), then the larger value, then the smaller index on ties. A total order, so the reduction is order-free
+// and any input replaces the (-inf, INT_MAX) seed: an all-NaN row still yields a real token id, never the seed's
+// out-of-range index (which the sampler's embed-next gather would then read past token_embd with).
 __device__ __forceinline__ void argmax_combine(float& v, int& i, float v2, int i2) {
-  if (v2 > v || (v2 == v && i2 < i) || (v != v)) {
+  const bool vn = v != v, v2n = v2 != v2;
+  if (v2n ? (!vn || i2 < i) : (!vn && (v2 > v || (v2 == v && i2 < i)))) {
     v = v2;
     i = i2;
   }

@@ -3452,6 +3452,7 @@ __global__ __launch_bounds__(SAMPLE_T) void k_sample(const float* __restrict__ l
       tok = S.pick;
     }
   }
+  tok = min(max(tok, 0), V - 1);  // the gather below indexes token_embd with it: never out of range, whatever the logits
   if (en.x) {
     // decode step tail: the next step's input row (D0, f32 token_embd row) and the position advance ride along,
     // so a step is forward + this launch (the row was consumed by the lm_head launch before this one)
