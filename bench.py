@@ -436,6 +436,8 @@ def main():
     ap.add_argument("--c4-steps", type=int, default=2)
     ap.add_argument("--c3-varlen", type=int, default=192, help="clips of the variable-length C3 leg (0 = skip)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 (300 s long-audio) leg")
+    ap.add_argument("--c2-only", action="store_true",
+                    help="the headline leg alone (counter-collection runs, where every dispatch is serialised)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -496,6 +498,7 @@ def main():
         res = step()
         assert res.n_gen == N_GEN, res.n_gen
     m.engine.synchronize()
+    log("[bench] C2 warmup done")
     barrier()
     # ---- timed region (production path: hipGraph decode steps, no timing events)
     t0 = time.perf_counter()
@@ -506,6 +509,7 @@ def main():
         stage += [tm.encode, tm.ctc, tm.prepare, tm.inject, tm.llm_generate, tm.align]
     m.engine.synchronize()
     dt = time.perf_counter() - t0
+    log("[bench] C2 timed steps done")
     barrier()
     # ---- roofline pass: same steps with HIP events on the engine stream around every launch of each
     # kernel class (decode: event nodes captured inside the step graph, replayed on the last step of every
@@ -529,6 +533,14 @@ def main():
     if rank == 0:
         out = headline(args, world, dt, dt_prof, prof, stage)
         out["decode_step_ms_graph"] = step1_ms  # graph-replayed batch-1 step at n_past 208-335 (box-normalised)
+    log("[bench] C2 headline leg done")
+    if args.c2_only:
+        eng.cleanup()
+        if rank == 0:
+            print(json.dumps(out, ensure_ascii=False), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     # ---- C5 leg (configs[4] on one GPU): the same clip with the fp16 encoder graph (02-Quantize-ONNX.py) and the
     # 73-token prefix; the 8-GPU segment-parallel part is the driver's scaling run of the same entry point
     m.engine.set_encoder_fp16(True)
@@ -594,21 +606,25 @@ def main():
                      "stage_ms": {k: round(v / args.steps * 1e3, 3) for k, v in zip(
                          ["encode", "ctc", "prompt", "prefill", "generate", "align"], st5)}}
     eng.cleanup()
+    log("[bench] C5 / sampled / exact-f32 legs done")
     if args.c3_batch > 0:
         try:
             out["c3"] = c3_leg(args.c3_batch, args.c3_steps, 1, local, args.model, barrier, dist)
         except Exception as e:  # reported, never fatal for the headline number
             out["c3"] = {"value": None, "error": str(e)[:300]}
+        log("[bench] C3 leg done")
     if args.c3_varlen > 0:
         try:
             out["c3_varlen"] = c3_varlen_leg(args.c3_varlen, args.c3_batch or 32, local, args.model, barrier, dist)
         except Exception as e:  # reported, never fatal for the headline number
             out["c3_varlen"] = {"value": None, "error": str(e)[:300]}
+        log("[bench] C3 varlen leg done")
     if not args.no_c4:
         try:
             out["c4"] = c4_leg(args.c4_steps, 1, local, args.model, barrier, dist)
         except Exception as e:  # reported, never fatal for the headline number
             out["c4"] = {"value": None, "error": str(e)[:300]}
+        log("[bench] C4 leg done")
         try:
             out["c5_long"] = c5_long_leg(args.c4_steps, 1, local, args.model, barrier, dist)
         except Exception as e:  # reported, never fatal for the headline number

@@ -46,7 +46,7 @@ if [[ " $STEPS " == *" trace32 "* ]]; then  # the graph-replayed batch-32 step's
 fi
 if [[ " $STEPS " == *" pmc "* ]]; then
   export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
-  B="python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --c3-batch 0 --c3-varlen 0 --no-c4"
+  B="python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --c2-only"
   for pf in 0 16; do
     d=gpurun_out/pmc_fetch_pf$pf
     FUNASR_L2PF=$pf timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $d -o run -- $B > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
