@@ -786,7 +786,9 @@ struct Engine {
     enc_attn_wk.cnt = alloc<int>(enc_attn_wk.cnt_n * CNT_LINE);
     FA_HIP(hipMemset(enc_attn_wk.cnt, 0, enc_attn_wk.cnt_n * CNT_LINE * sizeof(int)));
     enc_gemm_wk.cnt_n = 512;
-    enc_gemm_wk.part_n = (int64_t)512 * 256 * 16;  // tiles x splits <= 512
+    // f32 64x64 splits: tiles x splits <= 512 of 256 x 16 floats; bf16x3 128x128 splits (k_gemm_bf3_sk): tiles x
+    // splits <= 256 of 16 x 1024 floats
+    enc_gemm_wk.part_n = std::max<int64_t>((int64_t)512 * 256 * 16, (int64_t)256 * 16 * 1024);
     enc_gemm_wk.part = alloc<float>(enc_gemm_wk.part_n);
     enc_gemm_wk.cnt = alloc<int>(enc_gemm_wk.cnt_n * CNT_LINE);
     FA_HIP(hipMemset(enc_gemm_wk.cnt, 0, enc_gemm_wk.cnt_n * CNT_LINE * sizeof(int)));
@@ -1864,6 +1866,14 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_F16_DEEP")) fa::g_gemm_f16_deep = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_256_S")) fa::g_gemm_bf3_256_s = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_DMA")) fa::g_gemm_bf3_dma = atoi(g) != 0;
+    {  // the few-tile K splits: every creation takes the environment's setting or the default
+      const char* g = getenv("FUNASR_BF3_SK");
+      fa::g_gemm_bf3_sk = g ? atoi(g) != 0 : 1;
+      g = getenv("FUNASR_F16_SK");
+      fa::g_gemm_f16_sk = g ? atoi(g) != 0 : 1;
+      g = getenv("FUNASR_BF3_SK_KS");
+      fa::g_gemm_bf3_sk_ks = g ? std::max(0, std::min(8, atoi(g))) : 0;
+    }
     if (const char* g = getenv("FUNASR_BF3_PERSIST")) fa::g_gemm_bf3_persist = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_ATTN_WAB")) fa::g_attn_wab = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_GEMM_T_WAB")) fa::g_gemm_t_wab = atoi(g) != 0;

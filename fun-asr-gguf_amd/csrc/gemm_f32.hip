@@ -7,6 +7,7 @@
 // power epilogue (F3), the mel projection with a log epilogue, and the CTC projection with a fused
 // row-argmax epilogue (C1) so the [T, 60515] logits never reach HBM.
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 
@@ -863,16 +864,36 @@ __device__ __forceinline__ void store_b3(typename PrecB<P>::E* st, const float4 
   }
 }
 
+// Split-K partial of a 128x128 tile (4 waves as 2 x 2, 2 x 2 accumulators each) for k_gemm_sk_reduce:
+// [split gridDim.z][tile][wave][i][j][q][lane] float4, 1 KiB per wave-instruction
+__device__ __forceinline__ void sk_store_partial_impl(const f32x16& a, float* __restrict__ part, int64_t o) {
+  f32x4_t* dst = reinterpret_cast<f32x4_t*>(part) + o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dst[q * 64] = f32x4_t{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+}
+template <int WM, int WN>
+__device__ __forceinline__ void sk_store_partial(const f32x16 (&acc)[WM][WN], float* __restrict__ part, int tile,
+                                                 int ntiles, int wave, int lane) {
+  static_assert(WM == 2 && WN == 2, "split partials: 128x128 tiles of 4 waves");
+  const int64_t base = ((int64_t)blockIdx.z * ntiles + tile) * (4 * 4 * 16 * 64 / 4) + wave * 16 * 64 + lane;
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) sk_store_partial_impl(acc[i][j], part, base + (i * WN + j) * 4 * 64);
+}
+
 // KW = 2 / 4 (few-tile shapes): KW groups of 4 waves per block split K in equal parts, each with its own LDS stages;
 // groups 1..KW-1 hand their accumulators to group 0 through LDS (summed in a fixed order) and group 0 runs the
 // epilogue. KW times the waves per CU and 1/KW of the dependent k-steps per wave, with no cross-block split-K seam.
 // PF = 2: the global loads run two k-steps ahead (two register sets, the k loop unrolled by two), so a k-step's
 // tile has two steps of compute to land instead of one: few-tile shapes (one clip) have too little work per step to
 // cover the load latency.
-template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1, int P = 3>
+// SPL: gridDim.z splits K (KW = 1, 128x128 tiles): split z covers [z K / KS, (z + 1) K / KS) and stores its
+// accumulators for k_gemm_sk_reduce instead of running the epilogue
+template <class AL, class EPI, int WM, int WN, int KB, int KW = 1, int PF = 1, int P = 3, bool SPL = false>
 __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename PrecB<P>::E* __restrict__ Wh,
                                                        const typename PrecB<P>::E* __restrict__ Wl, int64_t ldw, int M,
-                                                       int N, int K, EPI epi) {
+                                                       int N, int K, EPI epi, float* __restrict__ part) {
   using T = TileB3<WM, WN, KB, P>;
   typedef typename PrecB<P>::E E;
   typedef typename PrecB<P>::V8 V8;
@@ -893,7 +914,8 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
   float4 ra[T::NA];
   uint4 rh[T::NB], rl[T::NB];
-  const int kq = K / KW, kb0 = grp * kq, ke = kb0 + kq;  // host: K % (KW * KB) == 0 when KW > 1
+  const int kz = SPL ? K / (int)gridDim.z : K;  // host: K % (KS * KB) == 0 when split
+  const int kq = kz / KW, kb0 = (SPL ? (int)blockIdx.z * kz : 0) + grp * kq, ke = kb0 + kq;  // K % (KW * KB) == 0, KW > 1
   load_b3<AL, WM, WN, KB, P>(al, Wh, Wl, ldw, m0, n0, kb0, M, N, ke, ra, rh, rl, t);
   store_b3<WM, WN, KB, P, IsPlanes<AL>::value>(sh, ra, rh, rl, t);
   __syncthreads();
@@ -987,6 +1009,12 @@ __global__ __launch_bounds__(256 * KW) void k_gemm_bf3(AL al, const typename Pre
     __syncthreads();  // the epilogue may reuse the LDS
     if (grp > 0) return;
   }
+  if constexpr (SPL) {
+    static_assert(KW == 1, "split partials: one K group");
+    const int nbx = (N + T::BN - 1) / T::BN;
+    sk_store_partial<WM, WN>(acc, part, tm * nbx + tn, nbx * ((M + T::BM - 1) / T::BM), wave, lane);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < WM; ++i)
 #pragma unroll
@@ -1015,7 +1043,7 @@ static void launch_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, in
     attr = true;
   }
   hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, WM, WN, KB, KW, PF, P>), grid, dim3(256 * KW), lds, s, al,
-                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi);
+                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi, nullptr);
 }
 
 // 256x256x32 tile (batched encoder, C3; P = 3 bf16x3, P = 1 the fp16 graph): 8 waves as 2 (M) x 4 (N), each wave
@@ -1364,6 +1392,216 @@ static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t 
                        reinterpret_cast<const __bf16*>(w.lo), ldw, M, N, K, epi);
 }
 
+// ---- few-tile bf16x3 shapes (one clip, M ~ 1000: 32-128 tiles of 128x128): K split over gridDim.z blocks so the
+// launch covers the chip with 128x128 tiles instead of 64x64 ones. The 64x64 tile streams 512 B of operand planes per
+// k for 64 x 64 outputs and its launch was bound by the per-CU L2 fetch rate (MI355X_MICROARCH.md "Indexed rows":
+// 66-73 GB/s per CU; the one-clip ffn2 fetched at ~49 GB/s per CU on half the CUs); the 128x128 tile halves the
+// bytes per output. Operands as bf16 planes (A from its producer's APlanes) staged by LDS-DMA into a ring of NB
+// 32-deep K-tiles, NB - 2 in flight across each barrier (k_gemm_bf3_256d's pipeline; 4 waves as 2 x 2, each
+// 64 x 64 = 2 x 2 accumulators). A DMA wave-instruction fills 16 rows x 64 B (4 lanes per row: a row's 64 B come
+// from one line; 16-deep tiles, 32 B per row, measured 4x slower per byte). Split z covers k in [z K / KS,
+// (z + 1) K / KS); with KS > 1 every split stores its accumulators (plain stores, accumulator layout) and
+// k_gemm_sk_reduce sums them in split order and runs the epilogue: deterministic, no counters, no co-residency (the
+// kernel boundary is the hand-off). Per-element MFMA order inside a split: lo.hi, hi.lo, hi.hi per 16 of k, k
+// ascending (as every bf16x3 tile), so KS = 1 is bit-identical to the unsplit tiles.
+int g_gemm_bf3_sk = 1;  // bf16x3 few-tile K >= 2048 launches split over blocks (k_gemm_bf3_sk / launch_gemm_b3_rs; FUNASR_BF3_SK)
+int g_gemm_f16_sk = 1;  // 1: the fp16 graph's few-tile K >= 2048 launches split over blocks (launch_gemm_b3_rs; FUNASR_F16_SK)
+int g_gemm_bf3_sk_ks = 0;  // microbenchmark hook: force the K split (1, 2, 4, 8)
+constexpr int SK_KB = 32;
+constexpr int SK_PLANE = 128 * SK_KB;  // bf16 per plane per buffer (8 KiB = 8 DMA wave-instructions)
+constexpr int SK_BUF = 4 * SK_PLANE;   // one K-tile: [Ah][Al][Wh][Wl] (32 KiB)
+constexpr int SK_KS_MAX = 8;
+constexpr int64_t SK_UNIT = 4 * 4 * 16 * 64;  // floats per (tile, split): 4 waves x 4 accumulators x 16 x 64 lanes
+
+__device__ __forceinline__ void sk_wait(int ahead) {  // retire all but `ahead` K-tiles of this wave's DMA (8 each)
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <class EPI, bool SPLIT>
+__global__ __launch_bounds__(256) void k_gemm_bf3_sk(ALoadPlanes al, const __bf16* __restrict__ Wh,
+                                                     const __bf16* __restrict__ Wl, int64_t ldw, int M, int N, int K,
+                                                     EPI epi, float* __restrict__ part) {
+  constexpr int WM = 2, WN = 2, NB = 4;  // 4 x 32 KiB ring, two K-tiles in flight (sk_wait)
+  extern __shared__ float smem[];  // the ring; the epilogue reuses it
+  const int nbx = (N + 127) / 128, nby = (M + 127) / 128;
+  int tm, tn;
+  if (!xcd_tile(nbx, nby, tm, tn)) return;
+  const int m0 = tm * 128, n0 = tn * 128;
+  const int kper = SPLIT ? K / (int)gridDim.z : K;  // host: K % (KS * 32) == 0
+  const int kb0 = SPLIT ? (int)blockIdx.z * kper : 0;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+  __bf16* ring = reinterpret_cast<__bf16*>(smem);
+  // DMA: wave w fills plane w (0 Ah, 1 Al, 2 Wh, 3 Wl) in 8 wave-instructions of 16 rows; lane s -> row
+  // 16 i + (s >> 2), LDS chunk s & 3 holding source chunk (s & 3) ^ ((s >> 4) & 3) (the bank swizzle of that row,
+  // undone on the read: the 16 rows a 16-lane fragment read touches then hit 16 distinct 16-B slots)
+  const int koff = 8 * ((lane & 3) ^ ((lane >> 4) & 3));
+  const __bf16* base;
+  int64_t ld;
+  if (wave < 2) {
+    base = reinterpret_cast<const __bf16*>(wave == 0 ? al.hi : al.lo);
+    ld = al.lda;
+  } else {
+    base = wave == 2 ? Wh : Wl;
+    ld = ldw;
+  }
+  const int lim = (wave < 2 ? M : N) - 1, r0 = wave < 2 ? m0 : n0;
+  const __bf16* src[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)  // rows past M / N: clamped (their products reach no stored output)
+    src[i] = base + (int64_t)min(r0 + 16 * i + (lane >> 2), lim) * ld + kb0 + koff;
+  auto issue = [&](int kt) {
+    __bf16* d = ring + (kt % NB) * SK_BUF + wave * SK_PLANE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src[i] + kt * SK_KB),
+                                       (__attribute__((address_space(3))) void*)(d + i * 16 * SK_KB), 16, 0, 0);
+  };
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  const int nk = kper / SK_KB;
+  const int sw = (r >> 2) & 3;  // fragment rows differ from r by multiples of 32: one swizzle for all of them
+  const int fa = (wr * 64 + r) * SK_KB, fb = 2 * SK_PLANE + (wc * 64 + r) * SK_KB;
+  for (int s = 0; s < NB - 1 && s < nk; ++s) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire tile kt (tiles kt + 1, kt + 2 stay in flight); the barrier then frees buffer (kt - 1) % NB
+    sk_wait(min(NB - 2, nk - 1 - kt));
+    asm volatile("s_barrier" ::: "memory");
+    if (kt + NB - 1 < nk) issue(kt + NB - 1);
+    const __bf16* b = ring + (kt % NB) * SK_BUF;
+#pragma unroll
+    for (int kk = 0; kk < SK_KB / 16; ++kk) {
+      const int c = 8 * ((2 * kk + h) ^ sw);
+      bf16x8 ah[WM], alo[WM], bh[WN], blo[WN];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(b + fb + 32 * j * SK_KB + c);
+        blo[j] = *reinterpret_cast<const bf16x8*>(b + fb + SK_PLANE + 32 * j * SK_KB + c);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        ah[i] = *reinterpret_cast<const bf16x8*>(b + fa + 32 * i * SK_KB + c);
+        alo[i] = *reinterpret_cast<const bf16x8*>(b + fa + SK_PLANE + 32 * i * SK_KB + c);
+      }
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) mma_step<3>(acc[i][j], ah[i], alo[i], bh[j], blo[j]);
+    }
+  }
+  if constexpr (SPLIT) {
+    sk_store_partial<WM, WN>(acc, part, tm * nbx + tn, nbx * nby, wave, lane);
+  } else {
+    __syncthreads();  // every wave's last fragment reads done before an epilogue reuses the LDS (no DMA in flight)
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) epi.apply(acc[i][j], m0 + (wr * WM + i) * 32, n0 + (wc * WN + j) * 32, M, N, smem);
+    epi.finish(m0, n0, M, N, smem);
+  }
+}
+
+// one wave per (tile, wave, i, j) accumulator of k_gemm_bf3_sk: the KS split partials summed in split order, then the
+// epilogue on the same (row0, col0) the unsplit kernel would give it (EpiLinear: no LDS, no block-wide finish)
+template <class EPI>
+__global__ __launch_bounds__(256) void k_gemm_sk_reduce(const float* __restrict__ part, int KS, int nbx, int ntiles,
+                                                        int M, int N, EPI epi) {
+  const int u = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (u >= ntiles * 16) return;
+  const int tile = u >> 4, wave = (u >> 2) & 3, ij = u & 3;
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(part) + (int64_t)u * 4 * 64 + lane;
+  const int64_t zs = (int64_t)ntiles * SK_UNIT / 4;  // float4 per split
+  f32x4_t p[SK_KS_MAX][4];
+#pragma unroll
+  for (int z = 0; z < SK_KS_MAX; ++z)  // all in flight; clamped duplicates past KS are not summed
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p[z][q] = src[min(z, KS - 1) * zs + q * 64];
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4_t v = p[0][q];
+#pragma unroll
+    for (int z = 1; z < SK_KS_MAX; ++z)
+      if (z < KS) v += p[z][q];
+    acc[4 * q] = v.x; acc[4 * q + 1] = v.y; acc[4 * q + 2] = v.z; acc[4 * q + 3] = v.w;
+  }
+  const int tm = tile / nbx, tn = tile - tm * nbx;
+  epi.apply(acc, tm * 128 + (wave >> 1) * 64 + (ij >> 1) * 32, tn * 128 + (wave & 1) * 64 + (ij & 1) * 32, M, N,
+            nullptr);
+}
+
+// K split of a few-tile launch: the largest power of two <= SK_KS_MAX with tiles x KS <= 256 (one block per CU) and
+// >= 64 of k per split; 0 = not this kernel (workspace too small, K not divisible, or enough tiles already)
+static int sk_splits(int64_t tiles, int K, const GemmF32Work* wk) {
+  int ks = g_gemm_bf3_sk_ks;
+  if (!ks) {
+    ks = 1;
+    while (ks < SK_KS_MAX && tiles * ks * 2 <= 256 && K % (ks * 2 * SK_KB) == 0 && K / (ks * 2) >= 64) ks *= 2;
+  }
+  if (K % (ks * SK_KB)) return 0;
+  if (ks > 1 && (!wk || !wk->part || tiles * ks * SK_UNIT > wk->part_n)) return 0;
+  return ks;
+}
+
+template <class EPI>
+static bool launch_gemm_b3_sk(const ALoadPlanes& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                              hipStream_t s, const GemmF32Work* wk) {
+  constexpr size_t lds = (size_t)4 * SK_BUF * 2;
+  const int nbx = cdiv(N, 128), nby = cdiv(M, 128);
+  const int ks = sk_splits((int64_t)nbx * nby, K, wk);
+  if (ks == 0) return false;
+  static bool attr = false;
+  if (!attr) {
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_sk<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    FA_HIP(hipFuncSetAttribute((const void*)k_gemm_bf3_sk<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    attr = true;
+  }
+  const auto* wh = reinterpret_cast<const __bf16*>(w.hi);
+  const auto* wl = reinterpret_cast<const __bf16*>(w.lo);
+  if (ks == 1) {
+    hipLaunchKernelGGL((k_gemm_bf3_sk<EPI, false>), xcd_grid(nbx, nby), dim3(256), lds, s, al, wh, wl, ldw, M, N, K,
+                       epi, nullptr);
+    return true;
+  }
+  hipLaunchKernelGGL((k_gemm_bf3_sk<EPI, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al, wh, wl, ldw, M, N, K,
+                     epi, wk->part);
+  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(cdiv(nbx * nby * 16, 4)), dim3(256), 0, s, wk->part, ks, nbx,
+                     nbx * nby, M, N, epi);
+  return true;
+}
+
+// the same split over the register-staged 128x128x32 tile (k_gemm_bf3 <2, 2, 32>, write-after-barrier staging): any A
+// operand (planes or f32) and both precisions (P = 1: the fp16 graph)
+template <class AL, class EPI, int P>
+static bool launch_gemm_b3_rs(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
+                              hipStream_t s, const GemmF32Work* wk) {
+  const int nbx = cdiv(N, 128), nby = cdiv(M, 128);
+  const int ks = sk_splits((int64_t)nbx * nby, K, wk);
+  if (ks == 0) return false;
+  using T = TileB3<2, 2, 32, P>;
+  typedef typename PrecB<P>::E E;
+  const size_t lds = (size_t)2 * T::STAGE * 2;
+  static bool attr = false;
+  if (!attr && lds > 65536) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_bf3<AL, EPI, 2, 2, 32, 1, 3, P, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, 2, 2, 32, 1, 3, P, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al,
+                     reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi, wk->part);
+  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(cdiv(nbx * nby * 16, 4)), dim3(256), 0, s, wk->part, ks, nbx,
+                     nbx * nby, M, N, epi);
+  return true;
+}
+
 template <class AL, class EPI, int P = 3>
 static void launch_gemm_b3_256(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi,
                                hipStream_t s) {
@@ -1391,8 +1629,22 @@ int gemm_bf3_occupancy_128() {
 
 // P = 3: bf16x3 planes (w.hi, w.lo); P = 1: the fp16 graph (w.hi = the fp16 weight copy)
 template <class AL, class EPI, int P = 3>
-static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s) {
+static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N, int K, const EPI& epi, hipStream_t s,
+                        const GemmF32Work* wk = nullptr) {
   const int f = g_gemm_bf3_force;
+  // few-tile linear launches with K >= 2048 (one clip's ffn2): 128x128 tiles, the K split over blocks. Planes-A
+  // bf16x3 on the LDS-DMA tile (k_gemm_bf3_sk), f32-A bf16x3 and the fp16 graph on the register-staged one
+  // (launch_gemm_b3_rs): both tiles run the same per-element MFMA order and split, so bf16x3 stays bit-identical
+  // between planes and f32 rows
+  if constexpr (std::is_same<EPI, EpiLinear>::value) {
+    const bool few = f == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) <= 128 && K >= 2048;
+    if (M > 0 && N > 0) {
+      if constexpr (IsPlanes<AL>::value && P == 3)
+        if ((f == 11 || (few && g_gemm_bf3_sk)) && launch_gemm_b3_sk(al, w, ldw, M, N, K, epi, s, wk)) return;
+      const bool rs = few && (P == 1 ? g_gemm_f16_sk != 0 : (g_gemm_bf3_sk != 0 && !IsPlanes<AL>::value));
+      if ((f == 12 || rs) && launch_gemm_b3_rs<AL, EPI, P>(al, w, ldw, M, N, K, epi, s, wk)) return;
+    }
+  }
   const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
   const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   const bool pf = g_gemm_bf3_pf > 1;
@@ -1460,12 +1712,13 @@ void gemm_linear(const float* A, int64_t lda, const float* W, int64_t ldw, const
   }
   if (ap.hi) {
     FA_REQUIRE(lda % 8 == 0 && K % 8 == 0, "gemm_linear: A planes need lda % 8 == 0 and K % 8 == 0");
-    run_gemm_b3(ALoadPlanes{ap.hi, ap.lo, lda}, wb, ldw, M, N, K, epi, s);
+    run_gemm_b3(ALoadPlanes{ap.hi, ap.lo, lda}, wb, ldw, M, N, K, epi, s, wk);
     return;
   }
-  if (W16 && g_gemm_f16_b3) run_gemm_b3<ALoadPlain, EpiLinear, 1>(al, WSplit{reinterpret_cast<const uint16_t*>(W16)}, ldw, M, N, K, epi, s);
+  if (W16 && g_gemm_f16_b3)
+    run_gemm_b3<ALoadPlain, EpiLinear, 1>(al, WSplit{reinterpret_cast<const uint16_t*>(W16)}, ldw, M, N, K, epi, s, wk);
   else if (W16) run_gemm16(al, W16, ldw, M, N, K, epi, s);
-  else if (wb.hi) run_gemm_b3(al, wb, ldw, M, N, K, epi, s);
+  else if (wb.hi) run_gemm_b3(al, wb, ldw, M, N, K, epi, s, wk);
   else run_gemm(al, W, ldw, M, N, K, epi, s, true, wk);
 }
 

@@ -41,6 +41,9 @@ extern int g_attn_wab;  // k_attn_bf3: 1 = write-after-barrier K/V staging
 extern int g_gemm_bf3_256_s;  // 256x256 tile: 1 = write-after-barrier staging
 extern int g_gemm_bf3_persist;  // 256x256 tiles as persistent blocks, one per CU (A/B, default 0)
 extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gemm_bf3_256d; default 0: measured slower)
+extern int g_gemm_bf3_sk;     // bf16x3 few-tile K >= 2048 linear GEMMs: 128x128 tiles, K split over blocks (default 1)
+extern int g_gemm_f16_sk;     // fp16 graph: the same split on the register-staged 128x128 tile (default 1)
+extern int g_gemm_bf3_sk_ks;  // force the K split of k_gemm_bf3_sk launches (0 = automatic)
 extern int g_gemm_f16_deep;  // fp16 one-clip GEMMs on 128-deep stages (default 1)
 extern int g_gemm_bf3_kw4;  // 1: four K groups per block for few-tile K >= 2048 shapes (FUNASR_BF3_KW4)
 extern int g_gemm_bf3_mid;  // 1: 128x64 tiles for one clip's 256-1024-tile GEMM shapes (A/B, default 0)

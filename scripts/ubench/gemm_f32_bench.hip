@@ -12,6 +12,7 @@ extern int g_gemm_bf3_force;
 extern int g_gemm_bf3_256_s;
 int gemm_bf3_occupancy_128();
 extern int g_gemm_ks_force;
+extern int g_gemm_bf3_sk_ks;
 void set_error(const std::string& m) { printf("error: %s\n", m.c_str()); }
 void log(int, const std::string&) {}
 }
@@ -102,6 +103,53 @@ int main(int argc, char** argv) {
     }
   }
   g_gemm_bf3_force = 0;
+  if (argc > 1 && std::string(argv[1]) == "sk") {  // few-tile planes-A shapes: 64x64 K groups vs k_gemm_bf3_sk (force 11)
+    uint16_t *Ah, *Al;
+    CK(hipMalloc(&Ah, (size_t)Mmax * Kmax * 2)); CK(hipMalloc(&Al, (size_t)Mmax * Kmax * 2));
+    float* R;  // residual operand (EpiLinear add1)
+    CK(hipMalloc(&R, (size_t)Mmax * Nmax * 4));
+    launch_synth_fill(R, (int64_t)Mmax * Nmax, 4, 0.5f, 0.f, s);
+    GemmF32Work big = wk;  // the engine's workspace after this change: 256 (tile, split) units
+    big.part_n = (int64_t)256 * 16 * 1024;
+    CK(hipMalloc(&big.part, big.part_n * 4));
+    struct Sh { const char* name; int N, K; };
+    const Sh sh4[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
+    const int Ms[] = {1001, 733, 2002};
+    for (int M : Ms)
+      for (const Sh& sh : sh4) {
+        launch_split_bf16(A, Ah, Al, (int64_t)M * sh.K, s);  // A rows of stride K as planes
+        APlanes ap; ap.hi = Ah; ap.lo = Al;
+        auto run = [&](int f, int ks) {
+          g_gemm_bf3_force = f;
+          g_gemm_bf3_sk_ks = ks;
+          gemm_linear(nullptr, sh.K, W, sh.K, bias, C, sh.N, M, sh.N, sh.K, 0, R, sh.N, nullptr, 0, s, nullptr, &big, wb, ap);
+        };
+        std::vector<float> c0((size_t)M * sh.N), c1(c0.size());
+        run(0, 0);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(c0.data(), C, c0.size() * 4, hipMemcpyDeviceToHost));
+        printf("M=%5d %-9s:", M, sh.name);
+        const double t0 = time_graph([&] { run(0, 0); }, 50);
+        printf(" default %6.1f us", t0);
+        for (int fv : {11, 12})
+        for (int ks : {0, 1, 2, 4, 8}) {
+          if (ks && sh.K % (ks * 32)) continue;
+          CK(hipMemsetAsync(C, 0, c1.size() * 4, s));
+          run(fv, ks);
+          CK(hipStreamSynchronize(s));
+          CK(hipGetLastError());
+          CK(hipMemcpy(c1.data(), C, c1.size() * 4, hipMemcpyDeviceToHost));
+          double e = 0, mx = 0;
+          for (size_t i = 0; i < c0.size(); ++i) { e = std::max(e, (double)std::fabs(c0[i] - c1[i])); mx = std::max(mx, (double)std::fabs(c0[i])); }
+          const double us = time_graph([&] { run(fv, ks); }, 50);
+          printf("  %s ks%d %6.1f us (dev %.0e%s)", fv == 11 ? "dma" : "reg", ks, us, e / mx, e / mx < 1e-5 ? "" : " FAIL");
+        }
+        printf("\n");
+      }
+    g_gemm_bf3_force = 0;
+    g_gemm_bf3_sk_ks = 0;
+    return 0;
+  }
   if (argc > 1 && std::string(argv[1]) == "sched") {  // 256x256 staging schedules A/B, interleaved rounds, M = 32032
     struct Sh { const char* name; int N, K; };
     const Sh sh4[] = {{"sanm qkv", 1536, 512}, {"sanm out", 512, 512}, {"ffn1", 2048, 512}, {"ffn2", 512, 2048}};
