@@ -193,6 +193,47 @@ struct EpiLinear {
       }
     }
   }
+  // registers 4 q .. 4 q + 3 of the accumulator apply() receives (rows row0 + 8 q + {0..3} + 4 (lane >> 5)), with
+  // apply()'s arithmetic per element (k_gemm_sk_reduce: one wave per quarter of an accumulator)
+  __device__ __forceinline__ void apply4(const f32x4_t& a, int q, int row0, int col0, int M, int N) const {
+    const int lane = threadIdx.x & 63;
+    const int col = col0 + (lane & 31);
+    const int rb = row0 + 8 * q + 4 * (lane >> 5);
+    if (ph) {
+      const bool cin = col < N;
+      const float b = bias && cin ? bias[col] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int row = rb + t;
+        const bool in = cin && row < M;
+        float v = a[t] + b;
+        if (relu) v = fmaxf(v, 0.f);
+        if (add2 && in) v = v + add2[(int64_t)row * ld2 + col];
+        if (add1 && in) v = add1[(int64_t)row * ld1 + col] + v;
+        __bf16 h, l;
+        split_bf16(v, h, l);
+        const float mine = __uint_as_float(((uint32_t)__builtin_bit_cast(unsigned short, l) << 16) | __builtin_bit_cast(unsigned short, h));
+        const uint32_t other = __float_as_uint(__shfl_xor(mine, 1, 64));
+        const uint32_t me = __float_as_uint(mine);
+        const uint32_t word = (lane & 1) ? ((other >> 16) | (me & 0xffff0000u)) : ((me & 0xffffu) | (other << 16));
+        if (in) *reinterpret_cast<uint32_t*>((lane & 1) ? pl + (int64_t)row * ldc + col - 1 : ph + (int64_t)row * ldc + col) = word;
+      }
+      return;
+    }
+    if (col >= N) return;
+    const float b = bias ? r16v(bias[col], r16) : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int row = rb + t;
+      if (row < M) {
+        float v = r16v(a[t] + b, r16);
+        if (relu) v = fmaxf(v, 0.f);
+        if (add2) v = r16v(v + add2[(int64_t)row * ld2 + col], r16);
+        if (add1) v = r16v(add1[(int64_t)row * ld1 + col] + v, r16);
+        C[(int64_t)row * ldc + col] = v;
+      }
+    }
+  }
 };
 
 // STFT: W rows interleave (cos_f, -sin_f); power[row][f] = re^2 + im^2 (model_definition.py:287).
@@ -1406,6 +1447,7 @@ static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t 
 // ascending (as every bf16x3 tile), so KS = 1 is bit-identical to the unsplit tiles.
 int g_gemm_bf3_sk = 1;  // bf16x3 few-tile K >= 2048 launches split over blocks (k_gemm_bf3_sk / launch_gemm_b3_rs; FUNASR_BF3_SK)
 int g_gemm_f16_sk = 1;  // 1: the fp16 graph's few-tile K >= 2048 launches split over blocks (launch_gemm_b3_rs; FUNASR_F16_SK)
+int g_gemm_bf3_sk_kmin = 2048;  // smallest K split over blocks (FUNASR_BF3_SK_KMIN; A/B)
 int g_gemm_bf3_sk_ks = 0;  // microbenchmark hook: force the K split (1, 2, 4, 8)
 constexpr int SK_KB = 32;
 constexpr int SK_PLANE = 128 * SK_KB;  // bf16 per plane per buffer (8 KiB = 8 DMA wave-instructions)
@@ -1507,33 +1549,27 @@ __global__ __launch_bounds__(256) void k_gemm_bf3_sk(ALoadPlanes al, const __bf1
   }
 }
 
-// one wave per (tile, wave, i, j) accumulator of k_gemm_bf3_sk: the KS split partials summed in split order, then the
-// epilogue on the same (row0, col0) the unsplit kernel would give it (EpiLinear: no LDS, no block-wide finish)
+// one wave per quarter (4 registers) of a (tile, wave, i, j) accumulator of the split tiles: the KS split partials
+// summed in split order, then EpiLinear's arithmetic on the rows / column the unsplit kernel gives those registers
 template <class EPI>
 __global__ __launch_bounds__(256) void k_gemm_sk_reduce(const float* __restrict__ part, int KS, int nbx, int ntiles,
                                                         int M, int N, EPI epi) {
-  const int u = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (u >= ntiles * 16) return;
+  // block b -> a unit of a tile the split launch ran on XCD b % 8 (xcd_tile's order): its partials are in that L2
+  const int per = (ntiles + 7) >> 3, b = blockIdx.x, u = (b & 7) * per * 16 + (b >> 3);
+  if ((b >> 3) >= per * 16 || u >= ntiles * 16) return;
+  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tile = u >> 4, wave = (u >> 2) & 3, ij = u & 3;
-  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(part) + (int64_t)u * 4 * 64 + lane;
+  const f32x4_t* src = reinterpret_cast<const f32x4_t*>(part) + ((int64_t)u * 4 + q) * 64 + lane;
   const int64_t zs = (int64_t)ntiles * SK_UNIT / 4;  // float4 per split
-  f32x4_t p[SK_KS_MAX][4];
+  f32x4_t p[SK_KS_MAX];
 #pragma unroll
-  for (int z = 0; z < SK_KS_MAX; ++z)  // all in flight; clamped duplicates past KS are not summed
+  for (int z = 0; z < SK_KS_MAX; ++z) p[z] = src[min(z, KS - 1) * zs];  // clamped duplicates past KS: not summed
+  f32x4_t v = p[0];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) p[z][q] = src[min(z, KS - 1) * zs + q * 64];
-  f32x16 acc;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x4_t v = p[0][q];
-#pragma unroll
-    for (int z = 1; z < SK_KS_MAX; ++z)
-      if (z < KS) v += p[z][q];
-    acc[4 * q] = v.x; acc[4 * q + 1] = v.y; acc[4 * q + 2] = v.z; acc[4 * q + 3] = v.w;
-  }
+  for (int z = 1; z < SK_KS_MAX; ++z)
+    if (z < KS) v += p[z];
   const int tm = tile / nbx, tn = tile - tm * nbx;
-  epi.apply(acc, tm * 128 + (wave >> 1) * 64 + (ij >> 1) * 32, tn * 128 + (wave & 1) * 64 + (ij & 1) * 32, M, N,
-            nullptr);
+  epi.apply4(v, q, tm * 128 + (wave >> 1) * 64 + (ij >> 1) * 32, tn * 128 + (wave & 1) * 64 + (ij & 1) * 32, M, N);
 }
 
 // K split of a few-tile launch: the largest power of two <= SK_KS_MAX with tiles x KS <= 256 (one block per CU) and
@@ -1573,7 +1609,7 @@ static bool launch_gemm_b3_sk(const ALoadPlanes& al, const WSplit& w, int64_t ld
   }
   hipLaunchKernelGGL((k_gemm_bf3_sk<EPI, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al, wh, wl, ldw, M, N, K,
                      epi, wk->part);
-  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(cdiv(nbx * nby * 16, 4)), dim3(256), 0, s, wk->part, ks, nbx,
+  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(((nbx * nby + 7) >> 3) * 8 * 16), dim3(256), 0, s, wk->part, ks, nbx,
                      nbx * nby, M, N, epi);
   return true;
 }
@@ -1597,7 +1633,7 @@ static bool launch_gemm_b3_rs(const AL& al, const WSplit& w, int64_t ldw, int M,
   }
   hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, 2, 2, 32, 1, 3, P, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al,
                      reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi, wk->part);
-  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(cdiv(nbx * nby * 16, 4)), dim3(256), 0, s, wk->part, ks, nbx,
+  hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(((nbx * nby + 7) >> 3) * 8 * 16), dim3(256), 0, s, wk->part, ks, nbx,
                      nbx * nby, M, N, epi);
   return true;
 }
@@ -1637,7 +1673,7 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   // (launch_gemm_b3_rs): both tiles run the same per-element MFMA order and split, so bf16x3 stays bit-identical
   // between planes and f32 rows
   if constexpr (std::is_same<EPI, EpiLinear>::value) {
-    const bool few = f == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) <= 128 && K >= 2048;
+    const bool few = f == 0 && (int64_t)cdiv(M, 128) * cdiv(N, 128) <= 128 && K >= g_gemm_bf3_sk_kmin;
     if (M > 0 && N > 0) {
       if constexpr (IsPlanes<AL>::value && P == 3)
         if ((f == 11 || (few && g_gemm_bf3_sk)) && launch_gemm_b3_sk(al, w, ldw, M, N, K, epi, s, wk)) return;
