@@ -1607,6 +1607,7 @@ static bool launch_gemm_b3_sk(const ALoadPlanes& al, const WSplit& w, int64_t ld
                        epi, nullptr);
     return true;
   }
+  FA_REQUIRE(wk && wk->part && (int64_t)nbx * nby * ks * SK_UNIT <= wk->part_n, "gemm_bf3_sk: split workspace");
   hipLaunchKernelGGL((k_gemm_bf3_sk<EPI, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al, wh, wl, ldw, M, N, K,
                      epi, wk->part);
   hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(((nbx * nby + 7) >> 3) * 8 * 16), dim3(256), 0, s, wk->part, ks, nbx,
@@ -1622,6 +1623,10 @@ static bool launch_gemm_b3_rs(const AL& al, const WSplit& w, int64_t ldw, int M,
   const int nbx = cdiv(N, 128), nby = cdiv(M, 128);
   const int ks = sk_splits((int64_t)nbx * nby, K, wk);
   if (ks == 0) return false;
+  if (ks == 1) {  // no split: the unsplit tile and its epilogue (sk_splits sized no workspace for it)
+    launch_gemm_b3<AL, EPI, 2, 2, 32, 1, 3, P>(al, w, ldw, M, N, K, epi, s);
+    return true;
+  }
   using T = TileB3<2, 2, 32, P>;
   typedef typename PrecB<P>::E E;
   const size_t lds = (size_t)2 * T::STAGE * 2;
@@ -1631,6 +1636,7 @@ static bool launch_gemm_b3_rs(const AL& al, const WSplit& w, int64_t ldw, int M,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
+  FA_REQUIRE(wk && wk->part && (int64_t)nbx * nby * ks * SK_UNIT <= wk->part_n, "gemm_bf3 split: workspace");
   hipLaunchKernelGGL((k_gemm_bf3<AL, EPI, 2, 2, 32, 1, 3, P, true>), xcd_grid(nbx, nby, ks), dim3(256), lds, s, al,
                      reinterpret_cast<const E*>(w.hi), reinterpret_cast<const E*>(w.lo), ldw, M, N, K, epi, wk->part);
   hipLaunchKernelGGL(k_gemm_sk_reduce<EPI>, dim3(((nbx * nby + 7) >> 3) * 8 * 16), dim3(256), 0, s, wk->part, ks, nbx,
