@@ -86,6 +86,70 @@ __device__ __forceinline__ void store_o4(const float4 v, float* __restrict__ O, 
   *reinterpret_cast<bf16x4_t*>(op.lo + off) = l;
 }
 
+// Merge of a query tile's KS split partials (m, l, O), queries [qa, qa + nq) of the tile: merged max / sum per query
+// and each split's weight exp(m_k - m) -> LDS, with every split's (m, l) load in flight at once; then the weighted sum
+// of the splits' O, KSM loads per output in flight (clamped duplicates past KS carry weight 0). Shared by the
+// last-arriving split (qa = 0, nq = AQ) and k_attn_merge (a slice of the tile per block): the same arithmetic.
+template <int D>
+__device__ __forceinline__ void attn_merge_rows(const __amdgpu_buffer_rsrc_t rs, float* lds, float* s_l, int qa, int nq,
+                                                float* __restrict__ O, int64_t ldo, int64_t row_base, int head, int q0,
+                                                int t_stride, int KS, int r16, const APlanesD& op) {
+  constexpr int PSZ = AQ * D + 2 * AQ;  // floats per split partial
+  constexpr int D4 = D / 4;
+  constexpr int KSM = 8;
+  float* s_w = lds;  // [KSM][AQ]
+  if ((int)threadIdx.x < nq) {
+    const int q = qa + threadIdx.x;
+    f4v ml[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) ml[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + AQ * D + 2 * (q & ~1)) * 4);
+    float mm = -INFINITY;
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2)
+      if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
+    float ll = 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) {
+      const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
+      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
+      ll += w * lk;
+      s_w[k2 * AQ + q] = w;
+    }
+    s_l[q] = ll;
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < nq * D4; f += 256) {
+    const int q = qa + f / D4, d4 = f % D4;
+    if (q0 + q >= t_stride) continue;
+    f4v pv[KSM];
+#pragma unroll
+    for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
+    f4v acc = s_w[q] * pv[0];
+#pragma unroll
+    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
+    const float inv = 1.0f / s_l[q];
+    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    if (r16) v = round_f16x4(v);
+    store_o4(v, O, op, (row_base + q0 + q) * ldo + head * D + 4 * d4);
+  }
+}
+
+// The merge of every key-split tile as its own launch (attn_f32 with g_attn_merge): block (slice, tile) merges AQ / MS
+// queries of one tile, so the 512 KB of split partials per tile are read by MS blocks instead of the last split alone
+int g_attn_ms = 8;  // query slices per tile (FUNASR_ATTN_MS: 1, 2, 4, 8, 16 or 32)
+template <int D>
+__global__ __launch_bounds__(256) void k_attn_merge(const float* __restrict__ part, int KS, int n_qt, int n_heads,
+                                                    float* __restrict__ O, int64_t ldo, int t_stride, int r16,
+                                                    APlanesD op, int ms) {
+  __shared__ float lds[8 * AQ + AQ];
+  constexpr int PSZ = AQ * D + 2 * AQ;
+  const int slice = blockIdx.x % ms, tile = blockIdx.x / ms;
+  const int qt = tile % n_qt, head = (tile / n_qt) % n_heads, clip = tile / (n_qt * n_heads);
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(part + (int64_t)tile * KS * PSZ, KS * PSZ * 4);
+  attn_merge_rows<D>(rs, lds, lds + 8 * AQ, slice * (AQ / ms), AQ / ms, O, ldo, (int64_t)clip * t_stride,
+                     head, qt * AQ, t_stride, KS, r16, op);
+}
+
 // The block's epilogue, shared by the exact-f32 and the bf16x3 kernels: O^T (d on registers, q on lanes) -> LDS [q][d]
 // for row-contiguous stores; with key splits, publish (m, l, O) and let the last split merge.
 template <int D>
@@ -143,51 +207,14 @@ __device__ __forceinline__ void attn_epilogue(const f32x16 (&o)[D / 32], float m
     const f4v v = {s_m[q], s_l[q], s_m[q + 1], s_l[q + 1]};
     st_sc1_f4(v, rs, (ks * PSZ + AQ * D + 2 * q) * 4);
   }
+  if (!cnt) return;  // merged by k_attn_merge (the kernel boundary is the hand-off)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
     *s_flag = __hip_atomic_fetch_add(cnt + tile * CNT_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == KS - 1;
   __syncthreads();
   if (!*s_flag) return;
-  // merged max / sum per query and each split's weight exp(m_k - m) -> LDS (the O staging area is free now), with
-  // every split's (m, l) load in flight at once; then the weighted sum of the splits' O, KSM loads per output in
-  // flight (clamped duplicates past KS carry weight 0)
-  constexpr int KSM = 8;
-  float* s_w = lds;  // [KSM][AQ]
-  if (threadIdx.x < AQ) {
-    const int q = threadIdx.x;
-    f4v ml[KSM];
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) ml[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + AQ * D + 2 * (q & ~1)) * 4);
-    float mm = -INFINITY;
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2)
-      if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
-    float ll = 0.f;
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) {
-      const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
-      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
-      ll += w * lk;
-      s_w[k2 * AQ + q] = w;
-    }
-    s_l[q] = ll;
-  }
-  __syncthreads();
-  for (int f = threadIdx.x; f < AQ * D4; f += 256) {
-    const int q = f / D4, d4 = f % D4;
-    if (q0 + q >= t_stride) continue;
-    f4v pv[KSM];
-#pragma unroll
-    for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
-    f4v acc = s_w[q] * pv[0];
-#pragma unroll
-    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
-    const float inv = 1.0f / s_l[q];
-    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
-    if (r16) v = round_f16x4(v);
-    store_o4(v, O, op, (row_base + q0 + q) * ldo + head * D + 4 * d4);
-  }
+  attn_merge_rows<D>(rs, lds, s_l, 0, AQ, O, ldo, row_base, head, q0, t_stride, KS, r16, op);
   if (threadIdx.x == 0) __hip_atomic_store(cnt + tile * CNT_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -651,6 +678,7 @@ int g_attn_f32_force_splits = 0;  // test hook (scripts/ubench/attn_f32_check.hi
 int g_attn_f16_mfma = 1;          // fp16 graph attention on f16 MFMAs (k_attn_bf3<D, 1>); 0: exact f32 + rounding (A/B)
 int g_attn_wab = 0;               // k_attn_bf3 write-after-barrier staging (S = 1; FUNASR_ATTN_WAB)
 int g_attn_xcd = 0;               // k_attn_bf3 XCD-aware block order (FUNASR_ATTN_XCD=1; measured neutral: off)
+int g_attn_merge = 1;             // key splits merged by their own launch (k_attn_merge) instead of the last split
 
 template <int D, int P>
 static void launch_attn_bf3(dim3 grid, hipStream_t s, const float* Q, const float* K, const float* V, int64_t ldq,
@@ -694,6 +722,22 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
                "attn_f32: split workspace too small");
   dim3 grid(KS == 1 ? cdiv(t_stride, AQ) : ((cdiv(t_stride, AQ) + 7) & ~7) * KS, n_heads, batch);
   const float scale = (float)std::pow((double)head_dim, -0.5);  // python d_k ** -0.5 rounded to f32
+  // g_attn_merge: the splits only publish (no counter: cnt = nullptr) and k_attn_merge merges every tile after them
+  const bool sep = KS > 1 && g_attn_merge;
+  AttnF32Work wka = wk;
+  if (sep) wka.cnt = nullptr;
+  auto merge = [&]() {
+    if (!sep) return;
+    const int n_qt = cdiv(t_stride, AQ);
+    const int r16m = r16 ? 1 : 0;
+    const int ms = (g_attn_ms >= 1 && g_attn_ms <= 32 && AQ % g_attn_ms == 0) ? g_attn_ms : 8;
+    if (head_dim == 128)
+      hipLaunchKernelGGL(k_attn_merge<128>, dim3(n_tiles * ms), dim3(256), 0, s, wk.part, KS, n_qt, n_heads, O,
+                         ldo, t_stride, r16m, opd, ms);
+    else
+      hipLaunchKernelGGL(k_attn_merge<64>, dim3(n_tiles * ms), dim3(256), 0, s, wk.part, KS, n_qt, n_heads, O,
+                         ldo, t_stride, r16m, opd, ms);
+  };
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_attn_f32<128>, hipFuncAttributeMaxDynamicSharedMemorySize, AttnLds<128>::BYTES);
@@ -702,22 +746,26 @@ void attn_f32(const float* Q, const float* K, const float* V, int64_t ldq, int64
   }
   if (r16 && g_attn_f16_mfma) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
-    if (head_dim == 128) launch_attn_bf3<128, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
-    else launch_attn_bf3<64, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk);
+    if (head_dim == 128) launch_attn_bf3<128, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wka);
+    else launch_attn_bf3<64, 1>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wka);
+    merge();
     return;
   }
   if (bf3 && !r16) {
     FA_REQUIRE(head_dim == 128 || head_dim == 64, "attn_f32: head_dim must be 64 or 128");
-    if (head_dim == 128) launch_attn_bf3<128, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk, opd);
-    else launch_attn_bf3<64, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wk, opd);
+    if (head_dim == 128) launch_attn_bf3<128, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wka, opd);
+    else launch_attn_bf3<64, 3>(grid, s, Q, K, V, ldq, ldk, ldv, O, ldo, t_stride, lens, scale, KS, wka, opd);
+    merge();
     return;
   }
   if (head_dim == 128) {
     hipLaunchKernelGGL(k_attn_f32<128>, grid, dim3(256), AttnLds<128>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, r16, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, r16, wka.part, wka.cnt);
+    merge();
   } else if (head_dim == 64) {
     hipLaunchKernelGGL(k_attn_f32<64>, grid, dim3(256), AttnLds<64>::BYTES, s, Q, K, V, ldq, ldk, ldv, O, ldo,
-                       t_stride, lens, scale, KS, r16, wk.part, wk.cnt);
+                       t_stride, lens, scale, KS, r16, wka.part, wka.cnt);
+    merge();
   } else {
     FA_REQUIRE(false, "attn_f32: head_dim must be 64 or 128");
   }

@@ -1866,6 +1866,12 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
     if (const char* g = getenv("FUNASR_F16_DEEP")) fa::g_gemm_f16_deep = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_256_S")) fa::g_gemm_bf3_256_s = atoi(g) != 0;
     if (const char* g = getenv("FUNASR_BF3_DMA")) fa::g_gemm_bf3_dma = atoi(g) != 0;
+    {
+      const char* g = getenv("FUNASR_ATTN_MERGE");  // encoder attention key splits merged by their own launch
+      fa::g_attn_merge = g ? atoi(g) != 0 : 1;
+      g = getenv("FUNASR_ATTN_MS");
+      fa::g_attn_ms = g ? atoi(g) : 8;
+    }
     {  // the few-tile K splits: every creation takes the environment's setting or the default
       const char* g = getenv("FUNASR_BF3_SK");
       fa::g_gemm_bf3_sk = g ? atoi(g) != 0 : 1;

@@ -865,3 +865,32 @@ def test_encoder_attention_xcd_order_bit_identical(monkeypatch, fp16):
             assert np.array_equal(outs[0][k]["enc"][b], outs[1][k]["enc"][b]), f"call {k} clip {b}: encoder rows"
             assert np.array_equal(outs[0][k]["audio_embd"][b], outs[1][k]["audio_embd"][b]), f"call {k} clip {b}"
 
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_encoder_attention_split_merge_launch_bit_identical(monkeypatch, fp16):
+    """The one-clip encoder attention's key splits merged by their own launch (k_attn_merge, FUNASR_ATTN_MERGE=1, the
+    default: every tile's partials read by 8 blocks) run the last-arriving split's merge arithmetic: one 60 s clip
+    (eight key splits) and a batch of two (no splits) encode bit-identically with the in-launch merge, in the bf16x3 and
+    the fp16 graphs; and with 1 and 32 query slices per merge block."""
+    from fun_asr_gguf import _native
+    from fun_asr_gguf.synthetic import synth_audio
+    clips = [synth_audio(SR * 60, 600 + i) for i in range(2)]
+    outs = []
+    for merge, ms in (("0", "8"), ("1", "8"), ("1", "1"), ("1", "32")):
+        monkeypatch.setenv("FUNASR_ATTN_MERGE", merge)
+        monkeypatch.setenv("FUNASR_ATTN_MS", ms)
+        e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=2,
+                           max_samples=SR * 62)
+        try:
+            e.synthetic_weights(0)
+            e.set_encoder_fp16(fp16)
+            outs.append((e.encode(clips[:1], want_enc=True), e.encode(clips, want_enc=True)))
+        finally:
+            e.close()
+    for v in range(1, len(outs)):
+        for k in range(2):
+            for b in range(len(outs[0][k]["enc"])):
+                assert np.array_equal(outs[0][k]["enc"][b], outs[v][k]["enc"][b]), f"mode {v} call {k} clip {b}: encoder"
+                assert np.array_equal(outs[0][k]["audio_embd"][b], outs[v][k]["audio_embd"][b]), f"mode {v} {k} {b}"
+                assert np.array_equal(outs[0][k]["ctc_ids"][b], outs[v][k]["ctc_ids"][b]), f"mode {v} {k} {b}: CTC"
