@@ -107,12 +107,14 @@ __device__ __forceinline__ void attn_merge_rows(const __amdgpu_buffer_rsrc_t rs,
 #pragma unroll
     for (int k2 = 0; k2 < KSM; ++k2)
       if (k2 < KS) mm = fmaxf(mm, (q & 1) ? ml[k2].z : ml[k2].x);
+    // explicit roundings (no fused multiply-add): the same bits wherever this is inlined (the last split of any
+    // attention kernel, or k_attn_merge), whatever the surrounding code lets the compiler contract
     float ll = 0.f;
 #pragma unroll
     for (int k2 = 0; k2 < KSM; ++k2) {
       const float mk = (q & 1) ? ml[k2].z : ml[k2].x, lk = (q & 1) ? ml[k2].w : ml[k2].y;
-      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(mk - mm);
-      ll += w * lk;
+      const float w = (k2 >= KS || mk == -INFINITY) ? 0.f : __expf(__fsub_rn(mk, mm));
+      ll = __fadd_rn(ll, __fmul_rn(w, lk));
       s_w[k2 * AQ + q] = w;
     }
     s_l[q] = ll;
@@ -124,11 +126,18 @@ __device__ __forceinline__ void attn_merge_rows(const __amdgpu_buffer_rsrc_t rs,
     f4v pv[KSM];
 #pragma unroll
     for (int k2 = 0; k2 < KSM; ++k2) pv[k2] = ld_sc1_f4(rs, (min(k2, KS - 1) * PSZ + q * D + 4 * d4) * 4);
-    f4v acc = s_w[q] * pv[0];
+    const float w0 = s_w[q];
+    float4 a = make_float4(__fmul_rn(w0, pv[0].x), __fmul_rn(w0, pv[0].y), __fmul_rn(w0, pv[0].z), __fmul_rn(w0, pv[0].w));
 #pragma unroll
-    for (int k2 = 1; k2 < KSM; ++k2) acc += s_w[k2 * AQ + q] * pv[k2];
-    const float inv = 1.0f / s_l[q];
-    float4 v = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    for (int k2 = 1; k2 < KSM; ++k2) {
+      const float wk = s_w[k2 * AQ + q];
+      a.x = __fadd_rn(a.x, __fmul_rn(wk, pv[k2].x));
+      a.y = __fadd_rn(a.y, __fmul_rn(wk, pv[k2].y));
+      a.z = __fadd_rn(a.z, __fmul_rn(wk, pv[k2].z));
+      a.w = __fadd_rn(a.w, __fmul_rn(wk, pv[k2].w));
+    }
+    const float inv = __frcp_rn(s_l[q]);
+    float4 v = make_float4(__fmul_rn(a.x, inv), __fmul_rn(a.y, inv), __fmul_rn(a.z, inv), __fmul_rn(a.w, inv));
     if (r16) v = round_f16x4(v);
     store_o4(v, O, op, (row_base + q0 + q) * ldo + head * D + 4 * d4);
   }
