@@ -894,3 +894,32 @@ def test_encoder_attention_split_merge_launch_bit_identical(monkeypatch, fp16):
                 assert np.array_equal(outs[0][k]["enc"][b], outs[v][k]["enc"][b]), f"mode {v} call {k} clip {b}: encoder"
                 assert np.array_equal(outs[0][k]["audio_embd"][b], outs[v][k]["audio_embd"][b]), f"mode {v} {k} {b}"
                 assert np.array_equal(outs[0][k]["ctc_ids"][b], outs[v][k]["ctc_ids"][b]), f"mode {v} {k} {b}: CTC"
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_encoder_ffn2_k_split_matches_unsplit(monkeypatch, fp16):
+    """One clip's ffn2 on 128x128 tiles with K split over 8 blocks and a split-order reduce launch (FUNASR_BF3_SK /
+    FUNASR_F16_SK = 1, the default) against the unsplit K-group tile (= 0): only the f32 summation order of the split
+    differs, so the 60 s clip's encoder rows agree to the encoder's f32 bar (fp16 graph: its own bar, the rounding to
+    fp16 after every op lets one-ulp flips travel), and the split path is deterministic."""
+    from fun_asr_gguf import _native
+    from fun_asr_gguf.synthetic import synth_audio
+    clip = [synth_audio(SR * 60, 700)]
+    outs = []
+    for v in ("0", "1", "1"):
+        monkeypatch.setenv("FUNASR_BF3_SK", v)
+        monkeypatch.setenv("FUNASR_F16_SK", v)
+        e = _native.Engine(synth.ENC_FULL, dict(synth.LLM_TINY, n_ctx=256, max_seqs=1), max_batch=1,
+                           max_samples=SR * 62)
+        try:
+            e.synthetic_weights(0)
+            e.set_encoder_fp16(fp16)
+            outs.append(e.encode(clip, want_enc=True))
+        finally:
+            e.close()
+    assert np.array_equal(outs[1]["enc"][0], outs[2]["enc"][0]), "split path not deterministic"
+    a, b = outs[0]["enc"][0], outs[1]["enc"][0]
+    if fp16:
+        assert _rel(b, a) < 1e-2 and _cos(b, a) > 0.9999
+    else:
+        assert _rel(b, a) < ENC_ATOL and _cos(b, a) > ENC_COS
