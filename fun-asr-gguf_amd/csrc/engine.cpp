@@ -1879,6 +1879,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_gemm_f16_sk = g ? atoi(g) != 0 : 1;
       g = getenv("FUNASR_BF3_SK_KMIN");
       fa::g_gemm_bf3_sk_kmin = g ? std::max(64, atoi(g)) : 2048;
+      g = getenv("FUNASR_EPI_GROUPED");
+      fa::g_gemm_epi_grouped = g ? atoi(g) != 0 : 1;
       g = getenv("FUNASR_BF3_SK_KS");
       fa::g_gemm_bf3_sk_ks = g ? std::max(0, std::min(8, atoi(g))) : 0;
     }
