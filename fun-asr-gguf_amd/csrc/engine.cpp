@@ -1871,6 +1871,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_attn_merge = g ? atoi(g) != 0 : 1;
       g = getenv("FUNASR_ATTN_MS");
       fa::g_attn_ms = g ? atoi(g) : 8;
+      g = getenv("FUNASR_ATTN_KS");  // A/B: encoder attention key splits (0 = automatic, 1-8)
+      fa::g_attn_f32_force_splits = g ? std::max(0, std::min(8, atoi(g))) : 0;
     }
     {  // the few-tile K splits: every creation takes the environment's setting or the default
       const char* g = getenv("FUNASR_BF3_SK");
