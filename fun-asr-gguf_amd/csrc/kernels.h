@@ -33,8 +33,8 @@ struct GemmF32Work {
 };
 extern int g_gemm_f32_split;  // 1 (default): K splits where the tiles leave the chip idle; 0: none
 extern int g_attn_merge;     // encoder attention key splits merged by their own launch (k_attn_merge; default 1)
-extern int g_attn_ms;
-extern int g_attn_f32_force_splits;  // encoder attention key splits (0: automatic; FUNASR_ATTN_KS)        // query slices per tile of k_attn_merge (8)
+extern int g_attn_ms;                 // query slices per tile of k_attn_merge (8)
+extern int g_attn_f32_force_splits;  // encoder attention key splits (0: automatic; FUNASR_ATTN_KS)
 extern int g_attn_f16_mfma;  // 1 (default): fp16-graph attention on f16 MFMAs; 0: exact f32 + fp16 rounding
 extern int g_gemm_f16_b3;  // 1 (default): fp16-graph GEMMs on the bf16x3 kernel family with one f16 plane; 0: k_gemm_f16
 extern int g_lm_tr;  // LM head of 2-8 tokens: transposed row x token reduction (default 1)
