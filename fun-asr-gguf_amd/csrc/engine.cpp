@@ -1289,8 +1289,9 @@ struct Engine {
     // prefill: rows are consecutive positions of one sequence, logits for the last row only.
     const int E = lc.n_embd, H = lc.n_head, KV = lc.n_head_kv, D = lc.head_dim, F = lc.n_ff;
     const int QKV = (H + 2 * KV) * D;
-    // row-local prefill (pf_row_local): every row's arithmetic that of its own sequence's prefill (gemv_q8 row_local,
-    // one key split, no query tiles; never the fused-GEMV path, whose use would depend on the call's row count)
+    // row-local prefill (pf_row_local): every row's arithmetic that of its own sequence's prefill (gemv_q8 row_local;
+    // attention in f16 query tiles that never span two sequences (attn_pf_rl), or one key split per row; never the
+    // fused-GEMV path, whose use would depend on the call's row count)
     const int rl = !decode && pf_row_local ? 1 : 0;
     const bool small = gemv_small(M) && !rl;
     // batched decode: the residual GEMMs (o, down) quantise their new rows times the next RMSNorm weight and leave
