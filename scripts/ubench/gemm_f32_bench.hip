@@ -131,6 +131,7 @@ int main(int argc, char** argv) {
         printf("M=%5d %-9s:", M, sh.name);
         const double t0 = time_graph([&] { run(0, 0); }, 50);
         printf(" default %6.1f us", t0);
+        printf("  64x64x64 pf2 %6.1f us", time_graph([&] { run(13, 0); }, 50));  // force 13: no branch -> the last one
         for (int fv : {11, 12})
         for (int ks : {0, 1, 2, 4, 8}) {
           if (ks && sh.K % (ks * 32)) continue;
