@@ -1478,6 +1478,8 @@ static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t 
 // ascending (as every bf16x3 tile), so KS = 1 is bit-identical to the unsplit tiles.
 int g_gemm_bf3_sk = 1;  // bf16x3 few-tile K >= 2048 launches split over blocks (k_gemm_bf3_sk / launch_gemm_b3_rs; FUNASR_BF3_SK)
 int g_gemm_f16_sk = 1;  // 1: the fp16 graph's few-tile K >= 2048 launches split over blocks (launch_gemm_b3_rs; FUNASR_F16_SK)
+int g_gemm_f16_pf32 = 1;  // the fp16 graph's batched 128-deep launches on the 32-deep prefetch tile instead (FUNASR_F16_PF32)
+int g_gemm_bf3_pf_kb = 0;  // k depth of the 64x64 two-step-prefetch tile: 0 = 32 above G_ROWS_MAX rows, else 64 (FUNASR_BF3_PF_KB)
 int g_gemm_bf3_sk_kmin = 2048;  // smallest K split over blocks (FUNASR_BF3_SK_KMIN; A/B)
 int g_gemm_bf3_sk_ks = 0;  // microbenchmark hook: force the K split (1, 2, 4, 8)
 constexpr int SK_KB = 32;
@@ -1732,7 +1734,8 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
   // fp16 graph, one clip: 128-deep stages (half the k-steps; fp16 planes leave the LDS for them). q|k|v and ffn1 keep
   // their per-element MFMA order (bit-identical to 64-deep stages); ffn2 also splits K in halves. scripts/ubench/
   // gemm_f32_bench kscan, graph-timed: q|k|v 10.1 -> 9.8, ffn1 10.9 -> 10.3, ffn2 14.7 -> 13.8 us (bf16x3: slower)
-  else if (P == 1 && f == 0 && g_gemm_f16_deep && t64 > 256 && t64 <= 1024 && K % 128 == 0)
+  else if (P == 1 && f == 0 && g_gemm_f16_deep && t64 > 256 && t64 <= 1024 && K % 128 == 0 &&
+           !(g_gemm_f16_pf32 && M > G_ROWS_MAX))
     launch_gemm_b3<AL, EPI, 1, 1, 128, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
   else if (P == 1 && f == 0 && g_gemm_f16_deep && t64 < 256 && K >= 2048 && K % 256 == 0)
     launch_gemm_b3<AL, EPI, 1, 1, 128, P == 1 ? 2 : 1, 2, P>(al, w, ldw, M, N, K, epi, s);
@@ -1753,6 +1756,9 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
     if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 2, P>(al, w, ldw, M, N, K, epi, s);
     else launch_gemm_b3<AL, EPI, 1, 1, 64, 2, 1, P>(al, w, ldw, M, N, K, epi, s);
   } else if (f == 5) launch_gemm_b3<AL, EPI, 1, 1, 32, 2, 1, P>(al, w, ldw, M, N, K, epi, s);
+  // 32-deep k-steps for batched launches (batch 6 encode 27.8 -> 25.5 ms), 64 for one clip (8.2 vs 8.3 ms)
+  else if (pf && (g_gemm_bf3_pf_kb == 32 || (g_gemm_bf3_pf_kb == 0 && M > G_ROWS_MAX)))
+    launch_gemm_b3<AL, EPI, 1, 1, 32, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
   else if (pf) launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 2, P>(al, w, ldw, M, N, K, epi, s);
   else launch_gemm_b3<AL, EPI, 1, 1, 64, 1, 1, P>(al, w, ldw, M, N, K, epi, s);
 }
