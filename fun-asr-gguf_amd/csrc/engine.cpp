@@ -1882,6 +1882,8 @@ int fa_engine_create(int32_t device, const fa_encoder_config* enc, const fa_llm_
       fa::g_gemm_f16_sk = g ? atoi(g) != 0 : 1;
       g = getenv("FUNASR_BF3_SK_KMIN");
       fa::g_gemm_bf3_sk_kmin = g ? std::max(64, atoi(g)) : 2048;
+      g = getenv("FUNASR_BF3_BIG");
+      fa::g_gemm_bf3_big = g ? std::max(1, atoi(g)) : 1024;
       g = getenv("FUNASR_F16_PF32");
       fa::g_gemm_f16_pf32 = g ? atoi(g) != 0 : 1;
       g = getenv("FUNASR_BF3_PF_KB");

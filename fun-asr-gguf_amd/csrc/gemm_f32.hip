@@ -1478,6 +1478,7 @@ static void launch_gemm_b3_256d(const ALoadPlanes& al, const WSplit& w, int64_t 
 // ascending (as every bf16x3 tile), so KS = 1 is bit-identical to the unsplit tiles.
 int g_gemm_bf3_sk = 1;  // bf16x3 few-tile K >= 2048 launches split over blocks (k_gemm_bf3_sk / launch_gemm_b3_rs; FUNASR_BF3_SK)
 int g_gemm_f16_sk = 1;  // 1: the fp16 graph's few-tile K >= 2048 launches split over blocks (launch_gemm_b3_rs; FUNASR_F16_SK)
+int g_gemm_bf3_big = 1024;  // 128x128 register-staged tiles from this many 128x128 tiles (FUNASR_BF3_BIG; batch 6: 64x64 faster)
 int g_gemm_f16_pf32 = 1;  // the fp16 graph's batched 128-deep launches on the 32-deep prefetch tile instead (FUNASR_F16_PF32)
 int g_gemm_bf3_pf_kb = 0;  // k depth of the 64x64 two-step-prefetch tile: 0 = 32 above G_ROWS_MAX rows, else 64 (FUNASR_BF3_PF_KB)
 int g_gemm_bf3_sk_kmin = 2048;  // smallest K split over blocks (FUNASR_BF3_SK_KMIN; A/B)
@@ -1721,7 +1722,7 @@ static void run_gemm_b3(const AL& al, const WSplit& w, int64_t ldw, int M, int N
       if ((f == 12 || rs) && launch_gemm_b3_rs<AL, EPI, P>(al, w, ldw, M, N, K, epi, s, wk)) return;
     }
   }
-  const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= 512;
+  const bool big = f ? f == 2 : (int64_t)cdiv(M, 128) * cdiv(N, 128) >= g_gemm_bf3_big;
   const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   const bool pf = g_gemm_bf3_pf > 1;
   // 256x256 tiles while they still give most CUs a block (f == 6 forces them)

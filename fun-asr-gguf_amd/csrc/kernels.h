@@ -47,6 +47,7 @@ extern int g_gemm_bf3_dma;    // planes-A 256x256 tiles staged by LDS-DMA (k_gem
 extern int g_gemm_bf3_sk;     // bf16x3 few-tile K >= 2048 linear GEMMs: 128x128 tiles, K split over blocks (default 1)
 extern int g_gemm_f16_sk;     // fp16 graph: the same split on the register-staged 128x128 tile (default 1)
 extern int g_gemm_epi_grouped;  // one-clip encoder GEMMs on the four-row grouped epilogue (default 1)
+extern int g_gemm_bf3_big;  // launches of at least this many 128x128 tiles take them (1024)
 extern int g_gemm_f16_pf32;   // fp16 batched 128-deep launches on the 32-deep prefetch tile (default 1)
 extern int g_gemm_bf3_pf_kb;  // k depth of the 64x64 two-step-prefetch tile (0: 32 for batched launches, 64 for one clip)
 extern int g_gemm_bf3_sk_kmin;  // smallest K of a split few-tile launch (2048: one clip's ffn2)
